@@ -1,0 +1,180 @@
+#!/usr/bin/env python3
+"""Benchmark: env steps/s (whole node) for the batched pick-and-place hot path on MI355X.
+
+Workload (BASELINE.json configs[2], "C3"): 4096 parallel envs per GPU, tasks='all' (9 combos),
+randomize_objects=True, env i seeded SeedSequence(42).spawn(N)[i].generate_state(1)[0]
+(scripts/generate_dataset.py:263-268) using the GLOBAL env index (results independent of
+sharding), FSM-expert abs_pos actions computed on device (pick_and_place.py plan(16)),
+same-step autoreset.  One "step" = one PickPlaceGymEnv.step for every env: decode -> 16 x
+(DLS IK + mj_step) -> mj_forward (position stage) -> staged reward -> 85-float obs.
+
+Multi-GPU: one process per GPU (torchrun), weak scaling (4096 envs per rank), no data-path
+collective; an all_reduce(MAX) of the elapsed time and an all_gather of per-rank stats for
+logging only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def algorithmic_bytes_per_substep(nefc: float) -> float:
+    """B_state + B_efc per env per substep (fp32 words)."""
+    return 2 * 4 * (30 + 27 + 27 + 8) + 2 * 4 * nefc * (27 + 4)
+
+
+def cpu_baseline(seconds: float = 12.0) -> dict:
+    """Oracle (fp64 C restatement, single thread) on a bounded sample of the same workload."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle_py as O
+    from mujoco_manip_amd.constants import ALL_TASKS, BINS, OBJECTS
+
+    O.build()
+    steps = 0
+    t0 = time.perf_counter()
+    ep = 0
+    while time.perf_counter() - t0 < seconds:
+        e = O.OracleEnv(action_mode="abs_pos", reward_type="staged", randomize_objects=True,
+                        tasks=[(OBJECTS.index(o), BINS.index(b)) for o, b in ALL_TASKS])
+        e.reset(seed=O.episode_seed(42, ep))
+        o, b = e.task()
+        e.fsm_init([(o, b)])
+        for _ in range(400):
+            st = e.fsm_plan(16)
+            if st == 10:
+                break
+            f = e.fsm_get()
+            tgt = f["target"] if f["state"] != 0 else e.body(9)[0]
+            e.step(np.array([*tgt, float(f["gripper_open"])], np.float32))
+            steps += 1
+            if time.perf_counter() - t0 > seconds:
+                break
+        ep += 1
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "env steps/s", "cores": 1, "kind": "port",
+            "sample": f"{steps} env steps ({ep} FSM-expert episodes, C3 settings) in {dt:.1f}s, 1 thread, "
+                      f"oracle/ fp64 C restatement (MuJoCo absent on the box)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=60)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--envs-per-gpu", type=int, default=4096)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl")
+    dev = torch.device(f"cuda:{local_rank}")
+    torch.cuda.set_device(dev)
+
+    from mujoco_manip_amd import _lib
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    N = args.envs_per_gpu
+    env = PickPlaceVecEnv(N, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
+                          autoreset=True, device=local_rank)
+    seeds = [_lib.episode_seed(42, rank * N + i) for i in range(N)]
+    env.reset(seed=seeds)
+
+    # warmup
+    env.rollout_expert(args.warmup)
+    torch.cuda.synchronize()
+    env.clear_stats()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    env.rollout_expert(args.steps)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    solver = env.solver_stats()
+    env_steps = args.steps * N * world
+    value = env_steps / elapsed
+    ms_per_step = 1000.0 * elapsed / args.steps
+
+    # dominant kernel (mmx_substep_kernel): live per-launch duration with HIP events on the
+    # sim's stream, same state distribution (continues the rollout)
+    stream = torch.cuda.current_stream(dev)
+    n_launch = 32
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    env.clear_stats()
+    ev0.record(stream)
+    env.sim.physics_step(n_launch, with_ik=True)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    kern_ms = ev0.elapsed_time(ev1) / n_launch
+    kstats = env.solver_stats()
+    bytes_per_launch = algorithmic_bytes_per_substep(kstats["mean_nefc"]) * N
+    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+
+    stats_all = None
+    if dist:
+        loc = torch.tensor([solver["mean_nefc"], solver["mean_pgs_iter"], value / world], device=dev)
+        gathered = [torch.zeros_like(loc) for _ in range(world)]
+        dist.all_gather(gathered, loc)
+        stats_all = [g.tolist() for g in gathered]
+
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            cpu = cpu_baseline(args.cpu_seconds)
+        traffic = None
+        tf = os.path.join(REPO, "profiles", "pmc_traffic.json")
+        if os.path.exists(tf):
+            try:
+                traffic = json.load(open(tf)).get("bytes_per_launch")
+            except Exception:
+                traffic = None
+        line = {
+            "metric": "env steps/sec (whole node) at 4096 parallel envs; 1/2/4/8 MI355X scaling",
+            "value": value, "unit": "env steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+            "dtype": "f32", "data": "synthetic (seeded randomized scenes, FSM-expert actions)",
+            "config": {"workload": "C3: PickPlaceGymEnv.step x 4096 envs/GPU, tasks=all, randomize_objects, "
+                                   "seed=42 episode seeds, staged reward, FSM expert abs_pos, autoreset",
+                       "envs_per_gpu": N, "global_envs": N * world, "substeps": 16,
+                       "parallelism": f"env-batch dp{world}"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "kernel": "mmx_substep_kernel", "kernel_ms": kern_ms,
+                         "algorithmic_bytes_per_launch": bytes_per_launch, "mean_nefc": kstats["mean_nefc"]},
+            "cpu_baseline": cpu,
+            "solver": solver,
+        }
+        if stats_all:
+            line["per_rank"] = stats_all
+        print(json.dumps(line), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,129 @@
+/* mmx_api.h — C-ABI of the MI355X batched pick-and-place simulator (libmmx.so).
+ *
+ * The reference path sits behind the Gymnasium Env API of PickPlaceGymEnv
+ * (mujoco_manip/gym_env.py:39-602) and, below it, the MuJoCo C API reached through
+ * pybind11 (mujoco.mj_step env.py:121, mj_forward gym_env.py:560, mj_jac controller.py:101).
+ * This header is the boundary a host binding (ctypes here; cgo/JNI/N-API elsewhere) binds
+ * to.  Plain C: no C++ or torch types, plain pointers and sizes.
+ *
+ * Conventions
+ *  - every function returns 0 on success or a negative MMX_E* code and never aborts;
+ *    mmx_last_error() gives a message;
+ *  - device buffers are fp32/int32 structure-of-arrays, field-major with the env index
+ *    fastest: element (field f, env i) is at ptr[f * num_envs + i];
+ *  - sim-owned buffers returned by mmx_get_buffers stay valid until mmx_destroy;
+ *  - all launches are asynchronous on the sim's stream (cfg.stream, or the null stream);
+ *  - one sim per host thread at a time (not re-entrant); per-env faults go to the
+ *    env_error buffer, never to return codes.
+ */
+#ifndef MMX_API_H
+#define MMX_API_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MMX_OK 0
+#define MMX_EINVAL (-1)   /* bad argument (ValueError in the reference) */
+#define MMX_EDEVICE (-2)  /* HIP runtime error */
+#define MMX_ENOMEM (-3)   /* device allocation failed */
+
+/* action modes, gym_env.py:30-36 */
+enum { MMX_ACTION_ABS_POS = 0, MMX_ACTION_EE_POS_QUAT_G = 1, MMX_ACTION_EE_POS_ROT6D_G = 2,
+       MMX_ACTION_EE_POS_QUAT_G_REL = 3, MMX_ACTION_EE_POS_ROT6D_G_REL = 4 };
+/* reward types, gym_env.py:86 */
+enum { MMX_REWARD_DENSE = 0, MMX_REWARD_SPARSE = 1, MMX_REWARD_STAGED = 2 };
+
+typedef struct mmx_sim mmx_sim;
+
+/* Constructor arguments of PickPlaceGymEnv (gym_env.py:62-75) plus batching knobs. */
+typedef struct {
+  int32_t num_envs;
+  int32_t device;               /* HIP device ordinal */
+  int32_t action_mode;          /* MMX_ACTION_* */
+  int32_t reward_type;          /* MMX_REWARD_* */
+  int32_t max_episode_steps;    /* truncation limit (constants.py:27) */
+  int32_t randomize_objects;    /* randomization.py on reset */
+  float spawn_x_range[2];
+  float spawn_y_range[2];
+  int32_t n_tasks;              /* task pool (constants.py:11-25), objects/bins 0=red 1=green 2=blue */
+  int8_t task_obj[9];
+  int8_t task_bin[9];
+  int32_t fixed_task_obj;       /* -1: sample from the pool (gym_env.py:511-517) */
+  int32_t fixed_task_bin;
+  int32_t image_size;           /* keypoint normalisation only; no rendering in this build */
+  int32_t autoreset;            /* same-step autoreset on terminated/truncated/FSM done */
+  int32_t solver_iterations;    /* PGS sweeps cap */
+  float solver_tolerance;       /* PGS relative force-change tolerance */
+  void* stream;                 /* hipStream_t, NULL = default stream */
+} mmx_config;
+
+/* Field-major device buffers (sim-owned). */
+typedef struct {
+  int32_t num_envs;
+  float* qpos;               /* [30][N] */
+  float* qvel;               /* [27][N] */
+  float* ctrl;               /* [8][N]  */
+  float* qacc_warmstart;     /* [27][N] */
+  float* obs;                /* [85][N] numeric observation, gym_env.py:295-339 order */
+  float* reward;             /* [N] */
+  int32_t* done;             /* [3][N] terminated, truncated, success */
+  float* reward_components;  /* [6][N] staged breakdown (gym_env.py:568-573) */
+  int32_t* episode_i;        /* [14][N] obj, bin, step_count, flags, fsm_state, fsm_task_index,
+                                fsm_settle, fsm_gripper_open, fsm_has_target, env_error, ncon, nefc,
+                                episodes, rng_has32 */
+  float* episode_f;          /* [28][N] T_init(12), hwm(5), target_kp(4), fsm_target(3), transit(3), return */
+  float* kin;                /* [54][N] hand pos/mat + arm joint axes/anchors of the last position stage */
+  float* stats;              /* [5][N] sum nefc, sum ncon, sum PGS sweeps, substeps, max residual */
+  float* contacts;           /* [40][12][N] dist, pos3, normal3, mu3, dim, geom1, geom2 (last substep) */
+} mmx_buffers;
+
+void mmx_config_default(mmx_config* cfg);
+
+/* PickPlaceGymEnv.__init__ (gym_env.py:62-208) for num_envs environments. */
+int mmx_create(const mmx_config* cfg, mmx_sim** out);
+void mmx_destroy(mmx_sim* sim);
+const char* mmx_last_error(const mmx_sim* sim);
+
+/* PickPlaceGymEnv.reset (gym_env.py:477-534) for the envs selected by env_mask (host,
+ * N bytes, NULL = all).  seeds: host, N entries, or NULL to continue each env's stream
+ * (gym semantics: reset(seed=None)).  seed_given: host, N bytes, NULL = all seeds valid.
+ * task_override: host, N entries of (obj << 4 | bin), -1 = none (options["task"]). */
+int mmx_reset(mmx_sim* sim, const uint64_t* seeds, const uint8_t* seed_given, const int32_t* task_override,
+              const uint8_t* env_mask);
+
+/* PickPlaceGymEnv.step (gym_env.py:536-581): action_dev is a device pointer to [N][action_dim]
+ * fp32 (row-major, env-major).  Runs decode -> 16 x (IK + mj_step) -> mj_forward -> reward -> obs. */
+int mmx_step(mmx_sim* sim, const float* action_dev, int32_t action_dim);
+
+/* PickAndPlaceTask.plan(n_steps) (pick_and_place.py:167-277) for every env; writes the
+ * abs_pos action [N][4] = (target_xyz, gripper_val) to action_dev_out (may be NULL). */
+int mmx_expert_plan(mmx_sim* sim, int32_t n_steps, float* action_dev_out);
+
+/* Expert rollout driver (scripts/generate_dataset.py:140-196): n_env_steps x (plan(16) ->
+ * step(abs_pos)); envs whose FSM is done auto-reset when cfg.autoreset is set.
+ * Requires action_mode == MMX_ACTION_ABS_POS. */
+int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps);
+
+/* Physics-level entry points (parity harnesses): n x mujoco.mj_step with the current ctrl
+ * (env.py:119-121), optionally preceded by IKController.compute toward the decoded target
+ * each substep; and the mj_forward position stage (kinematics + IK cache). */
+int mmx_physics_step(mmx_sim* sim, int32_t n, int32_t with_ik);
+int mmx_forward(mmx_sim* sim);
+
+int mmx_get_buffers(mmx_sim* sim, mmx_buffers* out);
+int mmx_synchronize(mmx_sim* sim);
+
+/* Host copies of the core state (host arrays of [field][N] fp32). NULL skips a field. */
+int mmx_get_state(mmx_sim* sim, float* qpos, float* qvel, float* ctrl, float* qacc_warmstart);
+int mmx_set_state(mmx_sim* sim, const float* qpos, const float* qvel, const float* ctrl, const float* qacc_warmstart);
+
+/* Host helper: SeedSequence(root).spawn(n)[index].generate_state(1)[0]
+ * (scripts/generate_dataset.py:263-268). */
+uint32_t mmx_episode_seed(uint64_t root_seed, int32_t index);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,228 @@
+"""ctypes binding of libmmx.so (include/mmx_api.h).
+
+This is the reference-side binding a maintainer would add: the reference is Python, so the
+binding to the C-ABI is ctypes.  Device buffers are exchanged as raw pointers; torch is used
+only to own action tensors and to view sim-owned buffers (``__cuda_array_interface__``).
+The product path fails loudly when the HIP library or the GPU is missing: there is no CPU
+fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import _build
+
+NQ, NV, NU, NOBS = 30, 27, 8, 85
+MAXCON, CON_F = 40, 12
+EPI_N, EPF_N, KIN_N, STAT_N = 14, 28, 54, 5
+EPI_FIELDS = ("obj", "bin", "step_count", "flags", "fsm_state", "fsm_task_index", "fsm_settle", "fsm_gripper_open",
+              "fsm_has_target", "env_error", "ncon", "nefc", "episodes", "rng_has32")
+STAT_FIELDS = ("sum_nefc", "sum_ncon", "sum_pgs_iter", "substeps", "max_resid")
+ACTION_MODES = ("abs_pos", "ee_pos_quat_g", "ee_pos_rot6d_g", "ee_pos_quat_g_rel", "ee_pos_rot6d_g_rel")
+ACTION_DIMS = (4, 8, 10, 8, 10)
+REWARD_TYPES = ("dense", "sparse", "staged")
+
+
+class MMXConfig(C.Structure):
+    _fields_ = [
+        ("num_envs", C.c_int32), ("device", C.c_int32), ("action_mode", C.c_int32), ("reward_type", C.c_int32),
+        ("max_episode_steps", C.c_int32), ("randomize_objects", C.c_int32),
+        ("spawn_x_range", C.c_float * 2), ("spawn_y_range", C.c_float * 2),
+        ("n_tasks", C.c_int32), ("task_obj", C.c_int8 * 9), ("task_bin", C.c_int8 * 9),
+        ("fixed_task_obj", C.c_int32), ("fixed_task_bin", C.c_int32), ("image_size", C.c_int32),
+        ("autoreset", C.c_int32), ("solver_iterations", C.c_int32), ("solver_tolerance", C.c_float),
+        ("stream", C.c_void_p),
+    ]
+
+
+class MMXBuffers(C.Structure):
+    _fields_ = [
+        ("num_envs", C.c_int32), ("qpos", C.c_void_p), ("qvel", C.c_void_p), ("ctrl", C.c_void_p),
+        ("qacc_warmstart", C.c_void_p), ("obs", C.c_void_p), ("reward", C.c_void_p), ("done", C.c_void_p),
+        ("reward_components", C.c_void_p), ("episode_i", C.c_void_p), ("episode_f", C.c_void_p),
+        ("kin", C.c_void_p), ("stats", C.c_void_p), ("contacts", C.c_void_p),
+    ]
+
+
+EXPORTED = ("mmx_config_default", "mmx_create", "mmx_destroy", "mmx_last_error", "mmx_reset", "mmx_step",
+            "mmx_expert_plan", "mmx_rollout_expert", "mmx_physics_step", "mmx_forward", "mmx_get_buffers",
+            "mmx_synchronize", "mmx_get_state", "mmx_set_state", "mmx_episode_seed")
+
+_lib = None
+
+
+def load(build_if_missing: bool = True):
+    """Load libmmx.so (built in-tree by _build.build)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_build.LIB):
+        if not build_if_missing:
+            raise RuntimeError(f"libmmx.so missing at {_build.LIB}; run __graft_entry__.build()")
+        _build.build()
+    L = C.CDLL(_build.LIB)
+    vp, u8p, i32p, u64p, fp = C.c_void_p, C.POINTER(C.c_uint8), C.POINTER(C.c_int32), C.POINTER(C.c_uint64), C.POINTER(C.c_float)
+    L.mmx_config_default.argtypes = [C.POINTER(MMXConfig)]
+    L.mmx_create.argtypes = [C.POINTER(MMXConfig), C.POINTER(vp)]
+    L.mmx_destroy.argtypes = [vp]
+    L.mmx_last_error.restype = C.c_char_p
+    L.mmx_last_error.argtypes = [vp]
+    L.mmx_reset.argtypes = [vp, u64p, u8p, i32p, u8p]
+    L.mmx_step.argtypes = [vp, vp, C.c_int32]
+    L.mmx_expert_plan.argtypes = [vp, C.c_int32, vp]
+    L.mmx_rollout_expert.argtypes = [vp, C.c_int32]
+    L.mmx_physics_step.argtypes = [vp, C.c_int32, C.c_int32]
+    L.mmx_forward.argtypes = [vp]
+    L.mmx_get_buffers.argtypes = [vp, C.POINTER(MMXBuffers)]
+    L.mmx_synchronize.argtypes = [vp]
+    L.mmx_get_state.argtypes = [vp, fp, fp, fp, fp]
+    L.mmx_set_state.argtypes = [vp, fp, fp, fp, fp]
+    L.mmx_episode_seed.restype = C.c_uint32
+    L.mmx_episode_seed.argtypes = [C.c_uint64, C.c_int32]
+    for name in ("mmx_create", "mmx_reset", "mmx_step", "mmx_expert_plan", "mmx_rollout_expert", "mmx_physics_step",
+                 "mmx_forward", "mmx_get_buffers", "mmx_synchronize", "mmx_get_state", "mmx_set_state"):
+        getattr(L, name).restype = C.c_int
+    _lib = L
+    return L
+
+
+def episode_seed(root: int, index: int) -> int:
+    """SeedSequence(root).spawn(n)[index].generate_state(1)[0] (generate_dataset.py:263-268)."""
+    return int(load().mmx_episode_seed(root, index))
+
+
+class _DevArray:
+    """Minimal __cuda_array_interface__ exporter for a sim-owned device buffer."""
+
+    def __init__(self, ptr: int, shape, typestr: str, owner):
+        self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": typestr, "data": (int(ptr), False),
+                                         "version": 2, "strides": None}
+        self._owner = owner
+
+
+def _fptr(a):
+    return None if a is None else a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+class Sim:
+    """Owner of one mmx_sim (a batch of num_envs environments on one GPU)."""
+
+    def __init__(self, num_envs: int, *, action_mode: str = "ee_pos_quat_g_rel", reward_type: str = "dense",
+                 max_episode_steps: int = 500, randomize_objects: bool = False,
+                 spawn_x_range=(-0.20, 0.20), spawn_y_range=(0.30, 0.45), task_pool=None, fixed_task=None,
+                 image_size: int = 224, autoreset: bool = False, solver_iterations: int = 100,
+                 solver_tolerance: float = 1e-5, device: int = 0, stream: int | None = None):
+        if action_mode not in ACTION_MODES:
+            raise ValueError(f"action_mode must be one of {ACTION_MODES}, got '{action_mode}'")
+        if reward_type not in REWARD_TYPES:
+            raise ValueError(f"reward_type must be one of {REWARD_TYPES}, got '{reward_type}'")
+        self.L = load()
+        cfg = MMXConfig()
+        self.L.mmx_config_default(C.byref(cfg))
+        cfg.num_envs = int(num_envs)
+        cfg.device = int(device)
+        cfg.action_mode = ACTION_MODES.index(action_mode)
+        cfg.reward_type = REWARD_TYPES.index(reward_type)
+        cfg.max_episode_steps = int(max_episode_steps)
+        cfg.randomize_objects = int(bool(randomize_objects))
+        cfg.spawn_x_range[0], cfg.spawn_x_range[1] = spawn_x_range
+        cfg.spawn_y_range[0], cfg.spawn_y_range[1] = spawn_y_range
+        if task_pool is not None:
+            cfg.n_tasks = len(task_pool)
+            for k, (o, b) in enumerate(task_pool):
+                cfg.task_obj[k], cfg.task_bin[k] = o, b
+        if fixed_task is not None:
+            cfg.fixed_task_obj, cfg.fixed_task_bin = fixed_task
+        cfg.image_size = int(image_size)
+        cfg.autoreset = int(bool(autoreset))
+        cfg.solver_iterations = int(solver_iterations)
+        cfg.solver_tolerance = float(solver_tolerance)
+        cfg.stream = stream
+        self.cfg = cfg
+        self.num_envs = int(num_envs)
+        self.action_dim = ACTION_DIMS[cfg.action_mode]
+        ptr = C.c_void_p()
+        rc = self.L.mmx_create(C.byref(cfg), C.byref(ptr))
+        if rc != 0 or not ptr.value:
+            raise RuntimeError(f"mmx_create failed ({rc}): no usable MI355X / HIP device?")
+        self.ptr = ptr
+        self.buffers = MMXBuffers()
+        self._check(self.L.mmx_get_buffers(self.ptr, C.byref(self.buffers)), "mmx_get_buffers")
+
+    def _check(self, rc, what):
+        if rc != 0:
+            raise RuntimeError(f"{what} failed ({rc}): {self.L.mmx_last_error(self.ptr).decode()}")
+
+    def close(self):
+        if getattr(self, "ptr", None) is not None and self.ptr.value:
+            self.L.mmx_destroy(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- C-ABI calls
+    def reset(self, seeds=None, task_override=None, env_mask=None):
+        N = self.num_envs
+        u64p, u8p, i32p = C.POINTER(C.c_uint64), C.POINTER(C.c_uint8), C.POINTER(C.c_int32)
+        s = g = t = m = None
+        if seeds is not None:
+            arr = np.zeros(N, np.uint64)
+            given = np.zeros(N, np.uint8)
+            for k, v in enumerate(seeds):
+                if v is not None:
+                    arr[k] = int(v)
+                    given[k] = 1
+            self._seed_arr, self._given_arr = arr, given
+            s, g = arr.ctypes.data_as(u64p), given.ctypes.data_as(u8p)
+        if task_override is not None:
+            self._task_arr = np.ascontiguousarray(task_override, np.int32)
+            t = self._task_arr.ctypes.data_as(i32p)
+        if env_mask is not None:
+            self._mask_arr = np.ascontiguousarray(env_mask, np.uint8)
+            m = self._mask_arr.ctypes.data_as(u8p)
+        self._check(self.L.mmx_reset(self.ptr, s, g, t, m), "mmx_reset")
+
+    def step(self, action_ptr: int, action_dim: int):
+        self._check(self.L.mmx_step(self.ptr, C.c_void_p(action_ptr), action_dim), "mmx_step")
+
+    def expert_plan(self, n_steps: int, action_ptr: int | None):
+        self._check(self.L.mmx_expert_plan(self.ptr, n_steps, C.c_void_p(action_ptr) if action_ptr else None),
+                    "mmx_expert_plan")
+
+    def rollout_expert(self, n_env_steps: int):
+        self._check(self.L.mmx_rollout_expert(self.ptr, n_env_steps), "mmx_rollout_expert")
+
+    def physics_step(self, n: int = 1, with_ik: bool = False):
+        self._check(self.L.mmx_physics_step(self.ptr, n, int(with_ik)), "mmx_physics_step")
+
+    def forward(self):
+        self._check(self.L.mmx_forward(self.ptr), "mmx_forward")
+
+    def synchronize(self):
+        self._check(self.L.mmx_synchronize(self.ptr), "mmx_synchronize")
+
+    def get_state(self):
+        N = self.num_envs
+        qpos, qvel = np.zeros((NQ, N), np.float32), np.zeros((NV, N), np.float32)
+        ctrl, ws = np.zeros((NU, N), np.float32), np.zeros((NV, N), np.float32)
+        self._check(self.L.mmx_get_state(self.ptr, _fptr(qpos), _fptr(qvel), _fptr(ctrl), _fptr(ws)), "mmx_get_state")
+        return qpos, qvel, ctrl, ws
+
+    def set_state(self, qpos=None, qvel=None, ctrl=None, qacc_ws=None):
+        arrs = [None if a is None else np.ascontiguousarray(a, np.float32) for a in (qpos, qvel, ctrl, qacc_ws)]
+        self._check(self.L.mmx_set_state(self.ptr, *[_fptr(a) for a in arrs]), "mmx_set_state")
+
+    # ---- zero-copy torch views of sim-owned buffers ([field][N])
+    def view(self, name: str, nfield: int, dtype: str = "<f4"):
+        import torch
+
+        ptr = getattr(self.buffers, name)
+        shape = (nfield, self.num_envs) if nfield > 1 else (self.num_envs,)
+        return torch.as_tensor(_DevArray(ptr, shape, dtype, self), device=f"cuda:{self.cfg.device}")

@@ -1,0 +1,363 @@
+// C-ABI implementation (include/mmx_api.h): device allocation, host-side seeding, launches.
+//
+// Host-side seeding restates numpy's SeedSequence / PCG64 initialisation (the reference seeds
+// every episode through gymnasium: Generator(PCG64(SeedSequence(seed))), gym_env.py:491) so the
+// device PCG64 streams are bit-identical to the reference's np_random streams.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../../include/mmx_api.h"
+#include "mmx_state.h"
+
+extern "C" hipError_t mmx_launch_reset(const MMXState* S, const unsigned char* mask, const int* task, hipStream_t st);
+extern "C" hipError_t mmx_launch_step(const MMXState* S, const float* action, int adim, int expert_autoreset,
+                                      hipStream_t st);
+extern "C" hipError_t mmx_launch_expert(const MMXState* S, int n, float* action, hipStream_t st);
+extern "C" hipError_t mmx_launch_physics(const MMXState* S, int n, int with_ik, hipStream_t st);
+extern "C" hipError_t mmx_launch_forward(const MMXState* S, hipStream_t st);
+
+struct mmx_sim {
+  MMXState S;
+  mmx_config cfg;
+  hipStream_t stream;
+  std::string err;
+  std::vector<void*> allocs;
+  float* expert_action;  // [N][4]
+  unsigned char* d_mask;
+  int* d_task;
+};
+
+namespace {
+
+// ---------------------------------------------------------------- numpy SeedSequence / PCG64
+constexpr uint32_t kInitA = 0x43b0d7e5u, kMultA = 0x931e8875u, kInitB = 0x8b51f9ddu, kMultB = 0x58f38dedu;
+constexpr uint32_t kMixL = 0xca01f9ddu, kMixR = 0x4973f715u;
+
+uint32_t hashmix(uint32_t v, uint32_t& hc) {
+  v ^= hc;
+  hc *= kMultA;
+  v *= hc;
+  v ^= v >> 16;
+  return v;
+}
+uint32_t mix(uint32_t x, uint32_t y) {
+  uint32_t r = kMixL * x - kMixR * y;
+  return r ^ (r >> 16);
+}
+std::vector<uint32_t> seed_words(uint64_t s) {
+  std::vector<uint32_t> w{static_cast<uint32_t>(s)};
+  if (s >> 32) w.push_back(static_cast<uint32_t>(s >> 32));
+  return w;
+}
+// SeedSequence(entropy, spawn_key).generate_state(n_out, uint32)
+std::vector<uint32_t> seedseq(std::vector<uint32_t> ent, const std::vector<uint32_t>& spawn, int n_out) {
+  if (!spawn.empty() && ent.size() < 4) ent.resize(4, 0u);
+  ent.insert(ent.end(), spawn.begin(), spawn.end());
+  uint32_t pool[4];
+  uint32_t hc = kInitA;
+  for (int i = 0; i < 4; i++) pool[i] = hashmix(i < static_cast<int>(ent.size()) ? ent[i] : 0u, hc);
+  for (int s = 0; s < 4; s++)
+    for (int d = 0; d < 4; d++)
+      if (s != d) pool[d] = mix(pool[d], hashmix(pool[s], hc));
+  for (size_t s = 4; s < ent.size(); s++)
+    for (int d = 0; d < 4; d++) pool[d] = mix(pool[d], hashmix(ent[s], hc));
+  std::vector<uint32_t> out(n_out);
+  uint32_t hb = kInitB;
+  for (int i = 0; i < n_out; i++) {
+    uint32_t v = pool[i % 4];
+    v ^= hb;
+    hb *= kMultB;
+    v *= hb;
+    v ^= v >> 16;
+    out[i] = v;
+  }
+  return out;
+}
+
+using u128 = unsigned __int128;
+const u128 kPcgMult = (static_cast<u128>(0x2360ED051FC65DA4ull) << 64) | 0x4385DF649FCCF645ull;
+
+// PCG64(SeedSequence(seed)) initial (state, inc)
+void pcg64_seed(uint64_t seed, uint64_t out[4]) {
+  std::vector<uint32_t> st = seedseq(seed_words(seed), {}, 8);
+  uint64_t v[4];
+  for (int i = 0; i < 4; i++) v[i] = static_cast<uint64_t>(st[2 * i]) | (static_cast<uint64_t>(st[2 * i + 1]) << 32);
+  u128 initstate = (static_cast<u128>(v[0]) << 64) | v[1];
+  u128 initseq = (static_cast<u128>(v[2]) << 64) | v[3];
+  u128 inc = (initseq << 1) | 1;
+  u128 s = 0;
+  s = s * kPcgMult + inc;
+  s += initstate;
+  s = s * kPcgMult + inc;
+  out[0] = static_cast<uint64_t>(s >> 64);
+  out[1] = static_cast<uint64_t>(s);
+  out[2] = static_cast<uint64_t>(inc >> 64);
+  out[3] = static_cast<uint64_t>(inc);
+}
+
+int fail(mmx_sim* sim, int code, const std::string& msg) {
+  if (sim) sim->err = msg;
+  return code;
+}
+int hip_check(mmx_sim* sim, hipError_t e, const char* what) {
+  if (e == hipSuccess) return MMX_OK;
+  return fail(sim, MMX_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <typename T>
+T* dalloc(mmx_sim* sim, size_t count) {
+  void* p = nullptr;
+  if (hipMalloc(&p, count * sizeof(T)) != hipSuccess) return nullptr;
+  hipMemset(p, 0, count * sizeof(T));
+  sim->allocs.push_back(p);
+  return static_cast<T*>(p);
+}
+
+}  // namespace
+
+extern "C" {
+
+void mmx_config_default(mmx_config* c) {
+  std::memset(c, 0, sizeof(*c));
+  c->num_envs = 1;
+  c->action_mode = MMX_ACTION_EE_POS_QUAT_G_REL;  // gym_env.py:67
+  c->reward_type = MMX_REWARD_DENSE;              // gym_env.py:68
+  c->max_episode_steps = 500;                     // constants.py:27
+  c->spawn_x_range[0] = -0.20f;
+  c->spawn_x_range[1] = 0.20f;
+  c->spawn_y_range[0] = 0.30f;
+  c->spawn_y_range[1] = 0.45f;
+  c->n_tasks = 9;  // "all" (constants.py:19)
+  for (int k = 0; k < 9; k++) {
+    c->task_obj[k] = static_cast<int8_t>(k / 3);
+    c->task_bin[k] = static_cast<int8_t>(k % 3);
+  }
+  c->fixed_task_obj = -1;
+  c->fixed_task_bin = -1;
+  c->image_size = 224;  // constants.py:23
+  c->solver_iterations = 100;
+  c->solver_tolerance = 1e-5f;
+}
+
+int mmx_create(const mmx_config* cfg, mmx_sim** out) {
+  if (!cfg || !out) return MMX_EINVAL;
+  *out = nullptr;
+  if (cfg->num_envs <= 0 || cfg->action_mode < 0 || cfg->action_mode > 4 || cfg->reward_type < 0 ||
+      cfg->reward_type > 2 || cfg->n_tasks < 1 || cfg->n_tasks > 9)
+    return MMX_EINVAL;
+  for (int k = 0; k < cfg->n_tasks; k++)
+    if (cfg->task_obj[k] < 0 || cfg->task_obj[k] > 2 || cfg->task_bin[k] < 0 || cfg->task_bin[k] > 2) return MMX_EINVAL;
+  mmx_sim* sim = new mmx_sim();
+  sim->cfg = *cfg;
+  if (hipSetDevice(cfg->device) != hipSuccess) {
+    delete sim;
+    return MMX_EDEVICE;
+  }
+  sim->stream = static_cast<hipStream_t>(cfg->stream);
+  const int N = cfg->num_envs;
+  MMXState& S = sim->S;
+  std::memset(&S, 0, sizeof(S));
+  S.N = N;
+  S.action_mode = cfg->action_mode;
+  S.reward_type = cfg->reward_type;
+  S.max_episode_steps = cfg->max_episode_steps;
+  S.randomize = cfg->randomize_objects;
+  S.image_size = cfg->image_size;
+  S.autoreset = cfg->autoreset;
+  S.spawn_x0 = cfg->spawn_x_range[0];
+  S.spawn_x1 = cfg->spawn_x_range[1];
+  S.spawn_y0 = cfg->spawn_y_range[0];
+  S.spawn_y1 = cfg->spawn_y_range[1];
+  S.ntask = cfg->n_tasks;
+  for (int k = 0; k < 9; k++) {
+    S.task_obj[k] = k < cfg->n_tasks ? cfg->task_obj[k] : 0;
+    S.task_bin[k] = k < cfg->n_tasks ? cfg->task_bin[k] : 0;
+  }
+  S.fixed_obj = cfg->fixed_task_obj;
+  S.fixed_bin = cfg->fixed_task_bin;
+  S.pgs_max_iter = cfg->solver_iterations > 0 ? cfg->solver_iterations : 100;
+  S.pgs_tol = cfg->solver_tolerance > 0 ? cfg->solver_tolerance : 1e-5f;
+  const size_t n = static_cast<size_t>(N);
+  S.qpos = dalloc<float>(sim, MMX_NQ_ * n);
+  S.qvel = dalloc<float>(sim, MMX_NV_ * n);
+  S.ctrl = dalloc<float>(sim, MMX_NU_ * n);
+  S.qacc_ws = dalloc<float>(sim, MMX_NV_ * n);
+  S.kin = dalloc<float>(sim, KIN_N * n);
+  S.target = dalloc<float>(sim, 3 * n);
+  S.epi = dalloc<int>(sim, EPI_N * n);
+  S.epf = dalloc<float>(sim, EPF_N * n);
+  S.rng = dalloc<unsigned long long>(sim, 4 * n);
+  S.rng32 = dalloc<unsigned int>(sim, n);
+  S.obs = dalloc<float>(sim, MMX_NOBS * n);
+  S.reward = dalloc<float>(sim, n);
+  S.reward_components = dalloc<float>(sim, 6 * n);
+  S.done = dalloc<int>(sim, 3 * n);
+  S.con = dalloc<float>(sim, static_cast<size_t>(MMX_MAXCON) * CON_F * n);
+  S.efc = dalloc<float>(sim, static_cast<size_t>(MMX_MAXEFC) * EFC_F * n);
+  S.stats = dalloc<float>(sim, STAT_N * n);
+  sim->expert_action = dalloc<float>(sim, 4 * n);
+  sim->d_mask = dalloc<unsigned char>(sim, n);
+  sim->d_task = dalloc<int>(sim, n);
+  for (void* p : sim->allocs)
+    if (!p) {
+      mmx_destroy(sim);
+      return MMX_ENOMEM;
+    }
+  if (!S.qpos || !S.efc || !sim->d_task) {
+    mmx_destroy(sim);
+    return MMX_ENOMEM;
+  }
+  // gymnasium's lazily created np_random uses OS entropy when never seeded
+  std::random_device rd;
+  std::vector<unsigned long long> rng(4 * n);
+  for (size_t i = 0; i < n; i++) {
+    uint64_t st[4];
+    pcg64_seed((static_cast<uint64_t>(rd()) << 32) ^ rd(), st);
+    for (int k = 0; k < 4; k++) rng[k * n + i] = st[k];
+  }
+  hipMemcpy(S.rng, rng.data(), rng.size() * sizeof(unsigned long long), hipMemcpyHostToDevice);
+  *out = sim;
+  return hip_check(sim, hipDeviceSynchronize(), "mmx_create");
+}
+
+void mmx_destroy(mmx_sim* sim) {
+  if (!sim) return;
+  hipDeviceSynchronize();
+  for (void* p : sim->allocs)
+    if (p) hipFree(p);
+  delete sim;
+}
+
+const char* mmx_last_error(const mmx_sim* sim) { return sim ? sim->err.c_str() : "null sim"; }
+
+int mmx_reset(mmx_sim* sim, const uint64_t* seeds, const uint8_t* seed_given, const int32_t* task_override,
+              const uint8_t* env_mask) {
+  if (!sim) return MMX_EINVAL;
+  MMXState& S = sim->S;
+  const size_t n = static_cast<size_t>(S.N);
+  if (seeds) {
+    // re-seed selected envs: PCG64(SeedSequence(seed)); the 32-bit buffer is cleared
+    std::vector<unsigned long long> rng(4 * n);
+    if (hipMemcpy(rng.data(), S.rng, rng.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
+      return fail(sim, MMX_EDEVICE, "rng readback");
+    std::vector<int> has32(n);
+    hipMemcpy(has32.data(), S.epi + static_cast<size_t>(EPI_RNG_HAS32) * n, n * sizeof(int), hipMemcpyDeviceToHost);
+    for (size_t i = 0; i < n; i++) {
+      if (env_mask && !env_mask[i]) continue;
+      if (seed_given && !seed_given[i]) continue;
+      uint64_t st[4];
+      pcg64_seed(seeds[i], st);
+      for (int k = 0; k < 4; k++) rng[k * n + i] = st[k];
+      has32[i] = 0;
+    }
+    hipMemcpy(S.rng, rng.data(), rng.size() * sizeof(unsigned long long), hipMemcpyHostToDevice);
+    hipMemcpy(S.epi + static_cast<size_t>(EPI_RNG_HAS32) * n, has32.data(), n * sizeof(int), hipMemcpyHostToDevice);
+  }
+  const unsigned char* dmask = nullptr;
+  const int* dtask = nullptr;
+  if (env_mask) {
+    hipMemcpyAsync(sim->d_mask, env_mask, n, hipMemcpyHostToDevice, sim->stream);
+    dmask = sim->d_mask;
+  }
+  if (task_override) {
+    for (size_t i = 0; i < n; i++) {
+      const int t = task_override[i];
+      if (t >= 0 && ((t >> 4) > 2 || (t & 15) > 2)) return fail(sim, MMX_EINVAL, "task_override out of range");
+    }
+    hipMemcpyAsync(sim->d_task, task_override, n * sizeof(int), hipMemcpyHostToDevice, sim->stream);
+    dtask = sim->d_task;
+  }
+  int rc = hip_check(sim, mmx_launch_reset(&S, dmask, dtask, sim->stream), "mmx_reset");
+  if (rc) return rc;
+  return hip_check(sim, hipStreamSynchronize(sim->stream), "mmx_reset sync");
+}
+
+int mmx_step(mmx_sim* sim, const float* action_dev, int32_t action_dim) {
+  if (!sim || !action_dev) return MMX_EINVAL;
+  static const int kDim[5] = {4, 8, 10, 8, 10};
+  if (action_dim < kDim[sim->S.action_mode]) return fail(sim, MMX_EINVAL, "action_dim too small for action_mode");
+  return hip_check(sim, mmx_launch_step(&sim->S, action_dev, action_dim, 0, sim->stream), "mmx_step");
+}
+
+int mmx_expert_plan(mmx_sim* sim, int32_t n_steps, float* action_dev_out) {
+  if (!sim || n_steps < 0) return MMX_EINVAL;
+  return hip_check(sim, mmx_launch_expert(&sim->S, n_steps, action_dev_out, sim->stream), "mmx_expert_plan");
+}
+
+int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
+  if (!sim || sim->S.action_mode != MMX_ACTION_ABS_POS) return MMX_EINVAL;
+  for (int k = 0; k < n_env_steps; k++) {
+    hipError_t e = mmx_launch_expert(&sim->S, MMX_NSUBSTEP, sim->expert_action, sim->stream);
+    if (e == hipSuccess) e = mmx_launch_step(&sim->S, sim->expert_action, 4, 1, sim->stream);
+    if (e != hipSuccess) return hip_check(sim, e, "mmx_rollout_expert");
+  }
+  return MMX_OK;
+}
+
+int mmx_physics_step(mmx_sim* sim, int32_t n, int32_t with_ik) {
+  if (!sim || n < 0) return MMX_EINVAL;
+  return hip_check(sim, mmx_launch_physics(&sim->S, n, with_ik, sim->stream), "mmx_physics_step");
+}
+
+int mmx_forward(mmx_sim* sim) {
+  if (!sim) return MMX_EINVAL;
+  return hip_check(sim, mmx_launch_forward(&sim->S, sim->stream), "mmx_forward");
+}
+
+int mmx_get_buffers(mmx_sim* sim, mmx_buffers* b) {
+  if (!sim || !b) return MMX_EINVAL;
+  const MMXState& S = sim->S;
+  b->num_envs = S.N;
+  b->qpos = S.qpos;
+  b->qvel = S.qvel;
+  b->ctrl = S.ctrl;
+  b->qacc_warmstart = S.qacc_ws;
+  b->obs = S.obs;
+  b->reward = S.reward;
+  b->done = S.done;
+  b->reward_components = S.reward_components;
+  b->episode_i = S.epi;
+  b->episode_f = S.epf;
+  b->kin = S.kin;
+  b->stats = S.stats;
+  b->contacts = S.con;
+  return MMX_OK;
+}
+
+int mmx_synchronize(mmx_sim* sim) {
+  if (!sim) return MMX_EINVAL;
+  return hip_check(sim, hipStreamSynchronize(sim->stream), "mmx_synchronize");
+}
+
+int mmx_get_state(mmx_sim* sim, float* qpos, float* qvel, float* ctrl, float* ws) {
+  if (!sim) return MMX_EINVAL;
+  const size_t n = static_cast<size_t>(sim->S.N);
+  hipError_t e = hipStreamSynchronize(sim->stream);
+  if (e == hipSuccess && qpos) e = hipMemcpy(qpos, sim->S.qpos, MMX_NQ_ * n * 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && qvel) e = hipMemcpy(qvel, sim->S.qvel, MMX_NV_ * n * 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && ctrl) e = hipMemcpy(ctrl, sim->S.ctrl, MMX_NU_ * n * 4, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && ws) e = hipMemcpy(ws, sim->S.qacc_ws, MMX_NV_ * n * 4, hipMemcpyDeviceToHost);
+  return hip_check(sim, e, "mmx_get_state");
+}
+
+int mmx_set_state(mmx_sim* sim, const float* qpos, const float* qvel, const float* ctrl, const float* ws) {
+  if (!sim) return MMX_EINVAL;
+  const size_t n = static_cast<size_t>(sim->S.N);
+  hipError_t e = hipStreamSynchronize(sim->stream);
+  if (e == hipSuccess && qpos) e = hipMemcpy(sim->S.qpos, qpos, MMX_NQ_ * n * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess && qvel) e = hipMemcpy(sim->S.qvel, qvel, MMX_NV_ * n * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess && ctrl) e = hipMemcpy(sim->S.ctrl, ctrl, MMX_NU_ * n * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess && ws) e = hipMemcpy(sim->S.qacc_ws, ws, MMX_NV_ * n * 4, hipMemcpyHostToDevice);
+  return hip_check(sim, e, "mmx_set_state");
+}
+
+uint32_t mmx_episode_seed(uint64_t root, int32_t index) {
+  return seedseq(seed_words(root), {static_cast<uint32_t>(index)}, 1)[0];
+}
+
+}  // extern "C"

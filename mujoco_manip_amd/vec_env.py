@@ -1,0 +1,149 @@
+"""PickPlaceVecEnv — batched torch façade over the C-ABI (one MI355X, num_envs lanes).
+
+Mirrors PickPlaceGymEnv (mujoco_manip/gym_env.py:39-602) with a leading env dimension:
+same constructor keywords, same 5 action modes, same numeric observation keys and reward
+types.  Differences, all documented in DESIGN.md:
+  * observations are torch tensors on the GPU ([N, ...]); images are not rendered in this
+    build (config 5 renderer is a follow-up), so the image keys are absent;
+  * reset(seed=s) seeds env i with s + i (gymnasium vector convention); a list gives one
+    seed per env;
+  * with autoreset=True an env that terminated/truncated is reset inside the same step
+    (the returned obs is the first obs of the new episode).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from .constants import ACTION_REPEAT, BINS, IMAGE_SIZE, MAX_EPISODE_STEPS, OBJECTS, OBS_SLICES, TASK_SETS, task_index
+
+
+class PickPlaceVecEnv:
+    metadata = {"render_modes": [], "render_fps": 30}
+
+    def __init__(self, num_envs: int = 1, task: tuple[str, str] | None = None, tasks="all",
+                 action_mode: str = "ee_pos_quat_g_rel", reward_type: str = "dense", image_size: int = IMAGE_SIZE,
+                 render_mode: str | None = None, max_episode_steps: int = MAX_EPISODE_STEPS,
+                 randomize_objects: bool = False, spawn_x_range=(-0.20, 0.20), spawn_y_range=(0.30, 0.45),
+                 autoreset: bool = False, device: int = 0, solver_iterations: int = 100,
+                 solver_tolerance: float = 1e-5):
+        if not torch.cuda.is_available():
+            raise RuntimeError("PickPlaceVecEnv needs an MI355X GPU (HIP); no CPU fallback exists")
+        pool = TASK_SETS[tasks] if isinstance(tasks, str) else list(tasks)
+        self.num_envs = int(num_envs)
+        self.device = torch.device(f"cuda:{device}")
+        self.render_mode = render_mode
+        self._action_mode = action_mode
+        self._reward_type = reward_type
+        self._task_pool = pool
+        self._fixed_task = task
+        with torch.cuda.device(self.device):
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+        self.sim = _lib.Sim(self.num_envs, action_mode=action_mode, reward_type=reward_type,
+                            max_episode_steps=max_episode_steps, randomize_objects=randomize_objects,
+                            spawn_x_range=spawn_x_range, spawn_y_range=spawn_y_range,
+                            task_pool=[task_index(t) for t in pool],
+                            fixed_task=None if task is None else task_index(task), image_size=image_size,
+                            autoreset=autoreset, solver_iterations=solver_iterations,
+                            solver_tolerance=solver_tolerance, device=device, stream=stream)
+        s = self.sim
+        self.action_dim = s.action_dim
+        self._obs = s.view("obs", _lib.NOBS)
+        self._reward = s.view("reward", 1)
+        self._done = s.view("done", 3, "<i4")
+        self._rc = s.view("reward_components", 6)
+        self._epi = s.view("episode_i", _lib.EPI_N, "<i4")
+        self._epf = s.view("episode_f", _lib.EPF_N)
+        self.qpos = s.view("qpos", _lib.NQ)
+        self.qvel = s.view("qvel", _lib.NV)
+        self.ctrl = s.view("ctrl", _lib.NU)
+        self.stats = s.view("stats", _lib.STAT_N)
+        self._expert_action = torch.zeros(self.num_envs, 4, device=self.device, dtype=torch.float32)
+
+    # ------------------------------------------------------------------ gym API
+    def _obs_dict(self):
+        flat = self._obs.t()
+        out = {}
+        for k, (a, b, shape) in OBS_SLICES.items():
+            out[k] = flat[:, a:b].reshape(self.num_envs, *shape).clone()
+        return out
+
+    def reset(self, *, seed=None, options: dict | None = None):
+        """PickPlaceGymEnv.reset (gym_env.py:477-534), batched."""
+        N = self.num_envs
+        seeds = None
+        if seed is not None:
+            seeds = [int(seed) + k for k in range(N)] if np.isscalar(seed) else list(seed)
+        task = None
+        if options and "task" in options:
+            t = options["task"]
+            if isinstance(t, tuple) and isinstance(t[0], str):
+                o, b = task_index(t)
+                task = np.full(N, (o << 4) | b, np.int32)
+            else:
+                task = np.array([(task_index(x)[0] << 4) | task_index(x)[1] for x in t], np.int32)
+        self.sim.reset(seeds=seeds, task_override=task)
+        return self._obs_dict(), {}
+
+    def step(self, actions: torch.Tensor):
+        """PickPlaceGymEnv.step (gym_env.py:536-581), batched: actions [N, action_dim] fp32 on the GPU."""
+        a = torch.as_tensor(actions, dtype=torch.float32, device=self.device)
+        if a.dim() != 2 or a.shape[0] != self.num_envs or a.shape[1] < self.action_dim:
+            raise ValueError(f"actions must be [{self.num_envs}, {self.action_dim}], got {tuple(a.shape)}")
+        a = a.contiguous()
+        self.sim.step(a.data_ptr(), a.shape[1])
+        obs = self._obs_dict()
+        reward = self._reward.clone()
+        terminated = self._done[0].bool().clone()
+        truncated = self._done[1].bool().clone()
+        info = {"success": self._done[2].bool().clone()}
+        if self._reward_type == "staged":
+            info["reward_components"] = self._rc.t().clone()
+        self._last_action = a
+        return obs, reward, terminated, truncated, info
+
+    # ------------------------------------------------------------------ expert + helpers
+    def expert_plan(self, n_steps: int = ACTION_REPEAT) -> torch.Tensor:
+        """PickAndPlaceTask.plan(n_steps) for all envs -> abs_pos actions [N, 4]."""
+        self.sim.expert_plan(n_steps, self._expert_action.data_ptr())
+        return self._expert_action.clone()
+
+    def rollout_expert(self, n_env_steps: int):
+        """Device-resident FSM rollout (generate_dataset.py:140-196), no host round trips."""
+        self.sim.rollout_expert(n_env_steps)
+
+    @property
+    def step_count(self) -> torch.Tensor:
+        return self._epi[2].clone()
+
+    @property
+    def tasks(self) -> list[tuple[str, str]]:
+        ob = self._epi[0].cpu().numpy()
+        bn = self._epi[1].cpu().numpy()
+        return [(OBJECTS[o], BINS[b]) for o, b in zip(ob, bn)]
+
+    @property
+    def fsm_state(self) -> torch.Tensor:
+        return self._epi[4].clone()
+
+    @property
+    def initial_ee_se3(self) -> torch.Tensor:
+        T = torch.zeros(self.num_envs, 4, 4, device=self.device)
+        f = self._epf.t()
+        T[:, :3, :3] = f[:, 0:9].reshape(-1, 3, 3)
+        T[:, :3, 3] = f[:, 9:12]
+        T[:, 3, 3] = 1.0
+        return T
+
+    def solver_stats(self) -> dict:
+        s = self.stats.double().sum(dim=1).cpu().numpy()
+        sub = max(s[3], 1.0)
+        return {"mean_nefc": s[0] / sub, "mean_ncon": s[1] / sub, "mean_pgs_iter": s[2] / sub,
+                "max_resid": float(self.stats[4].max().item())}
+
+    def clear_stats(self):
+        self.stats.zero_()
+
+    def close(self):
+        self.sim.close()

@@ -658,3 +658,21 @@ void or_get_initial_ee(or_env* e, double* T16) { memcpy(T16, e->T_init, sizeof(e
 int or_step_count(or_env* e) { return e->step_count; }
 void or_get_task(or_env* e, int* o, int* b) { *o = e->obj; *b = e->bin; }
 void or_get_hwm(or_env* e, double* h) { memcpy(h, e->hwm, sizeof(e->hwm)); }
+
+/* ======================================================================= test hooks
+ * Overwrite derived quantities so golden traces generated with scripted body positions
+ * (tests/golden/make_golden.py) can be replayed through the same task-layer code. */
+void or_debug_set_xpos(or_env* e, int body, const double* p) { v3_copy(e->xpos[body], p); }
+void or_debug_set_contacts(or_env* e, int n, const int* pairs) {
+  e->ncon = n;
+  for (int i = 0; i < n; i++) { e->con[i].geom[0] = pairs[2 * i]; e->con[i].geom[1] = pairs[2 * i + 1]; }
+}
+void or_debug_set_episode(or_env* e, int obj, int bin, const double* T16) {
+  e->obj = obj;
+  e->bin = bin;
+  memcpy(e->T_init, T16, sizeof(e->T_init));
+  e->has_grasped = e->has_lifted = e->above_target = e->has_placed = 0;
+  e->hwm_valid = 0;
+  memset(e->hwm, 0, sizeof(e->hwm));
+}
+double or_debug_reward(or_env* e, int* success) { return compute_reward(e, success); }

@@ -97,6 +97,12 @@ int64_t or_pcg64_integers(or_pcg64* r, int64_t high);
 uint32_t or_episode_seed(uint64_t root_seed, int index); /* SeedSequence(root).spawn(N)[i].generate_state(1)[0] */
 int or_sample_positions(or_pcg64* r, const double* xr, const double* yr, double min_sep, double* xy6);
 
+/* test hooks (golden-trace replay) */
+void or_debug_set_xpos(or_env* e, int body, const double* p);
+void or_debug_set_contacts(or_env* e, int n, const int* pairs);
+void or_debug_set_episode(or_env* e, int obj, int bin, const double* T16);
+double or_debug_reward(or_env* e, int* success);
+
 #ifdef __cplusplus
 }
 #endif

@@ -92,6 +92,11 @@ def lib():
         L.or_episode_seed.argtypes = [C.c_uint64, C.c_int]
         L.or_sample_positions.restype = C.c_int
         L.or_sample_positions.argtypes = [C.c_void_p, dp, dp, C.c_double, dp]
+        L.or_debug_set_xpos.argtypes = [C.c_void_p, C.c_int, dp]
+        L.or_debug_set_contacts.argtypes = [C.c_void_p, C.c_int, ip]
+        L.or_debug_set_episode.argtypes = [C.c_void_p, C.c_int, C.c_int, dp]
+        L.or_debug_reward.restype = C.c_double
+        L.or_debug_reward.argtypes = [C.c_void_p, ip]
         _lib = L
     return _lib
 
@@ -287,6 +292,22 @@ class OracleEnv:
         h = np.zeros(5)
         lib().or_get_hwm(self.ptr, _d(h))
         return h
+
+    # test hooks
+    def debug_set_xpos(self, body, p):
+        lib().or_debug_set_xpos(self.ptr, body, _d(np.ascontiguousarray(p, float)))
+
+    def debug_set_contacts(self, pairs):
+        arr = np.array(pairs if len(pairs) else [[0, 0]], np.int32).ravel()
+        lib().or_debug_set_contacts(self.ptr, len(pairs), _i(arr))
+
+    def debug_set_episode(self, obj, bin_, T_init):
+        lib().or_debug_set_episode(self.ptr, obj, bin_, _d(np.ascontiguousarray(T_init, float)))
+
+    def debug_reward(self):
+        s = C.c_int()
+        r = lib().or_debug_reward(self.ptr, C.byref(s))
+        return r, bool(s.value)
 
     @property
     def step_count(self):

@@ -1,0 +1,144 @@
+"""Pin the CPU oracle against golden vectors generated from the reference Python.
+
+Fixtures: tests/golden/golden.json, produced by tests/golden/make_golden.py, which drives
+the reference's own functions (pose_utils.py, controller.py, pick_and_place.py,
+randomization.py, gym_env.py) through stub mujoco/gymnasium modules.
+"""
+import numpy as np
+import pytest
+
+import oracle_py as O
+
+OBJ = ["obj_red", "obj_green", "obj_blue"]
+BIN = ["bin_red", "bin_green", "bin_blue"]
+STATE_NAMES = ["IDLE", "PRE_GRASP", "GRASP", "CLOSE_GRIPPER", "LIFT", "MOVE_TO_BIN", "SETTLE_AT_BIN",
+               "LOWER_TO_BIN", "RELEASE", "RETREAT", "DONE"]
+BODY = {"hand": 9, "obj_red": 16, "obj_green": 17, "obj_blue": 18, "bin_red": 13, "bin_green": 14, "bin_blue": 15}
+
+
+def test_rotmat_to_quat(golden):  # pose_utils.py:48-82 (branch-exact)
+    for c in golden["rotmat_to_quat"]:
+        np.testing.assert_allclose(O.rotmat_to_quat_xyzw(np.array(c["R"])), c["q"], atol=1e-12)
+
+
+def test_quat_to_rotmat(golden):  # pose_utils.py:85-101
+    for c in golden["quat_to_rotmat"]:
+        np.testing.assert_allclose(O.quat_xyzw_to_rotmat(np.array(c["q"])), c["R"], atol=1e-12)
+
+
+def test_rotmat_from_6d(golden):  # pose_utils.py:121-146
+    for c in golden["rotmat_from_6d"]:
+        np.testing.assert_allclose(O.rotmat_from_6d(np.array(c["d6"])), c["R"], atol=1e-12)
+
+
+def test_orientation_error(golden):  # controller.py:21-43
+    TARGET = np.array([[0, 1, 0], [1, 0, 0], [0, 0, -1.0]])
+    for c in golden["orientation_error"]:
+        np.testing.assert_allclose(O.orientation_error(np.array(c["Rc"]), TARGET), c["err"], atol=1e-9)
+
+
+def test_ik_math(golden):  # controller.py:87-137 given the Jacobian
+    rng = np.array(golden["jnt_range"])
+    for c in golden["ik"]:
+        out = O.ik_math(np.array(c["J"]), c["ee_pos"], np.array(c["ee_xmat"]), c["q"], c["target"], rng)
+        np.testing.assert_allclose(out, c["q_target"], atol=1e-9)
+
+
+def test_decode_action(golden):  # gym_env.py:252-281
+    for c in golden["decode"]:
+        tgt, g = O.decode_action(c["mode"], c["action"], np.array(c["T_init"]))
+        np.testing.assert_allclose(tgt, c["target"], atol=1e-12)
+        assert g == pytest.approx(c["grip"], abs=1e-7)
+
+
+def test_pcg64_raw_stream(golden):  # gymnasium np_random = Generator(PCG64(SeedSequence(seed)))
+    for seed, raw in golden["pcg64_raw"].items():
+        r = O.PCG64(int(seed))
+        assert [r.next64() for _ in range(len(raw))] == raw
+
+
+def test_reset_rng_positions_and_task(golden):  # randomization.py:70-98 + gym_env.py:515-517
+    for c in golden["resets"]:
+        r = O.PCG64(c["seed"])
+        xy, n = r.sample_positions()
+        np.testing.assert_array_equal(xy, np.array(c["xy"]))
+        assert r.integers(9) == c["task_idx"]
+
+
+def test_episode_seeds(golden):  # scripts/generate_dataset.py:263-268
+    g = golden["episode_seeds"]
+    assert [O.episode_seed(g["root"], i) for i in range(len(g["seeds"]))] == g["seeds"]
+
+
+def test_seedsequence_against_numpy():
+    for ent, key in [((42,), ()), ((7,), (3,)), ((2**32 + 9,), (1, 2)), ((0,), (5,))]:
+        ss = np.random.SeedSequence(ent[0], spawn_key=key)
+        ref = ss.generate_state(6)
+        words = [ent[0] & 0xFFFFFFFF] + ([ent[0] >> 32] if ent[0] >> 32 else [])
+        np.testing.assert_array_equal(O.seedseq_state(words, key, 6), ref)
+
+
+def test_integers_against_numpy():
+    for seed in range(20):
+        g = np.random.Generator(np.random.PCG64(np.random.SeedSequence(seed)))
+        r = O.PCG64(seed)
+        for high in (9, 3, 6, 1000, 7):
+            assert r.integers(high) == int(g.integers(high))
+        assert r.random() == g.random()
+
+
+def test_fsm_traces(golden):  # pick_and_place.py:167-277 on scripted positions
+    for tr in golden["fsm"]:
+        e = O.OracleEnv()
+        tasks = [(OBJ.index(o), BIN.index(b)) for o, b in tr["tasks"]]
+        e.fsm_init(tasks)
+        for k, st in enumerate(tr["trace"]):
+            e.debug_set_xpos(BODY["hand"], st["ee"])
+            for nm, p in st["objs"].items():
+                e.debug_set_xpos(BODY[nm], p)
+            for nm, p in [("bin_red", [-0.3, 0.55, 0.24]), ("bin_green", [0.0, 0.65, 0.24]),
+                          ("bin_blue", [0.3, 0.55, 0.24])]:
+                e.debug_set_xpos(BODY[nm], p)
+            e.fsm_plan(tr["n_steps"])
+            s = e.fsm_get()
+            assert STATE_NAMES[s["state"]] == st["state"], f"step {k}"
+            assert s["task_index"] == st["task_index"]
+            assert s["settle"] == st["settle"]
+            assert float(s["gripper_open"]) == st["gripper"]
+            if st["target"] is not None:
+                np.testing.assert_allclose(s["target"], st["target"], atol=1e-12)
+        assert STATE_NAMES[e.fsm_get()["state"]] == "DONE"
+
+
+def test_rewards(golden):  # gym_env.py:341-470
+    rtypes = {"dense": "dense", "sparse": "sparse", "staged": "staged"}
+    for ep in golden["rewards"]:
+        e = O.OracleEnv(reward_type=rtypes[ep["reward_type"]])
+        obj, bin_ = OBJ.index(ep["obj"]), BIN.index(ep["bin"])
+        e.debug_set_episode(obj, bin_, np.array(ep["T_init"]))
+        for st in ep["seq"]:
+            e.debug_set_xpos(BODY[ep["obj"]], st["obj"])
+            e.debug_set_xpos(BODY[ep["bin"]], ep["bin_pos"])
+            e.debug_set_xpos(BODY["hand"], st["ee"])
+            qpos, qvel, ctrl, ws = e.get_state()
+            ctrl[7] = st["ctrl7"]
+            e.set_state(ctrl=ctrl)
+            e.debug_set_contacts(st["contacts"])
+            r, s = e.debug_reward()
+            assert r == pytest.approx(st["reward"], abs=1e-12)
+            assert s == st["success"]
+            if st["hwm"] is not None:
+                np.testing.assert_allclose(e.hwm(), st["hwm"], atol=1e-12)
+
+
+def test_geom_classes_match_reference(golden):  # gym_env.py:137-152
+    import json
+    import os
+
+    model = json.load(open(os.path.join(os.path.dirname(__file__), "..", "mujoco_manip_amd", "model",
+                                        "panda_pickplace.json")))
+    robot_names = {"link0", "link1", "link2", "link3", "link4", "link5", "link6", "link7", "hand", "left_finger",
+                   "right_finger"}
+    names = [b["name"] for b in model["bodies"]]
+    rob = [i for i, g in enumerate(model["col_geoms"]) if names[model["geoms"][g]["body"]] in robot_names]
+    assert rob == golden["robot_geoms"]

@@ -590,13 +590,67 @@ def to_jsonable(model):
     return out
 
 
+QUAL = "static const"
+
+
 def c_array(name, ctype, values, fmt="{:.17g}"):
     flat = np.asarray(values).ravel().tolist()
     body = ", ".join(fmt.format(x) if ctype in ("double", "float") else str(int(x)) for x in flat)
-    suffix = "f" if ctype == "float" else ""
     if ctype == "float":
-        body = ", ".join((fmt.format(x) + "f") for x in flat)
-    return f"static const {ctype} {name}[{len(flat)}] = {{{body}}};\n"
+        body = ", ".join((repr(float(np.float32(x))) + "f") for x in flat)
+    return f"{QUAL} {ctype} {name}[{len(flat)}] = {{{body}}};\n"
+
+
+def device_tables(model, P, R):
+    """Extra tables for the device kernels: static geom world poses, body bounding
+    spheres and the candidate pairs grouped by body pair (hierarchical broadphase)."""
+    bodies, geoms = model["bodies"], model["geoms"]
+    col = model["col_geoms"]
+    cid = {g: i for i, g in enumerate(col)}
+    kin = kinematics_np(model, np.array(model["key_qpos"]))
+    xpos, xmat = kin[0], kin[1]
+    L = []
+    sx, sm = [], []
+    for g in col:
+        G = geoms[g]
+        b = G["body"]
+        p = xpos[b] + xmat[b] @ np.array(G["pos"])
+        Rm = xmat[b] @ quat2mat(G["quat"])
+        sx.append(p.tolist())
+        sm.append(Rm.ravel().tolist())
+    L.append(c_array(f"{P}geom_static_xpos", R, sx))
+    L.append(c_array(f"{P}geom_static_xmat", R, sm))
+    L.append(c_array(f"{P}geom_lmat", R, [quat2mat(geoms[g]["quat"]).ravel().tolist() for g in col]))
+    L.append(c_array(f"{P}body_static", "int", [1 if b["weld"] == 0 else 0 for b in bodies]))
+    # body bounding spheres (body frame for moving bodies, world frame for static ones)
+    spheres = []
+    for bid, b in enumerate(bodies):
+        gl = [cid[g] for g in b["geoms"] if g in cid]
+        if not gl or bid == 0:
+            spheres.append([0, 0, 0, 0])
+            continue
+        cs = np.array([geoms[col[i]]["pos"] for i in gl])
+        rs = np.array([geoms[col[i]]["rbound"] for i in gl])
+        lo, hi = (cs - rs[:, None]).min(0), (cs + rs[:, None]).max(0)
+        c = 0.5 * (lo + hi)
+        r = float(max(np.linalg.norm(cs - c, axis=1) + rs))
+        if b["weld"] == 0:
+            c = xpos[bid] + xmat[bid] @ c
+        spheres.append(c.tolist() + [r])
+    L.append(c_array(f"{P}body_bsphere", R, spheres))
+    # group pairs by body pair
+    groups = {}
+    for a, bb in model["pairs"]:
+        key = (geoms[a]["body"], geoms[bb]["body"])
+        groups.setdefault(key, []).append((cid[a], cid[bb]))
+    bp, pl = [], []
+    for (b1, b2), lst in groups.items():
+        bp.append([b1, b2, len(pl), len(lst)])
+        pl.extend(lst)
+    L.append(f"#define {P}NBODYPAIR {len(bp)}\n")
+    L.append(c_array(f"{P}bodypair", "int", bp))
+    L.append(c_array(f"{P}bodypair_geoms", "int", pl))
+    return L
 
 
 def emit_header(model, path, real, prefix, guard):
@@ -605,10 +659,14 @@ def emit_header(model, path, real, prefix, guard):
     col = model["col_geoms"]
     cid = {g: i for i, g in enumerate(col)}
     nb, nj, ng = len(bodies), len(joints), len(col)
+    global QUAL
+    QUAL = "MMX_MODEL_QUAL" if prefix == "MMX_" else "static const"
     L = [f"/* GENERATED by tools/compile_model.py from the reference MJCF\n"
          f" * (mujoco_manip/data/pick_and_place_scene.xml + franka_emika_panda/panda.xml).\n"
          f" * Data only; do not edit. */\n",
          f"#ifndef {guard}\n#define {guard}\n\n"]
+    if prefix == "MMX_":
+        L.append("#ifndef MMX_MODEL_QUAL\n#define MMX_MODEL_QUAL static const\n#endif\n\n")
     P = prefix
     L.append(f"#define {P}NBODY {nb}\n#define {P}NJNT {nj}\n#define {P}NQ {model['nq']}\n#define {P}NV {model['nv']}\n")
     L.append(f"#define {P}NGEOM {ng}\n#define {P}NMESH {len(model['meshes'])}\n#define {P}NPAIR {len(model['pairs'])}\n")
@@ -713,6 +771,8 @@ def emit_header(model, path, real, prefix, guard):
         else:
             gclass.append(0)
     L.append(c_array(f"{P}geom_class", "int", gclass))
+    if prefix == "MMX_":
+        L.extend(device_tables(model, P, R))
     L.append(f"\n#define {P}TIMESTEP {model['opt']['timestep']!r}\n#define {P}GRAVITY_Z (-9.81)\n")
     L.append(f"\n#endif /* {guard} */\n")
     with open(path, "w") as f:

@@ -1,0 +1,121 @@
+"""GPU-vs-oracle diagnostic probe (writes gpurun_out/probe.json). Test infrastructure."""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+import oracle_py as O  # noqa: E402
+import torch  # noqa: E402
+
+from mujoco_manip_amd import _lib  # noqa: E402
+
+out = {}
+
+
+def states_from_oracle_rollout(n_states=32, seed=0):
+    """Collect diverse states (free space, resting, grasping, transporting) from an oracle FSM episode."""
+    e = O.OracleEnv()
+    e.reset_keyframe()
+    e.fsm_init([(0, 0)])
+    states = []
+    k = 0
+    while len(states) < 200 and k < 2000:
+        e.fsm_plan(16)
+        e.fsm_actuate()
+        for _ in range(16):
+            e.mj_step()
+        states.append(e.get_state())
+        k += 1
+        if e.fsm_get()["state"] == 10:
+            break
+    idx = np.linspace(0, len(states) - 1, n_states).astype(int)
+    return [states[i] for i in idx]
+
+
+def physics_parity(n_sub):
+    sts = states_from_oracle_rollout(64)
+    N = len(sts)
+    sim = _lib.Sim(N)
+    qpos = np.stack([s[0] for s in sts], 1).astype(np.float32)
+    qvel = np.stack([s[1] for s in sts], 1).astype(np.float32)
+    ctrl = np.stack([s[2] for s in sts], 1).astype(np.float32)
+    ws = np.stack([s[3] for s in sts], 1).astype(np.float32)
+    sim.set_state(qpos, qvel, ctrl, ws)
+    sim.physics_step(n_sub, with_ik=False)
+    gq, gv, _, _ = sim.get_state()
+    dq, dv = [], []
+    for k, s in enumerate(sts):
+        e = O.OracleEnv()
+        e.set_state(qpos[:, k].astype(float), qvel[:, k].astype(float), ctrl[:, k].astype(float), ws[:, k].astype(float))
+        for _ in range(n_sub):
+            e.mj_step()
+        rq, rv, _, _ = e.get_state()
+        dq.append(np.abs(gq[:, k] - rq).max())
+        dv.append(np.abs(gv[:, k] - rv).max())
+    st = sim.view("stats", _lib.STAT_N).double().cpu().numpy()
+    return {"max_dqpos": float(max(dq)), "max_dqvel": float(max(dv)), "per_state_dq": [float(x) for x in dq],
+            "per_state_dv": [float(x) for x in dv], "mean_nefc": float(st[0].sum() / max(st[3].sum(), 1)),
+            "mean_pgs_iter": float(st[2].sum() / max(st[3].sum(), 1)), "max_resid": float(st[4].max())}
+
+
+def gym_parity(steps=30, mode="abs_pos"):
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    N = 8
+    env = PickPlaceVecEnv(N, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True)
+    obs, _ = env.reset(seed=100)
+    refs = [O.OracleEnv(action_mode="abs_pos", reward_type="staged", randomize_objects=True) for _ in range(N)]
+    robs = np.stack([r.reset(seed=100 + k) for k, r in enumerate(refs)])
+    flat = lambda o: torch.cat([o[k].reshape(N, -1) for k in o], 1).cpu().numpy()  # noqa: E731
+    d0 = np.abs(flat(obs) - robs).max(0)
+    tasks_match = [tuple(refs[k].task()) for k in range(N)] == [(int(a), int(b)) for a, b in zip(env._epi[0].cpu(), env._epi[1].cpu())]
+    errs = []
+    for t in range(steps):
+        act = env.expert_plan(16)
+        obs, r, term, trunc, info = env.step(act)
+        a = act.cpu().numpy()
+        ro = np.stack([refs[k].step(a[k])[0] for k in range(N)])
+        errs.append(float(np.abs(flat(obs)[:, :11] - ro[:, :11]).max()))
+    return {"reset_obs_maxdiff_per_field": d0.tolist(), "tasks_match": bool(tasks_match), "step_state_err": errs}
+
+
+def expert_success(N=256, steps=150):
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    env = PickPlaceVecEnv(N, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True)
+    env.reset(seed=0)
+    t = time.time()
+    succ = torch.zeros(N, dtype=torch.bool, device="cuda")
+    done_at = torch.full((N,), -1, device="cuda")
+    for k in range(steps):
+        act = env.expert_plan(16)
+        obs, r, term, trunc, info = env.step(act)
+        succ |= info["success"]
+        fsm_done = env.fsm_state == 10
+        done_at = torch.where((done_at < 0) & fsm_done, torch.full_like(done_at, k), done_at)
+    torch.cuda.synchronize()
+    return {"success_rate": float(succ.float().mean()), "fsm_done_rate": float((done_at >= 0).float().mean()),
+            "mean_done_step": float(done_at[done_at >= 0].float().mean()) if (done_at >= 0).any() else -1,
+            "secs": time.time() - t, "solver": env.solver_stats()}
+
+
+if __name__ == "__main__":
+    os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
+    for name, fn in [("phys1", lambda: physics_parity(1)), ("phys16", lambda: physics_parity(16)),
+                     ("gym", gym_parity), ("expert", expert_success)]:
+        t = time.time()
+        try:
+            out[name] = fn()
+        except Exception as ex:  # keep going: this is a probe
+            import traceback
+
+            out[name] = {"error": repr(ex), "tb": traceback.format_exc()}
+        out[name + "_secs"] = time.time() - t
+        print(name, json.dumps(out[name])[:600], flush=True)
+        with open(os.path.join(REPO, "gpurun_out", "probe.json"), "w") as f:
+            json.dump(out, f, indent=1)
