@@ -29,9 +29,17 @@ sys.path.insert(0, REPO)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
-def algorithmic_bytes_per_substep(nefc: float) -> float:
-    """B_state + B_efc per env per substep (fp32 words)."""
-    return 2 * 4 * (30 + 27 + 27 + 8) + 2 * 4 * nefc * (27 + 4)
+def algorithmic_bytes_per_env_step(nefc: float) -> float:
+    """B = B_io + 16 (B_state + B_efc) bytes per env step, fp32 words, with
+    B_io = 416, B_state = 2*4*(nq+nv+nv+nu) = 736, B_efc = 2*4*nefc*(nv+4) = 248 nefc."""
+    return 416 + 16 * (2 * 4 * (30 + 27 + 27 + 8) + 2 * 4 * nefc * (27 + 4))
+
+
+def min_hbm_bytes_per_env_step() -> float:
+    """Bytes the fused kernel must move per env step: env record in+out (qpos, qvel, ctrl,
+    warm start, IK cache, target, episode ints/floats, rng, stats) + obs/reward/flags out."""
+    rec = 4 * (30 + 27 + 8 + 27 + 54 + 4 + 14 + 28 + 5) + 8 * 4 + 4
+    return 2 * rec + 4 * (85 + 1 + 3 + 6)
 
 
 def cpu_baseline(seconds: float = 12.0) -> dict:
@@ -102,15 +110,22 @@ def main():
     env.rollout_expert(args.warmup)
     torch.cuda.synchronize()
     env.clear_stats()
+    # the sim launches on torch's current stream: events there bracket exactly the K launches of
+    # the dominant (and only) kernel of a step, mmx_env_step_kernel
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    ev0.record(stream)
     env.rollout_expert(args.steps)
+    ev1.record(stream)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
     if dist:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -119,25 +134,13 @@ def main():
     env_steps = args.steps * N * world
     value = env_steps / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
-
-    # dominant kernel (mmx_substep_kernel): live per-launch duration with HIP events on the
-    # sim's stream, same state distribution (continues the rollout)
-    stream = torch.cuda.current_stream(dev)
-    n_launch = 32
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    env.clear_stats()
-    ev0.record(stream)
-    env.sim.physics_step(n_launch, with_ik=True)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    kern_ms = ev0.elapsed_time(ev1) / n_launch
-    kstats = env.solver_stats()
-    bytes_per_launch = algorithmic_bytes_per_substep(kstats["mean_nefc"]) * N
+    bytes_per_launch = algorithmic_bytes_per_env_step(solver["mean_nefc"]) * N
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+    min_bytes = min_hbm_bytes_per_env_step() * N
 
     stats_all = None
     if dist:
-        loc = torch.tensor([solver["mean_nefc"], solver["mean_pgs_iter"], value / world], device=dev)
+        loc = torch.tensor([solver["mean_nefc"], solver["mean_solver_iter"], value / world], device=dev)
         gathered = [torch.zeros_like(loc) for _ in range(world)]
         dist.all_gather(gathered, loc)
         stats_all = [g.tolist() for g in gathered]
@@ -164,8 +167,10 @@ def main():
                        "parallelism": f"env-batch dp{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "mmx_substep_kernel", "kernel_ms": kern_ms,
-                         "algorithmic_bytes_per_launch": bytes_per_launch, "mean_nefc": kstats["mean_nefc"]},
+                         "kernel": "mmx_env_step_kernel", "kernel_ms": kern_ms,
+                         "algorithmic_bytes_per_launch": bytes_per_launch, "mean_nefc": solver["mean_nefc"],
+                         "min_hbm_bytes_per_launch": min_bytes,
+                         "min_hbm_GBs": min_bytes / (kern_ms * 1e-3) / 1e9},
             "cpu_baseline": cpu,
             "solver": solver,
         }

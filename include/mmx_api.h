@@ -9,8 +9,8 @@
  * Conventions
  *  - every function returns 0 on success or a negative MMX_E* code and never aborts;
  *    mmx_last_error() gives a message;
- *  - device buffers are fp32/int32 structure-of-arrays, field-major with the env index
- *    fastest: element (field f, env i) is at ptr[f * num_envs + i];
+ *  - device buffers are fp32/int32, env-major (one contiguous record per env, matching a
+ *    torch [N, F] tensor): element (env i, field f) is at ptr[i * F + f];
  *  - sim-owned buffers returned by mmx_get_buffers stay valid until mmx_destroy;
  *  - all launches are asynchronous on the sim's stream (cfg.stream, or the null stream);
  *  - one sim per host thread at a time (not re-entrant); per-env faults go to the
@@ -54,29 +54,29 @@ typedef struct {
   int32_t fixed_task_bin;
   int32_t image_size;           /* keypoint normalisation only; no rendering in this build */
   int32_t autoreset;            /* same-step autoreset on terminated/truncated/FSM done */
-  int32_t solver_iterations;    /* PGS sweeps cap */
-  float solver_tolerance;       /* PGS relative force-change tolerance */
+  int32_t solver_iterations;    /* Newton iteration cap (default 30) */
+  float solver_tolerance;       /* relative gradient-norm tolerance (default 1e-6) */
   void* stream;                 /* hipStream_t, NULL = default stream */
 } mmx_config;
 
-/* Field-major device buffers (sim-owned). */
+/* Env-major device buffers (sim-owned): [N][F]. */
 typedef struct {
   int32_t num_envs;
-  float* qpos;               /* [30][N] */
-  float* qvel;               /* [27][N] */
-  float* ctrl;               /* [8][N]  */
-  float* qacc_warmstart;     /* [27][N] */
-  float* obs;                /* [85][N] numeric observation, gym_env.py:295-339 order */
+  float* qpos;               /* [N][30] */
+  float* qvel;               /* [N][27] */
+  float* ctrl;               /* [N][8]  */
+  float* qacc_warmstart;     /* [N][27] */
+  float* obs;                /* [N][85] numeric observation, gym_env.py:295-339 order */
   float* reward;             /* [N] */
-  int32_t* done;             /* [3][N] terminated, truncated, success */
-  float* reward_components;  /* [6][N] staged breakdown (gym_env.py:568-573) */
-  int32_t* episode_i;        /* [14][N] obj, bin, step_count, flags, fsm_state, fsm_task_index,
+  int32_t* done;             /* [N][3] terminated, truncated, success */
+  float* reward_components;  /* [N][6] staged breakdown (gym_env.py:568-573) */
+  int32_t* episode_i;        /* [N][14] obj, bin, step_count, flags, fsm_state, fsm_task_index,
                                 fsm_settle, fsm_gripper_open, fsm_has_target, env_error, ncon, nefc,
                                 episodes, rng_has32 */
-  float* episode_f;          /* [28][N] T_init(12), hwm(5), target_kp(4), fsm_target(3), transit(3), return */
-  float* kin;                /* [54][N] hand pos/mat + arm joint axes/anchors of the last position stage */
-  float* stats;              /* [5][N] sum nefc, sum ncon, sum PGS sweeps, substeps, max residual */
-  float* contacts;           /* [40][12][N] dist, pos3, normal3, mu3, dim, geom1, geom2 (last substep) */
+  float* episode_f;          /* [N][28] T_init(12), hwm(5), target_kp(4), fsm_target(3), transit(3), return */
+  float* kin;                /* [N][54] hand pos/mat + arm joint axes/anchors of the last position stage */
+  float* stats;              /* [N][5] sum nefc, sum ncon, sum solver iterations, substeps, max residual */
+  float* contacts;           /* [N][48][12] dist, pos3, normal3, mu3, dim, geom1, geom2 (last substep) */
 } mmx_buffers;
 
 void mmx_config_default(mmx_config* cfg);
@@ -115,7 +115,7 @@ int mmx_forward(mmx_sim* sim);
 int mmx_get_buffers(mmx_sim* sim, mmx_buffers* out);
 int mmx_synchronize(mmx_sim* sim);
 
-/* Host copies of the core state (host arrays of [field][N] fp32). NULL skips a field. */
+/* Host copies of the core state (host arrays of [N][field] fp32). NULL skips a field. */
 int mmx_get_state(mmx_sim* sim, float* qpos, float* qvel, float* ctrl, float* qacc_warmstart);
 int mmx_set_state(mmx_sim* sim, const float* qpos, const float* qvel, const float* ctrl, const float* qacc_warmstart);
 

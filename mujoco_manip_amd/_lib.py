@@ -16,11 +16,11 @@ import numpy as np
 from . import _build
 
 NQ, NV, NU, NOBS = 30, 27, 8, 85
-MAXCON, CON_F = 40, 12
+MAXCON, CON_F = 64, 12
 EPI_N, EPF_N, KIN_N, STAT_N = 14, 28, 54, 5
 EPI_FIELDS = ("obj", "bin", "step_count", "flags", "fsm_state", "fsm_task_index", "fsm_settle", "fsm_gripper_open",
               "fsm_has_target", "env_error", "ncon", "nefc", "episodes", "rng_has32")
-STAT_FIELDS = ("sum_nefc", "sum_ncon", "sum_pgs_iter", "substeps", "max_resid")
+STAT_FIELDS = ("sum_nefc", "sum_ncon", "sum_solver_iter", "substeps", "max_resid")
 ACTION_MODES = ("abs_pos", "ee_pos_quat_g", "ee_pos_rot6d_g", "ee_pos_quat_g_rel", "ee_pos_rot6d_g_rel")
 ACTION_DIMS = (4, 8, 10, 8, 10)
 REWARD_TYPES = ("dense", "sparse", "staged")
@@ -113,8 +113,8 @@ class Sim:
     def __init__(self, num_envs: int, *, action_mode: str = "ee_pos_quat_g_rel", reward_type: str = "dense",
                  max_episode_steps: int = 500, randomize_objects: bool = False,
                  spawn_x_range=(-0.20, 0.20), spawn_y_range=(0.30, 0.45), task_pool=None, fixed_task=None,
-                 image_size: int = 224, autoreset: bool = False, solver_iterations: int = 100,
-                 solver_tolerance: float = 1e-5, device: int = 0, stream: int | None = None):
+                 image_size: int = 224, autoreset: bool = False, solver_iterations: int = 30,
+                 solver_tolerance: float = 1e-6, device: int = 0, stream: int | None = None):
         if action_mode not in ACTION_MODES:
             raise ValueError(f"action_mode must be one of {ACTION_MODES}, got '{action_mode}'")
         if reward_type not in REWARD_TYPES:
@@ -210,8 +210,8 @@ class Sim:
 
     def get_state(self):
         N = self.num_envs
-        qpos, qvel = np.zeros((NQ, N), np.float32), np.zeros((NV, N), np.float32)
-        ctrl, ws = np.zeros((NU, N), np.float32), np.zeros((NV, N), np.float32)
+        qpos, qvel = np.zeros((N, NQ), np.float32), np.zeros((N, NV), np.float32)
+        ctrl, ws = np.zeros((N, NU), np.float32), np.zeros((N, NV), np.float32)
         self._check(self.L.mmx_get_state(self.ptr, _fptr(qpos), _fptr(qvel), _fptr(ctrl), _fptr(ws)), "mmx_get_state")
         return qpos, qvel, ctrl, ws
 
@@ -219,10 +219,10 @@ class Sim:
         arrs = [None if a is None else np.ascontiguousarray(a, np.float32) for a in (qpos, qvel, ctrl, qacc_ws)]
         self._check(self.L.mmx_set_state(self.ptr, *[_fptr(a) for a in arrs]), "mmx_set_state")
 
-    # ---- zero-copy torch views of sim-owned buffers ([field][N])
+    # ---- zero-copy torch views of sim-owned buffers (env-major [N][F])
     def view(self, name: str, nfield: int, dtype: str = "<f4"):
         import torch
 
         ptr = getattr(self.buffers, name)
-        shape = (nfield, self.num_envs) if nfield > 1 else (self.num_envs,)
+        shape = (self.num_envs, nfield) if nfield > 1 else (self.num_envs,)
         return torch.as_tensor(_DevArray(ptr, shape, dtype, self), device=f"cuda:{self.cfg.device}")

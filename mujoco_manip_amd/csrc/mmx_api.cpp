@@ -140,8 +140,8 @@ void mmx_config_default(mmx_config* c) {
   c->fixed_task_obj = -1;
   c->fixed_task_bin = -1;
   c->image_size = 224;  // constants.py:23
-  c->solver_iterations = 100;
-  c->solver_tolerance = 1e-5f;
+  c->solver_iterations = 30;
+  c->solver_tolerance = 1e-6f;
 }
 
 int mmx_create(const mmx_config* cfg, mmx_sim** out) {
@@ -180,15 +180,16 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
   }
   S.fixed_obj = cfg->fixed_task_obj;
   S.fixed_bin = cfg->fixed_task_bin;
-  S.pgs_max_iter = cfg->solver_iterations > 0 ? cfg->solver_iterations : 100;
-  S.pgs_tol = cfg->solver_tolerance > 0 ? cfg->solver_tolerance : 1e-5f;
+  S.solver = MMX_SOLVER_NEWTON;
+  S.solver_max_iter = cfg->solver_iterations > 0 ? cfg->solver_iterations : 30;
+  S.solver_tol = cfg->solver_tolerance > 0 ? cfg->solver_tolerance : 1e-6f;
   const size_t n = static_cast<size_t>(N);
   S.qpos = dalloc<float>(sim, MMX_NQ_ * n);
   S.qvel = dalloc<float>(sim, MMX_NV_ * n);
   S.ctrl = dalloc<float>(sim, MMX_NU_ * n);
   S.qacc_ws = dalloc<float>(sim, MMX_NV_ * n);
   S.kin = dalloc<float>(sim, KIN_N * n);
-  S.target = dalloc<float>(sim, 3 * n);
+  S.target = dalloc<float>(sim, 4 * n);
   S.epi = dalloc<int>(sim, EPI_N * n);
   S.epf = dalloc<float>(sim, EPF_N * n);
   S.rng = dalloc<unsigned long long>(sim, 4 * n);
@@ -198,7 +199,6 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
   S.reward_components = dalloc<float>(sim, 6 * n);
   S.done = dalloc<int>(sim, 3 * n);
   S.con = dalloc<float>(sim, static_cast<size_t>(MMX_MAXCON) * CON_F * n);
-  S.efc = dalloc<float>(sim, static_cast<size_t>(MMX_MAXEFC) * EFC_F * n);
   S.stats = dalloc<float>(sim, STAT_N * n);
   sim->expert_action = dalloc<float>(sim, 4 * n);
   sim->d_mask = dalloc<unsigned char>(sim, n);
@@ -208,7 +208,7 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
       mmx_destroy(sim);
       return MMX_ENOMEM;
     }
-  if (!S.qpos || !S.efc || !sim->d_task) {
+  if (!S.qpos || !S.con || !sim->d_task) {
     mmx_destroy(sim);
     return MMX_ENOMEM;
   }
@@ -218,7 +218,7 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
   for (size_t i = 0; i < n; i++) {
     uint64_t st[4];
     pcg64_seed((static_cast<uint64_t>(rd()) << 32) ^ rd(), st);
-    for (int k = 0; k < 4; k++) rng[k * n + i] = st[k];
+    for (int k = 0; k < 4; k++) rng[4 * i + k] = st[k];
   }
   hipMemcpy(S.rng, rng.data(), rng.size() * sizeof(unsigned long long), hipMemcpyHostToDevice);
   *out = sim;
@@ -245,18 +245,18 @@ int mmx_reset(mmx_sim* sim, const uint64_t* seeds, const uint8_t* seed_given, co
     std::vector<unsigned long long> rng(4 * n);
     if (hipMemcpy(rng.data(), S.rng, rng.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
       return fail(sim, MMX_EDEVICE, "rng readback");
-    std::vector<int> has32(n);
-    hipMemcpy(has32.data(), S.epi + static_cast<size_t>(EPI_RNG_HAS32) * n, n * sizeof(int), hipMemcpyDeviceToHost);
+    std::vector<int> epi(EPI_N * n);
+    hipMemcpy(epi.data(), S.epi, epi.size() * sizeof(int), hipMemcpyDeviceToHost);
     for (size_t i = 0; i < n; i++) {
       if (env_mask && !env_mask[i]) continue;
       if (seed_given && !seed_given[i]) continue;
       uint64_t st[4];
       pcg64_seed(seeds[i], st);
-      for (int k = 0; k < 4; k++) rng[k * n + i] = st[k];
-      has32[i] = 0;
+      for (int k = 0; k < 4; k++) rng[4 * i + k] = st[k];
+      epi[EPI_N * i + EPI_RNG_HAS32] = 0;
     }
     hipMemcpy(S.rng, rng.data(), rng.size() * sizeof(unsigned long long), hipMemcpyHostToDevice);
-    hipMemcpy(S.epi + static_cast<size_t>(EPI_RNG_HAS32) * n, has32.data(), n * sizeof(int), hipMemcpyHostToDevice);
+    hipMemcpy(S.epi, epi.data(), epi.size() * sizeof(int), hipMemcpyHostToDevice);
   }
   const unsigned char* dmask = nullptr;
   const int* dtask = nullptr;
@@ -291,9 +291,8 @@ int mmx_expert_plan(mmx_sim* sim, int32_t n_steps, float* action_dev_out) {
 
 int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
   if (!sim || sim->S.action_mode != MMX_ACTION_ABS_POS) return MMX_EINVAL;
-  for (int k = 0; k < n_env_steps; k++) {
-    hipError_t e = mmx_launch_expert(&sim->S, MMX_NSUBSTEP, sim->expert_action, sim->stream);
-    if (e == hipSuccess) e = mmx_launch_step(&sim->S, sim->expert_action, 4, 1, sim->stream);
+  for (int k = 0; k < n_env_steps; k++) {  // the step kernel plans with the FSM itself (expert=1)
+    hipError_t e = mmx_launch_step(&sim->S, sim->expert_action, 4, 1, sim->stream);
     if (e != hipSuccess) return hip_check(sim, e, "mmx_rollout_expert");
   }
   return MMX_OK;

@@ -1,0 +1,456 @@
+// Narrowphase geometry for the MI355X kernels (fp32, one geom pair per lane).
+//
+// Restates MuJoCo's collision functions for the pair classes of this scene:
+// plane-box (corners), plane-convex (support point), box-box (separating-axis test with
+// reference-face clipping, up to 8 points), and the general convex path GJK + EPA (one contact,
+// as MuJoCo 3.x nativeccd without multiccd).  Contacts are emitted through Sink::add(g1, g2,
+// dist, pos, normal) with the normal pointing from geom1 to geom2.
+#ifndef MMX_GEOM_H
+#define MMX_GEOM_H
+#include "mmx_device.h"
+
+enum { GT_PLANE = 0, GT_CYL = 5, GT_BOX = 6, GT_MESH = 7 };
+
+struct Geom {
+  V3 x;
+  M3 R;
+  int type, g;
+};
+
+DEV V3 support(const Geom& G, V3 dir) {
+  V3 dl = mulT(G.R, dir), sl;
+  const int g = G.g;
+  if (G.type == GT_BOX) {
+    sl = V3{dl.x >= 0.f ? MMX_geom_size[3 * g] : -MMX_geom_size[3 * g],
+            dl.y >= 0.f ? MMX_geom_size[3 * g + 1] : -MMX_geom_size[3 * g + 1],
+            dl.z >= 0.f ? MMX_geom_size[3 * g + 2] : -MMX_geom_size[3 * g + 2]};
+  } else if (G.type == GT_CYL) {
+    const float r = MMX_geom_size[3 * g], hh = MMX_geom_size[3 * g + 1];
+    const float n = sqrtf(dl.x * dl.x + dl.y * dl.y);
+    sl = n > 1e-12f ? V3{r * dl.x / n, r * dl.y / n, 0.f} : V3{r, 0.f, 0.f};
+    sl.z = dl.z >= 0.f ? hh : -hh;
+  } else {  // convex hull of a collision mesh (brute-force support over hull vertices)
+    const int m = MMX_geom_mesh[g];
+    const int a = MMX_mesh_vertadr[m], nvert = MMX_mesh_vertnum[m];
+    float best = -3.0e38f;
+    int bi = a;
+    for (int v = a; v < a + nvert; v++) {
+      const float s = MMX_mesh_vert[3 * v] * dl.x + MMX_mesh_vert[3 * v + 1] * dl.y + MMX_mesh_vert[3 * v + 2] * dl.z;
+      if (s > best) {
+        best = s;
+        bi = v;
+      }
+    }
+    sl = V3{MMX_mesh_vert[3 * bi], MMX_mesh_vert[3 * bi + 1], MMX_mesh_vert[3 * bi + 2]};
+  }
+  return G.x + mul(G.R, sl);
+}
+
+DEV bool obb_overlap(const Geom& A, const Geom& B) {
+  const float* ha = &MMX_geom_aabb[3 * A.g];
+  const float* hb = &MMX_geom_aabb[3 * B.g];
+  const V3 d = B.x - A.x;
+#pragma unroll
+  for (int s = 0; s < 2; s++) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      const V3 L = col(s ? B.R : A.R, k);
+      const float r1 = ha[0] * fabsf(dot(L, col(A.R, 0))) + ha[1] * fabsf(dot(L, col(A.R, 1))) + ha[2] * fabsf(dot(L, col(A.R, 2)));
+      const float r2 = hb[0] * fabsf(dot(L, col(B.R, 0))) + hb[1] * fabsf(dot(L, col(B.R, 1))) + hb[2] * fabsf(dot(L, col(B.R, 2)));
+      if (fabsf(dot(d, L)) > r1 + r2) return false;
+    }
+  }
+  return true;
+}
+
+template <class Sink>
+DEV void plane_box(Sink& cs, const Geom& P, const Geom& B) {
+  const V3 nz = col(P.R, 2);
+  const float* h = &MMX_geom_size[3 * B.g];
+  float depth[8];
+  V3 pts[8];
+  int cnt = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const V3 l = V3{(k & 1) ? h[0] : -h[0], (k & 2) ? h[1] : -h[1], (k & 4) ? h[2] : -h[2]};
+    const V3 w = B.x + mul(B.R, l);
+    const float d = dot(w - P.x, nz);
+    if (d <= 0.f) {
+      depth[cnt] = d;
+      pts[cnt] = w - nz * (0.5f * d);
+      cnt++;
+    }
+  }
+  for (int k = 0; k < cnt && k < 4; k++) {  // keep the 4 deepest corners
+    int bi = k;
+    for (int m = k + 1; m < cnt; m++)
+      if (depth[m] < depth[bi]) bi = m;
+    const float td = depth[k];
+    depth[k] = depth[bi];
+    depth[bi] = td;
+    const V3 tp = pts[k];
+    pts[k] = pts[bi];
+    pts[bi] = tp;
+    cs.add(P.g, B.g, depth[k], pts[k], nz);
+  }
+}
+
+template <class Sink>
+DEV void plane_convex(Sink& cs, const Geom& P, const Geom& C) {
+  const V3 nz = col(P.R, 2);
+  const V3 s = support(C, -nz);
+  const float d = dot(s - P.x, nz);
+  if (d <= 0.f) cs.add(P.g, C.g, d, s - nz * (0.5f * d), nz);
+}
+
+DEV int clip_poly(const V3* in, int n, V3* out, V3 a, float b) {
+  int m = 0;
+  for (int k = 0; k < n; k++) {
+    const V3 p = in[k], q = in[(k + 1) % n];
+    const float dp = dot(p, a) - b, dq = dot(q, a) - b;
+    if (dp <= 0.f) out[m++] = p;
+    if ((dp < 0.f && dq > 0.f) || (dp > 0.f && dq < 0.f)) {
+      const float t = dp / (dp - dq);
+      out[m++] = p + (q - p) * t;
+    }
+  }
+  return m;
+}
+
+// box-box: 15-axis SAT; face contacts clip the incident face against the reference face
+// (<= 8 points), edge-edge contacts give one point at the midpoint of the closest points.
+template <class Sink>
+DEV void box_box(Sink& cs, const Geom& G1, const Geom& G2) {
+  const float* h1 = &MMX_geom_size[3 * G1.g];
+  const float* h2 = &MMX_geom_size[3 * G2.g];
+  const V3 A[3] = {col(G1.R, 0), col(G1.R, 1), col(G1.R, 2)};
+  const V3 B[3] = {col(G2.R, 0), col(G2.R, 1), col(G2.R, 2)};
+  const V3 d = G2.x - G1.x;
+  float best_face = 3e38f, best_edge = 3e38f;
+  int face_axis = 0, ei = -1, ej = -1;
+  V3 eL = V3{0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ax = 0; ax < 6; ax++) {
+    const V3 L = ax < 3 ? A[ax] : B[ax - 3];
+    const float r1 = h1[0] * fabsf(dot(L, A[0])) + h1[1] * fabsf(dot(L, A[1])) + h1[2] * fabsf(dot(L, A[2]));
+    const float r2 = h2[0] * fabsf(dot(L, B[0])) + h2[1] * fabsf(dot(L, B[1])) + h2[2] * fabsf(dot(L, B[2]));
+    const float s = r1 + r2 - fabsf(dot(d, L));
+    if (s < 0.f) return;
+    if (s < best_face) {
+      best_face = s;
+      face_axis = ax;
+    }
+  }
+#pragma unroll
+  for (int a = 0; a < 3; a++)
+#pragma unroll
+    for (int b = 0; b < 3; b++) {
+      V3 L = cross(A[a], B[b]);
+      const float ln = norm(L);
+      if (ln < 1e-6f) continue;
+      L = L * (1.0f / ln);
+      const float r1 = h1[0] * fabsf(dot(L, A[0])) + h1[1] * fabsf(dot(L, A[1])) + h1[2] * fabsf(dot(L, A[2]));
+      const float r2 = h2[0] * fabsf(dot(L, B[0])) + h2[1] * fabsf(dot(L, B[1])) + h2[2] * fabsf(dot(L, B[2]));
+      const float s = r1 + r2 - fabsf(dot(d, L));
+      if (s < 0.f) return;
+      if (s < best_edge) {
+        best_edge = s;
+        ei = a;
+        ej = b;
+        eL = L;
+      }
+    }
+  if (ei >= 0 && best_edge < 0.95f * best_face - 1e-9f) {
+    const V3 L = dot(eL, d) < 0.f ? -eL : eL;
+    V3 ca = G1.x, cb = G2.x;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      if (k != ei) ca = ca + A[k] * (dot(A[k], L) >= 0.f ? h1[k] : -h1[k]);
+      if (k != ej) cb = cb + B[k] * (dot(B[k], L) >= 0.f ? -h2[k] : h2[k]);
+    }
+    const V3 ua = A[ei], ub = B[ej], w = ca - cb;
+    const float bb = dot(ua, ub), dd = dot(ua, w), ee = dot(ub, w);
+    const float den = 1.f - bb * bb;
+    float ta = den > 1e-9f ? (bb * ee - dd) / den : 0.f;
+    float tb = den > 1e-9f ? (ee - bb * dd) / den : 0.f;
+    ta = fminf(fmaxf(ta, -h1[ei]), h1[ei]);
+    tb = fminf(fmaxf(tb, -h2[ej]), h2[ej]);
+    cs.add(G1.g, G2.g, -best_edge, ((ca + ua * ta) + (cb + ub * tb)) * 0.5f, L);
+    return;
+  }
+  const bool ref1 = face_axis < 3;
+  const int k = ref1 ? face_axis : face_axis - 3;
+  const V3* Rr = ref1 ? A : B;
+  const V3* Ri = ref1 ? B : A;
+  const float* hr = ref1 ? h1 : h2;
+  const float* hi = ref1 ? h2 : h1;
+  const V3 pr = ref1 ? G1.x : G2.x, pi = ref1 ? G2.x : G1.x;
+  V3 nref = Rr[k];
+  if (dot(nref, pi - pr) < 0.f) nref = -nref;
+  int bj = 0;
+  float bdot = 0.f;
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    const float t = fabsf(dot(Ri[j], nref));
+    if (t > bdot) {
+      bdot = t;
+      bj = j;
+    }
+  }
+  V3 ni = Ri[bj];
+  if (dot(ni, nref) > 0.f) ni = -ni;
+  const V3 ci = pi + ni * hi[bj];
+  const int u = (bj + 1) % 3, v = (bj + 2) % 3;
+  V3 poly[16], tmp[16];
+  int np = 4;
+  poly[0] = ci + Ri[u] * hi[u] + Ri[v] * hi[v];
+  poly[1] = ci - Ri[u] * hi[u] + Ri[v] * hi[v];
+  poly[2] = ci - Ri[u] * hi[u] - Ri[v] * hi[v];
+  poly[3] = ci + Ri[u] * hi[u] - Ri[v] * hi[v];
+  const V3 cr = pr + nref * hr[k];
+  const int ru = (k + 1) % 3, rv = (k + 2) % 3;
+  const V3 ax0 = Rr[ru], ax1 = Rr[rv];
+  np = clip_poly(poly, np, tmp, ax0, dot(ax0, cr) + hr[ru]);
+  np = clip_poly(tmp, np, poly, -ax0, dot(-ax0, cr) + hr[ru]);
+  np = clip_poly(poly, np, tmp, ax1, dot(ax1, cr) + hr[rv]);
+  np = clip_poly(tmp, np, poly, -ax1, dot(-ax1, cr) + hr[rv]);
+  const V3 nout = ref1 ? nref : -nref;
+  for (int c = 0; c < np; c++) {
+    const float depth = -dot(poly[c] - cr, nref);
+    if (depth >= 0.f) cs.add(G1.g, G2.g, -depth, poly[c] + nref * (0.5f * depth), nout);
+  }
+}
+
+// ---------------------------------------------------------------- GJK + EPA
+struct SVx {
+  V3 w, a, b;
+};
+DEV SVx mk_sv(const Geom& A, const Geom& B, V3 dir) {
+  SVx s;
+  s.a = support(A, dir);
+  s.b = support(B, -dir);
+  s.w = s.a - s.b;
+  return s;
+}
+DEV bool gjk_line(SVx* S, int& n, V3& dir) {
+  const V3 ab = S[1].w - S[0].w, ao = -S[0].w;
+  if (dot(ab, ao) > 0.f) {
+    dir = cross(cross(ab, ao), ab);
+    n = 2;
+    return norm(dir) < 1e-12f * (1.f + dot(ab, ab));
+  }
+  n = 1;
+  dir = ao;
+  return false;
+}
+DEV bool gjk_tri(SVx* S, int& n, V3& dir) {
+  const V3 ab = S[1].w - S[0].w, ac = S[2].w - S[0].w, ao = -S[0].w;
+  const V3 abc = cross(ab, ac);
+  if (dot(cross(abc, ac), ao) > 0.f) {
+    if (dot(ac, ao) > 0.f) {
+      S[1] = S[2];
+      n = 2;
+      dir = cross(cross(ac, ao), ac);
+      return false;
+    }
+    n = 2;
+    return gjk_line(S, n, dir);
+  }
+  if (dot(cross(ab, abc), ao) > 0.f) {
+    n = 2;
+    return gjk_line(S, n, dir);
+  }
+  const float dd = dot(abc, ao);
+  n = 3;
+  if (fabsf(dd) < 1e-12f * (1.f + dot(abc, abc))) return true;
+  if (dd > 0.f) dir = abc;
+  else {
+    const SVx t = S[1];
+    S[1] = S[2];
+    S[2] = t;
+    dir = -abc;
+  }
+  return false;
+}
+DEV bool gjk_tet(SVx* S, int& n, V3& dir) {
+  const V3 ao = -S[0].w;
+  const int F[3][3] = {{0, 1, 2}, {0, 2, 3}, {0, 3, 1}};
+  const int O[3] = {3, 1, 2};
+  for (int f = 0; f < 3; f++) {
+    V3 nn = cross(S[F[f][1]].w - S[0].w, S[F[f][2]].w - S[0].w);
+    if (dot(nn, S[O[f]].w - S[0].w) > 0.f) nn = -nn;
+    if (dot(nn, ao) > 0.f) {
+      const SVx t0 = S[F[f][0]], t1 = S[F[f][1]], t2 = S[F[f][2]];
+      S[0] = t0;
+      S[1] = t1;
+      S[2] = t2;
+      n = 3;
+      return gjk_tri(S, n, dir);
+    }
+  }
+  n = 4;
+  return true;
+}
+DEV bool gjk(const Geom& A, const Geom& B, SVx* S, int& n) {
+  V3 dir = A.x - B.x;
+  if (norm(dir) < 1e-9f) dir = V3{1.f, 0.f, 0.f};
+  S[0] = mk_sv(A, B, dir);
+  n = 1;
+  dir = -S[0].w;
+  for (int it = 0; it < 48; it++) {
+    if (norm(dir) < 1e-12f) return true;
+    const SVx P = mk_sv(A, B, dir);
+    if (dot(P.w, dir) < 0.f) return false;
+    for (int k = n; k > 0; k--) S[k] = S[k - 1];
+    S[0] = P;
+    n++;
+    const bool hit = n == 2 ? gjk_line(S, n, dir) : (n == 3 ? gjk_tri(S, n, dir) : gjk_tet(S, n, dir));
+    if (hit) return true;
+  }
+  return norm(dir) < 1e-12f;
+}
+
+#define EPA_MAXV 40
+#define EPA_MAXF 80
+struct EFace {
+  int v0, v1, v2;
+  V3 n;
+  float d;
+};
+DEV bool epa_face(const SVx* V, EFace& f, int a, int b, int c) {
+  f.v0 = a;
+  f.v1 = b;
+  f.v2 = c;
+  const V3 n = cross(V[b].w - V[a].w, V[c].w - V[a].w);
+  const float ln = norm(n);
+  if (ln < 1e-20f) return false;
+  f.n = n * (1.f / ln);
+  f.d = dot(f.n, V[a].w);
+  return true;
+}
+DEV bool epa(const Geom& A, const Geom& B, SVx* V, int nv, V3& nrm, float& depth, V3& pa, V3& pb) {
+  EFace F[EPA_MAXF];
+  int nf = 0;
+  const V3 dirs[6] = {V3{1.f, 0.f, 0.f}, V3{-1.f, 0.f, 0.f}, V3{0.f, 1.f, 0.f},
+                      V3{0.f, -1.f, 0.f}, V3{0.f, 0.f, 1.f}, V3{0.f, 0.f, -1.f}};
+  if (nv == 1) {
+    for (int k = 0; k < 6 && nv < 2; k++) {
+      V[nv] = mk_sv(A, B, dirs[k]);
+      if (norm(V[nv].w - V[0].w) > 1e-7f) nv++;
+    }
+  }
+  if (nv == 2) {
+    const V3 ab = V[1].w - V[0].w;
+    const V3 ax = fabsf(ab.x) <= fabsf(ab.y) && fabsf(ab.x) <= fabsf(ab.z)
+                      ? V3{1.f, 0.f, 0.f}
+                      : (fabsf(ab.y) <= fabsf(ab.z) ? V3{0.f, 1.f, 0.f} : V3{0.f, 0.f, 1.f});
+    const V3 t = normalize(cross(ab, ax));
+    V[2] = mk_sv(A, B, t);
+    if (norm(cross(V[2].w - V[0].w, ab)) < 1e-10f) V[2] = mk_sv(A, B, -t);
+    nv = 3;
+  }
+  if (nv == 3) {
+    const V3 n = normalize(cross(V[1].w - V[0].w, V[2].w - V[0].w));
+    V[3] = mk_sv(A, B, n);
+    if (fabsf(dot(V[3].w - V[0].w, n)) < 1e-9f) V[3] = mk_sv(A, B, -n);
+    nv = 4;
+  }
+  const int T[4][3] = {{0, 1, 2}, {0, 3, 1}, {0, 2, 3}, {1, 3, 2}};
+  const V3 cen = (V[0].w + V[1].w + V[2].w + V[3].w) * 0.25f;
+  for (int k = 0; k < 4; k++) {
+    if (!epa_face(V, F[nf], T[k][0], T[k][1], T[k][2])) continue;
+    if (dot(F[nf].n, V[T[k][0]].w - cen) < 0.f) epa_face(V, F[nf], T[k][0], T[k][2], T[k][1]);
+    nf++;
+  }
+  int best = -1;
+  for (int it = 0; it < 32; it++) {
+    best = -1;
+    float bd = 3e38f;
+    for (int k = 0; k < nf; k++)
+      if (F[k].d < bd) {
+        bd = F[k].d;
+        best = k;
+      }
+    if (best < 0) return false;
+    const SVx P = mk_sv(A, B, F[best].n);
+    const float dist = dot(P.w, F[best].n);
+    if (dist - F[best].d < 1e-6f * (1.f + fabsf(dist)) || nv >= EPA_MAXV) break;
+    int edges[EPA_MAXF * 3][2];
+    int ne = 0, m = 0;
+    for (int k = 0; k < nf; k++) {
+      const EFace f = F[k];
+      if (dot(f.n, P.w - V[f.v0].w) > 1e-9f) {
+        const int vv[3] = {f.v0, f.v1, f.v2};
+        for (int e = 0; e < 3; e++) {
+          const int a = vv[e], b = vv[(e + 1) % 3];
+          int found = -1;
+          for (int q = 0; q < ne; q++)
+            if (edges[q][0] == b && edges[q][1] == a) {
+              found = q;
+              break;
+            }
+          if (found >= 0) {
+            edges[found][0] = edges[ne - 1][0];
+            edges[found][1] = edges[ne - 1][1];
+            ne--;
+          } else if (ne < EPA_MAXF * 3) {
+            edges[ne][0] = a;
+            edges[ne][1] = b;
+            ne++;
+          }
+        }
+      } else {
+        F[m++] = f;
+      }
+    }
+    nf = m;
+    const int pi = nv++;
+    V[pi] = P;
+    for (int q = 0; q < ne && nf < EPA_MAXF; q++)
+      if (epa_face(V, F[nf], edges[q][0], edges[q][1], pi)) nf++;
+  }
+  if (best < 0) return false;
+  const EFace& f = F[best];
+  const V3 p = f.n * f.d;
+  const V3 v0 = V[f.v1].w - V[f.v0].w, v1 = V[f.v2].w - V[f.v0].w, v2 = p - V[f.v0].w;
+  const float d00 = dot(v0, v0), d01 = dot(v0, v1), d11 = dot(v1, v1), d20 = dot(v2, v0), d21 = dot(v2, v1);
+  const float den = d00 * d11 - d01 * d01;
+  const float lv = den > 1e-30f ? (d11 * d20 - d01 * d21) / den : 0.f;
+  const float lw = den > 1e-30f ? (d00 * d21 - d01 * d20) / den : 0.f;
+  const float lu = 1.f - lv - lw;
+  pa = V[f.v0].a * lu + V[f.v1].a * lv + V[f.v2].a * lw;
+  pb = V[f.v0].b * lu + V[f.v1].b * lv + V[f.v2].b * lw;
+  nrm = f.n;
+  depth = f.d;
+  return true;
+}
+
+template <class Sink>
+DEV void convex_convex(Sink& cs, const Geom& A, const Geom& B) {
+  SVx V[EPA_MAXV];
+  int n = 0;
+  if (!gjk(A, B, V, n)) return;
+  V3 nrm, pa, pb;
+  float depth;
+  if (!epa(A, B, V, n, nrm, depth, pa, pb)) return;
+  if (depth < 0.f) return;
+  // Minkowski A-B face normal n: translating B by +depth n separates -> normal A->B is n
+  cs.add(A.g, B.g, -depth, (pa + pb) * 0.5f, nrm);
+}
+
+// soft-constraint impedance d(pos) (MuJoCo solimp: dmin, dmax, width, midpoint, power)
+DEV float impedance(const float* si, float pos) {
+  const float dmin = fminf(fmaxf(si[0], 1e-4f), 0.9999f), dmax = fminf(fmaxf(si[1], 1e-4f), 0.9999f);
+  const float width = si[2], mid = si[3], power = si[4];
+  if (dmin == dmax || width <= 1e-15f) return 0.5f * (dmin + dmax);
+  const float x = fabsf(pos / width);
+  if (x >= 1.f) return dmax;
+  if (x <= 0.f) return dmin;
+  float y;
+  if (power == 1.f) y = x;
+  else if (x <= mid) y = powf(x, power) / powf(mid, power - 1.f);
+  else y = 1.f - powf(1.f - x, power) / powf(1.f - mid, power - 1.f);
+  return dmin + y * (dmax - dmin);
+}
+
+#endif

@@ -26,8 +26,8 @@ class PickPlaceVecEnv:
                  action_mode: str = "ee_pos_quat_g_rel", reward_type: str = "dense", image_size: int = IMAGE_SIZE,
                  render_mode: str | None = None, max_episode_steps: int = MAX_EPISODE_STEPS,
                  randomize_objects: bool = False, spawn_x_range=(-0.20, 0.20), spawn_y_range=(0.30, 0.45),
-                 autoreset: bool = False, device: int = 0, solver_iterations: int = 100,
-                 solver_tolerance: float = 1e-5):
+                 autoreset: bool = False, device: int = 0, solver_iterations: int = 30,
+                 solver_tolerance: float = 1e-6):
         if not torch.cuda.is_available():
             raise RuntimeError("PickPlaceVecEnv needs an MI355X GPU (HIP); no CPU fallback exists")
         pool = TASK_SETS[tasks] if isinstance(tasks, str) else list(tasks)
@@ -63,7 +63,7 @@ class PickPlaceVecEnv:
 
     # ------------------------------------------------------------------ gym API
     def _obs_dict(self):
-        flat = self._obs.t()
+        flat = self._obs
         out = {}
         for k, (a, b, shape) in OBS_SLICES.items():
             out[k] = flat[:, a:b].reshape(self.num_envs, *shape).clone()
@@ -95,11 +95,11 @@ class PickPlaceVecEnv:
         self.sim.step(a.data_ptr(), a.shape[1])
         obs = self._obs_dict()
         reward = self._reward.clone()
-        terminated = self._done[0].bool().clone()
-        truncated = self._done[1].bool().clone()
-        info = {"success": self._done[2].bool().clone()}
+        terminated = self._done[:, 0].bool().clone()
+        truncated = self._done[:, 1].bool().clone()
+        info = {"success": self._done[:, 2].bool().clone()}
         if self._reward_type == "staged":
-            info["reward_components"] = self._rc.t().clone()
+            info["reward_components"] = self._rc.clone()
         self._last_action = a
         return obs, reward, terminated, truncated, info
 
@@ -115,32 +115,41 @@ class PickPlaceVecEnv:
 
     @property
     def step_count(self) -> torch.Tensor:
-        return self._epi[2].clone()
+        return self._epi[:, 2].clone()
 
     @property
     def tasks(self) -> list[tuple[str, str]]:
-        ob = self._epi[0].cpu().numpy()
-        bn = self._epi[1].cpu().numpy()
+        ob = self._epi[:, 0].cpu().numpy()
+        bn = self._epi[:, 1].cpu().numpy()
         return [(OBJECTS[o], BINS[b]) for o, b in zip(ob, bn)]
 
     @property
     def fsm_state(self) -> torch.Tensor:
-        return self._epi[4].clone()
+        return self._epi[:, 4].clone()
+
+    @property
+    def episode_flags(self) -> torch.Tensor:
+        """staged-reward sticky flags: 1 grasped, 2 lifted, 4 above target, 8 placed"""
+        return self._epi[:, 3].clone()
+
+    @property
+    def env_error(self) -> torch.Tensor:
+        return self._epi[:, 9].clone()
 
     @property
     def initial_ee_se3(self) -> torch.Tensor:
         T = torch.zeros(self.num_envs, 4, 4, device=self.device)
-        f = self._epf.t()
+        f = self._epf
         T[:, :3, :3] = f[:, 0:9].reshape(-1, 3, 3)
         T[:, :3, 3] = f[:, 9:12]
         T[:, 3, 3] = 1.0
         return T
 
     def solver_stats(self) -> dict:
-        s = self.stats.double().sum(dim=1).cpu().numpy()
+        s = self.stats.double().sum(dim=0).cpu().numpy()
         sub = max(s[3], 1.0)
-        return {"mean_nefc": s[0] / sub, "mean_ncon": s[1] / sub, "mean_pgs_iter": s[2] / sub,
-                "max_resid": float(self.stats[4].max().item())}
+        return {"mean_nefc": s[0] / sub, "mean_ncon": s[1] / sub, "mean_solver_iter": s[2] / sub,
+                "max_resid": float(self.stats[:, 4].max().item())}
 
     def clear_stats(self):
         self.stats.zero_()

@@ -1,0 +1,73 @@
+"""C-ABI boundary checks that need no GPU: libmmx.so loads, exports every symbol declared in
+include/mmx_api.h, and its host-side seeding matches numpy (scripts/generate_dataset.py:263-268)."""
+import os
+import re
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    src = open(os.path.join(REPO, "include", "mmx_api.h")).read()
+    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*|uint32_t)\s+(mmx_\w+)\s*\(", src, re.M)))
+
+
+def test_library_exports_every_declared_symbol():
+    from mujoco_manip_amd import _lib
+
+    L = _lib.load()
+    names = declared_functions()
+    assert len(names) >= 14
+    for n in names:
+        assert hasattr(L, n), f"libmmx.so does not export {n}"
+    assert set(names) == set(_lib.EXPORTED)
+
+
+def test_episode_seed_matches_numpy():
+    from mujoco_manip_amd import _lib
+
+    ss = np.random.SeedSequence(42)
+    ref = [int(c.generate_state(1)[0]) for c in ss.spawn(64)]
+    assert [_lib.episode_seed(42, i) for i in range(64)] == ref
+    ss = np.random.SeedSequence(2**40 + 3)
+    assert [_lib.episode_seed(2**40 + 3, i) for i in range(8)] == [int(c.generate_state(1)[0]) for c in ss.spawn(8)]
+
+
+def test_create_fails_cleanly_without_gpu_or_with_bad_args():
+    import ctypes as C
+
+    from mujoco_manip_amd import _lib
+
+    L = _lib.load()
+    cfg = _lib.MMXConfig()
+    L.mmx_config_default(C.byref(cfg))
+    assert cfg.max_episode_steps == 500 and cfg.n_tasks == 9 and cfg.image_size == 224
+    cfg.action_mode = 7  # invalid -> MMX_EINVAL, never aborts (ValueError in the reference)
+    ptr = C.c_void_p()
+    assert L.mmx_create(C.byref(cfg), C.byref(ptr)) == -1
+    assert not ptr.value
+
+
+def test_state_layout_constants_match_header():
+    src = open(os.path.join(REPO, "mujoco_manip_amd", "csrc", "mmx_state.h")).read()
+    from mujoco_manip_amd import _lib
+
+    assert f"#define MMX_MAXCON {_lib.MAXCON}" in src
+    assert "KIN_N = 54" in src and _lib.KIN_N == 54
+    assert len(_lib.EPI_FIELDS) == _lib.EPI_N
+
+
+def test_obs_layout_covers_reference_keys():
+    from mujoco_manip_amd.constants import OBS_SLICES
+
+    # gym_env.py:172-208 observation keys minus the two camera images
+    keys = {"state", "state.ee.pos_quat_g", "state.ee.pos_rot6d_g", "state.ee.pos_quat_g_rel",
+            "state.ee.pos_rot6d_g_rel", "target_bin_onehot", "target_obj_onehot", "keypoints_overhead",
+            "keypoints_wrist", "target_obj_keypoints_overhead", "target_bin_keypoints_overhead"}
+    assert set(OBS_SLICES) == keys
+    end = 0
+    for k, (a, b, shape) in OBS_SLICES.items():
+        assert a == end and int(np.prod(shape)) == b - a
+        end = b
+    assert end == 85

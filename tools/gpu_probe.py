@@ -41,26 +41,29 @@ def physics_parity(n_sub):
     sts = states_from_oracle_rollout(64)
     N = len(sts)
     sim = _lib.Sim(N)
-    qpos = np.stack([s[0] for s in sts], 1).astype(np.float32)
-    qvel = np.stack([s[1] for s in sts], 1).astype(np.float32)
-    ctrl = np.stack([s[2] for s in sts], 1).astype(np.float32)
-    ws = np.stack([s[3] for s in sts], 1).astype(np.float32)
+    qpos = np.stack([s[0] for s in sts], 0).astype(np.float32)
+    qvel = np.stack([s[1] for s in sts], 0).astype(np.float32)
+    ctrl = np.stack([s[2] for s in sts], 0).astype(np.float32)
+    ws = np.stack([s[3] for s in sts], 0).astype(np.float32)
     sim.set_state(qpos, qvel, ctrl, ws)
     sim.physics_step(n_sub, with_ik=False)
     gq, gv, _, _ = sim.get_state()
-    dq, dv = [], []
+    dq, dv, nefc_o = [], [], []
     for k, s in enumerate(sts):
         e = O.OracleEnv()
-        e.set_state(qpos[:, k].astype(float), qvel[:, k].astype(float), ctrl[:, k].astype(float), ws[:, k].astype(float))
+        e.set_state(qpos[k].astype(float), qvel[k].astype(float), ctrl[k].astype(float), ws[k].astype(float))
         for _ in range(n_sub):
             e.mj_step()
         rq, rv, _, _ = e.get_state()
-        dq.append(np.abs(gq[:, k] - rq).max())
-        dv.append(np.abs(gv[:, k] - rv).max())
+        dq.append(np.abs(gq[k] - rq).max())
+        dv.append(np.abs(gv[k] - rv).max())
+        nefc_o.append(e.nefc())
     st = sim.view("stats", _lib.STAT_N).double().cpu().numpy()
+    epi = sim.view("episode_i", _lib.EPI_N, "<i4").cpu().numpy()
     return {"max_dqpos": float(max(dq)), "max_dqvel": float(max(dv)), "per_state_dq": [float(x) for x in dq],
-            "per_state_dv": [float(x) for x in dv], "mean_nefc": float(st[0].sum() / max(st[3].sum(), 1)),
-            "mean_pgs_iter": float(st[2].sum() / max(st[3].sum(), 1)), "max_resid": float(st[4].max())}
+            "per_state_dv": [float(x) for x in dv], "mean_nefc": float(st[:, 0].sum() / max(st[:, 3].sum(), 1)),
+            "nefc_gpu_last": epi[:, 11].tolist(), "nefc_oracle_last": nefc_o,
+            "mean_solver_iter": float(st[:, 2].sum() / max(st[:, 3].sum(), 1)), "max_resid": float(st[:, 4].max())}
 
 
 def gym_parity(steps=30, mode="abs_pos"):
@@ -73,7 +76,7 @@ def gym_parity(steps=30, mode="abs_pos"):
     robs = np.stack([r.reset(seed=100 + k) for k, r in enumerate(refs)])
     flat = lambda o: torch.cat([o[k].reshape(N, -1) for k in o], 1).cpu().numpy()  # noqa: E731
     d0 = np.abs(flat(obs) - robs).max(0)
-    tasks_match = [tuple(refs[k].task()) for k in range(N)] == [(int(a), int(b)) for a, b in zip(env._epi[0].cpu(), env._epi[1].cpu())]
+    tasks_match = [tuple(refs[k].task()) for k in range(N)] == [(int(a), int(b)) for a, b in zip(env._epi[:, 0].cpu(), env._epi[:, 1].cpu())]
     errs = []
     for t in range(steps):
         act = env.expert_plan(16)
@@ -90,24 +93,41 @@ def expert_success(N=256, steps=150):
     env = PickPlaceVecEnv(N, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True)
     env.reset(seed=0)
     t = time.time()
-    succ = torch.zeros(N, dtype=torch.bool, device="cuda")
+    placed = torch.zeros(N, dtype=torch.bool, device="cuda")
     done_at = torch.full((N,), -1, device="cuda")
     for k in range(steps):
         act = env.expert_plan(16)
         obs, r, term, trunc, info = env.step(act)
-        succ |= info["success"]
+        placed |= (env.episode_flags & 8) != 0
         fsm_done = env.fsm_state == 10
         done_at = torch.where((done_at < 0) & fsm_done, torch.full_like(done_at, k), done_at)
     torch.cuda.synchronize()
-    return {"success_rate": float(succ.float().mean()), "fsm_done_rate": float((done_at >= 0).float().mean()),
+    return {"placed_rate": float(placed.float().mean()), "fsm_done_rate": float((done_at >= 0).float().mean()),
             "mean_done_step": float(done_at[done_at >= 0].float().mean()) if (done_at >= 0).any() else -1,
+            "env_error": int((env.env_error != 0).sum()),
+            "env_error_bits": {str(b): int(((env.env_error & b) != 0).sum()) for b in (1, 2, 4, 8)},
             "secs": time.time() - t, "solver": env.solver_stats()}
+
+
+def rollout_speed(N=4096, steps=20):
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    env = PickPlaceVecEnv(N, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
+                          autoreset=True)
+    env.reset(seed=[_lib.episode_seed(42, i) for i in range(N)])
+    env.rollout_expert(2)
+    torch.cuda.synchronize()
+    t = time.time()
+    env.rollout_expert(steps)
+    torch.cuda.synchronize()
+    dt = time.time() - t
+    return {"env_steps_per_s": N * steps / dt, "ms_per_step": 1000 * dt / steps, "solver": env.solver_stats()}
 
 
 if __name__ == "__main__":
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     for name, fn in [("phys1", lambda: physics_parity(1)), ("phys16", lambda: physics_parity(16)),
-                     ("gym", gym_parity), ("expert", expert_success)]:
+                     ("gym", gym_parity), ("expert", expert_success), ("speed", rollout_speed)]:
         t = time.time()
         try:
             out[name] = fn()
