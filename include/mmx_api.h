@@ -45,8 +45,8 @@ typedef struct {
   int32_t reward_type;          /* MMX_REWARD_* */
   int32_t max_episode_steps;    /* truncation limit (constants.py:27) */
   int32_t randomize_objects;    /* randomization.py on reset */
-  float spawn_x_range[2];
-  float spawn_y_range[2];
+  double spawn_x_range[2];      /* fp64: the spawn draws are numpy-identical fp64 */
+  double spawn_y_range[2];
   int32_t n_tasks;              /* task pool (constants.py:11-25), objects/bins 0=red 1=green 2=blue */
   int8_t task_obj[9];
   int8_t task_bin[9];

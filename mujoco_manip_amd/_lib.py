@@ -30,7 +30,7 @@ class MMXConfig(C.Structure):
     _fields_ = [
         ("num_envs", C.c_int32), ("device", C.c_int32), ("action_mode", C.c_int32), ("reward_type", C.c_int32),
         ("max_episode_steps", C.c_int32), ("randomize_objects", C.c_int32),
-        ("spawn_x_range", C.c_float * 2), ("spawn_y_range", C.c_float * 2),
+        ("spawn_x_range", C.c_double * 2), ("spawn_y_range", C.c_double * 2),
         ("n_tasks", C.c_int32), ("task_obj", C.c_int8 * 9), ("task_bin", C.c_int8 * 9),
         ("fixed_task_obj", C.c_int32), ("fixed_task_bin", C.c_int32), ("image_size", C.c_int32),
         ("autoreset", C.c_int32), ("solver_iterations", C.c_int32), ("solver_tolerance", C.c_float),

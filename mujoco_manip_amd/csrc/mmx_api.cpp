@@ -128,10 +128,10 @@ void mmx_config_default(mmx_config* c) {
   c->action_mode = MMX_ACTION_EE_POS_QUAT_G_REL;  // gym_env.py:67
   c->reward_type = MMX_REWARD_DENSE;              // gym_env.py:68
   c->max_episode_steps = 500;                     // constants.py:27
-  c->spawn_x_range[0] = -0.20f;
-  c->spawn_x_range[1] = 0.20f;
-  c->spawn_y_range[0] = 0.30f;
-  c->spawn_y_range[1] = 0.45f;
+  c->spawn_x_range[0] = -0.20;
+  c->spawn_x_range[1] = 0.20;
+  c->spawn_y_range[0] = 0.30;
+  c->spawn_y_range[1] = 0.45;
   c->n_tasks = 9;  // "all" (constants.py:19)
   for (int k = 0; k < 9; k++) {
     c->task_obj[k] = static_cast<int8_t>(k / 3);

@@ -59,7 +59,7 @@ struct MMXState {
   int N;
   // configuration (gym_env.py:62-75 constructor arguments)
   int action_mode, reward_type, max_episode_steps, randomize, image_size, autoreset;
-  float spawn_x0, spawn_x1, spawn_y0, spawn_y1;
+  double spawn_x0, spawn_x1, spawn_y0, spawn_y1;
   int ntask, task_obj[9], task_bin[9], fixed_obj, fixed_bin;
   int solver, solver_max_iter;
   float solver_tol;

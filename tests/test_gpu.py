@@ -1,0 +1,269 @@
+"""GPU parity and behavioural tests (MI355X only), all through the C-ABI library libmmx.so.
+
+Parity tiers (tolerances stated per test):
+  L0  reset / RNG / observation codecs vs the fp64 oracle: fp32 rounding only;
+  L1  physics (IK + CRBA/RNE + contacts + Newton + implicitfast) one substep and one env step
+      (16 substeps) from states sampled along an oracle expert episode, incl. grasps;
+  L2  multi-step env parity with expert actions, all 5 action modes;
+  L3  the reference's own behavioural thresholds (tests/test_controller.py, test_gym_env.py,
+      test_pick_and_place.py) run on the GPU batch.
+The oracle is the checker only; every value under test comes out of the HIP kernels.
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _require_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs an MI355X")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    _require_gpu()
+    from mujoco_manip_amd import _lib
+
+    _lib.load(build_if_missing=False)  # the native library must be the one under test
+
+
+TARGET_ORI = np.array([[0, 1, 0], [1, 0, 0], [0, 0, -1.0]])
+
+
+def oracle_states(n=40):
+    import oracle_py as O
+
+    e = O.OracleEnv()
+    e.reset_keyframe()
+    e.fsm_init([(0, 0)])
+    states = []
+    for _ in range(200):
+        st = e.fsm_plan(16)
+        e.fsm_actuate()
+        for _ in range(16):
+            e.mj_step()
+        states.append(e.get_state())
+        if st == 10:
+            break
+    idx = np.linspace(0, len(states) - 1, n).astype(int)
+    return [states[i] for i in idx]
+
+
+def _physics_parity(nsub):
+    import oracle_py as O
+    from mujoco_manip_amd import _lib
+
+    sts = oracle_states()
+    qpos, qvel, ctrl, ws = [np.stack([s[k] for s in sts]).astype(np.float32) for k in range(4)]
+    sim = _lib.Sim(len(sts))
+    sim.set_state(qpos, qvel, ctrl, ws)
+    sim.physics_step(nsub)
+    gq, gv, _, _ = sim.get_state()
+    err_q, err_v = [], []
+    for k in range(len(sts)):
+        e = O.OracleEnv()
+        e.set_state(*(a[k].astype(float) for a in (qpos, qvel, ctrl, ws)))
+        for _ in range(nsub):
+            e.mj_step()
+        rq, rv, _, _ = e.get_state()
+        err_q.append(np.abs(gq[k] - rq).max())
+        err_v.append(np.abs(gv[k] - rv).max())
+    errs = sim.view("episode_i", _lib.EPI_N, "<i4")[:, 9].cpu().numpy()
+    assert (errs == 0).all(), "contact/row capacity overflow or NaN"
+    return np.array(err_q), np.array(err_v)
+
+
+def test_physics_parity_one_substep():  # L1: fp32 GPU vs fp64 oracle, contacts incl. grasps
+    dq, dv = _physics_parity(1)
+    assert dq.max() < 1e-5, dq.max()
+    assert dv.max() < 5e-3, dv.max()
+
+
+def test_physics_parity_one_env_step():  # L1: 16 substeps; SURVEY bound qpos <= 1e-4
+    dq, dv = _physics_parity(16)
+    assert dq.max() < 1e-4, dq.max()
+    assert dv.max() < 2e-2, dv.max()
+
+
+def _flat(obs, n):
+    return torch.cat([obs[k].reshape(n, -1) for k in obs], 1).cpu().numpy()
+
+
+def test_reset_parity_randomized_seeds():  # L0: PCG64 stream, spawn, task draw, obs codecs
+    import oracle_py as O
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    N = 16
+    seeds = [O.episode_seed(42, i) for i in range(N)]
+    env = PickPlaceVecEnv(N, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True)
+    obs, _ = env.reset(seed=seeds)
+    refs = [O.OracleEnv(action_mode="abs_pos", reward_type="staged", randomize_objects=True) for _ in range(N)]
+    robs = np.stack([r.reset(seed=s) for r, s in zip(refs, seeds)])
+    np.testing.assert_allclose(_flat(obs, N), robs, atol=2e-6)
+    assert [tuple(r.task()) for r in refs] == [(o, b) for o, b in env._epi[:, :2].cpu().numpy().tolist()]
+    ref_q = np.stack([r.get_state()[0] for r in refs])
+    np.testing.assert_array_equal(env.qpos.cpu().numpy()[:, 9:30], ref_q[:, 9:30].astype(np.float32))
+
+
+@pytest.mark.parametrize("mode", ["abs_pos", "ee_pos_quat_g", "ee_pos_rot6d_g", "ee_pos_quat_g_rel", "ee_pos_rot6d_g_rel"])
+def test_env_step_parity_action_modes(mode):  # L2: decode + 16 x (IK + mj_step) + forward + obs
+    import oracle_py as O
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    N = 4
+    rng = np.random.default_rng(7)
+    env = PickPlaceVecEnv(N, task=("obj_red", "bin_red"), action_mode=mode, reward_type="dense")
+    env.reset(seed=0)
+    refs = [O.OracleEnv(action_mode=mode, reward_type="dense", task=(0, 0)) for _ in range(N)]
+    for k, r in enumerate(refs):
+        r.reset(seed=k)
+    dim = env.action_dim
+    for t in range(6):
+        a = np.zeros((N, dim), np.float32)
+        a[:, :3] = rng.uniform(-0.05, 0.05, (N, 3)) + ([0.0, 0.45, 0.42] if "rel" not in mode else 0.0)
+        if dim >= 8:
+            a[:, 3:7] = [0, 0, 0, 1] if "quat" in mode else [1, 0, 0, 0]
+        if dim == 10:
+            a[:, 3:9] = [1, 0, 0, 0, 1, 0]
+        a[:, -1] = float(t % 2)
+        obs, rew, term, trunc, info = env.step(torch.tensor(a, device="cuda"))
+        got = _flat(obs, N)
+        for k, r in enumerate(refs):
+            ro, rr, rt, rtr, ri = r.step(a[k])
+            np.testing.assert_allclose(got[k, :11], ro[:11], atol=1e-4)
+            assert abs(float(rew[k]) - rr) < 1e-3
+
+
+def test_expert_rollout_parity_and_completion():  # L2 + L3 (test_pick_and_place.py:274-289)
+    import oracle_py as O
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    N = 18
+    seeds = [O.episode_seed(7, i) for i in range(N)]
+    env = PickPlaceVecEnv(N, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True)
+    env.reset(seed=seeds)
+    done_at = np.full(N, -1)
+    placed = np.zeros(N, bool)
+    first_err = []
+    refs = [O.OracleEnv(action_mode="abs_pos", reward_type="staged", randomize_objects=True) for _ in range(2)]
+    for r, s in zip(refs, seeds[:2]):
+        r.reset(seed=s)
+    for t in range(200):
+        act = env.expert_plan(16)
+        obs, rew, term, trunc, info = env.step(act)
+        if t < 5:  # early steps: trajectories still comparable to the oracle
+            a = act.cpu().numpy()
+            for k, r in enumerate(refs):
+                ro = r.step(a[k])[0]
+                first_err.append(np.abs(obs["state"][k].cpu().numpy() - ro[:11]).max())
+        placed |= ((env.episode_flags & 8) != 0).cpu().numpy()
+        fsm = env.fsm_state.cpu().numpy()
+        done_at[(done_at < 0) & (fsm == 10)] = t
+        if (done_at >= 0).all():
+            break
+    assert max(first_err) < 1e-4
+    assert (done_at >= 0).all(), f"FSM unfinished: {np.where(done_at < 0)[0]}"
+    assert done_at.max() < 2000  # reference KAT: <= 2000 gym steps
+    assert placed.all()
+    assert (env.env_error.cpu().numpy() == 0).all()
+
+
+def test_ik_convergence_kat():  # tests/test_controller.py:84-139 on the GPU batch
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    targets = np.array([[0.0, 0.4, 0.4], [-0.15, 0.45, 0.36], [-0.3, 0.55, 0.45]], np.float32)
+    env = PickPlaceVecEnv(3, task=("obj_red", "bin_red"), action_mode="abs_pos")
+    env.reset(seed=0)
+    a = torch.tensor(np.concatenate([targets, np.ones((3, 1), np.float32)], 1), device="cuda")
+    for _ in range(13):  # 208 x (IK + mj_step) >= the reference's 200
+        obs, *_ = env.step(a)
+    ee = obs["state"][:, :3].cpu().numpy()
+    assert (np.linalg.norm(ee - targets, axis=1) < 0.03).all()
+    q = obs["state.ee.pos_quat_g"][:, 3:7].cpu().numpy()
+    for k in range(3):
+        x, y, z, w = q[k]
+        R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                      [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                      [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+        np.testing.assert_allclose(R, TARGET_ORI, atol=0.1)
+
+
+def test_gym_kats_relative_and_absolute():  # tests/test_gym_env.py:258-339, 622-687
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    env = PickPlaceVecEnv(2, task=("obj_red", "bin_red"), action_mode="ee_pos_quat_g_rel", max_episode_steps=50)
+    env.reset(seed=0)
+    T0 = env.initial_ee_se3.cpu().numpy()
+    ident = torch.tensor([[0, 0, 0, 0, 0, 0, 1, 1]] * 2, dtype=torch.float32, device="cuda")
+    for _ in range(5):
+        obs, *_ = env.step(ident)
+    assert (np.linalg.norm(obs["state"][:, :3].cpu().numpy() - T0[:, :3, 3], axis=1) < 0.05).all()
+    move = torch.tensor([[0.1, 0, 0, 0, 0, 0, 1, 1]] * 2, dtype=torch.float32, device="cuda")
+    for _ in range(20):
+        obs, *_ = env.step(move)
+    want = (T0 @ np.array([0.1, 0, 0, 1.0]))[:, :3]
+    assert (np.linalg.norm(obs["state"][:, :3].cpu().numpy() - want, axis=1) < 0.05).all()
+    env = PickPlaceVecEnv(1, task=("obj_red", "bin_red"), action_mode="abs_pos")
+    env.reset(seed=0)
+    a = torch.tensor([[0.0, 0.4, 0.45, 1.0]], device="cuda")
+    for _ in range(20):
+        obs, *_ = env.step(a)
+    assert np.linalg.norm(obs["state"][0, :3].cpu().numpy() - [0.0, 0.4, 0.45]) < 0.05
+
+
+def test_staged_collision_penalty():  # gym_env.py:428-430 ; tests/test_gym_env.py:868-876
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    env = PickPlaceVecEnv(1, task=("obj_red", "bin_red"), action_mode="abs_pos", reward_type="staged")
+    env.reset(seed=0)
+    a = torch.tensor([[0.25, 0.35, 0.05, 1.0]], device="cuda")  # drive the hand into the tabletop
+    hit = False
+    for _ in range(60):
+        obs, rew, term, trunc, info = env.step(a)
+        if float(rew[0]) == -1.0:
+            hit = True
+            assert bool(term[0]) and not bool(info["success"][0])
+            break
+    assert hit
+
+
+def test_determinism_and_shard_independence():
+    import oracle_py as O
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    seeds = [O.episode_seed(42, i) for i in range(8)]
+    outs = []
+    for ss in (seeds, seeds, seeds[4:]):
+        env = PickPlaceVecEnv(len(ss), tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True)
+        env.reset(seed=ss)
+        for _ in range(8):
+            obs, *_ = env.step(env.expert_plan(16))
+        outs.append(_flat(obs, len(ss)))
+    np.testing.assert_array_equal(outs[0], outs[1])  # bit-identical reruns
+    np.testing.assert_array_equal(outs[0][4:], outs[2])  # result independent of batch composition
+
+
+def test_autoreset_and_truncation():
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    env = PickPlaceVecEnv(4, tasks="all", action_mode="abs_pos", max_episode_steps=3, autoreset=True,
+                          randomize_objects=True)
+    env.reset(seed=1)
+    a = torch.tensor([[0.0, 0.45, 0.45, 1.0]] * 4, device="cuda")
+    for t in range(3):
+        obs, rew, term, trunc, info = env.step(a)
+    assert bool(trunc.all())
+    assert (env.step_count.cpu().numpy() == 0).all()  # reset inside the same step
+    assert (env._epi[:, 12].cpu().numpy() == 2).all()  # second episode running
+
+
+def test_abi_rejects_bad_action_dim():
+    from mujoco_manip_amd import _lib
+
+    sim = _lib.Sim(2, action_mode="ee_pos_rot6d_g")
+    a = torch.zeros(2, 4, device="cuda")
+    with pytest.raises(RuntimeError):
+        sim.step(a.data_ptr(), 4)
