@@ -8,7 +8,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libmmx.so")
 SOURCES = ["mmx_kernels.hip", "mmx_api.cpp"]
-HEADERS = ["mmx_model_gen.h", "mmx_state.h", "mmx_device.h", os.path.join("..", "..", "include", "mmx_api.h")]
+HEADERS = ["mmx_model_gen.h", "mmx_state.h", "mmx_device.h", "mmx_geom.h", os.path.join("..", "..", "include", "mmx_api.h")]
 ARCH = os.environ.get("MMX_OFFLOAD_ARCH", "gfx950")
 
 

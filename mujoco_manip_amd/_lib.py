@@ -17,10 +17,11 @@ from . import _build
 
 NQ, NV, NU, NOBS = 30, 27, 8, 85
 MAXCON, CON_F = 64, 12
-EPI_N, EPF_N, KIN_N, STAT_N = 14, 28, 54, 5
+EPI_N, EPF_N, KIN_N, STAT_N = 14, 28, 54, 13
 EPI_FIELDS = ("obj", "bin", "step_count", "flags", "fsm_state", "fsm_task_index", "fsm_settle", "fsm_gripper_open",
               "fsm_has_target", "env_error", "ncon", "nefc", "episodes", "rng_has32")
-STAT_FIELDS = ("sum_nefc", "sum_ncon", "sum_solver_iter", "substeps", "max_resid")
+STAT_FIELDS = ("sum_nefc", "sum_ncon", "sum_solver_iter", "substeps", "max_resid", "cyc_ik", "cyc_kinematics",
+               "cyc_dynamics", "cyc_collision", "cyc_constraints", "cyc_solver", "cyc_integrate", "cyc_step_end")
 ACTION_MODES = ("abs_pos", "ee_pos_quat_g", "ee_pos_rot6d_g", "ee_pos_quat_g_rel", "ee_pos_rot6d_g_rel")
 ACTION_DIMS = (4, 8, 10, 8, 10)
 REWARD_TYPES = ("dense", "sparse", "staged")

@@ -670,38 +670,100 @@ DEV float cost_wave(const EnvSh& E, const float* x) {
   return wave_sum(c);
 }
 
-DEV void chol_wave(EnvSh& E) {  // in-place lower Cholesky of E.H (27x27), right-looking
-  for (int k = 0; k < 27; k++) {
-    if (LANE == 0) E.H[k][k] = sqrtf(fmaxf(E.H[k][k], 1e-20f));
-    SYNC();
-    const float inv = 1.f / E.H[k][k];
-    if (LANE > k && LANE < 27) E.H[LANE][k] *= inv;
-    SYNC();
-    const int m = 26 - k;
-    const int nent = m * (m + 1) / 2;
-    for (int e = LANE; e < nent; e += WG) {
-      int ii, jj;
-      tri_index(e, ii, jj);
-      const int i = k + 1 + ii, j = k + 1 + jj;
-      E.H[i][j] -= E.H[i][k] * E.H[j][k];
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+DEV float readlane_f(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+
+// J' W [J | r] on the matrix cores: A = J' (dof x row), B = W [J | r] (row x 28), K = rows, two
+// rows per v_mfma_f32_32x32x2_f32 (lane l supplies row t + (l >> 5), dof / column l & 31, for
+// both operands).  Writes the Hessian H = M + J'WJ (full, 27 x 27) and the gradient
+// g = M (x - xs) + J'W r.  Two accumulators interleave the dependent 64-cycle MFMA chain.
+DEV void hess_grad_mfma(EnvSh& E, int nefc, bool want_h) {
+  const int col = LANE & 31, kh = LANE >> 5;
+  const int ba = col < 27 ? dof_blk(col) : -1;
+  f32x16 acc0 = {}, acc1 = {};
+  for (int t = 0; t < nefc; t += 4) {
+    float a[2], b[2];
+#pragma unroll
+    for (int u = 0; u < 2; u++) {
+      const int i = t + 2 * u + kh;
+      a[u] = 0.f;
+      b[u] = 0.f;
+      if (i < nefc) {
+        const float w = E.s[i];
+        if (col < 27) {
+          const int h = E.hdr[i], b0 = h & 15, b1 = (h >> 4) & 15;
+          const int sl = ba == b0 ? col - blk_d0(b0) : (ba == b1 ? blk_size(b0) + col - blk_d0(b1) : -1);
+          a[u] = sl >= 0 ? E.J[i][sl] : 0.f;
+          b[u] = w * a[u];
+        } else if (col == 27) {
+          b[u] = w * E.r[i];
+        }
+      }
     }
-    SYNC();
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0], b[0], acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1], b[1], acc1, 0, 0, 0);
   }
+  float mdx = 0.f;  // (M (x - xs))[col]; M is symmetric
+  if (col < 27 && kh == 0) {
+    for (int b = 0; b < 27; b++) mdx += E.M[col][b] * (E.x[b] - E.qacc_s[b]);
+    E.p[col] = mdx;  // staging
+  }
+  SYNC();
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    const int row = (r & 3) + 8 * (r >> 2) + 4 * kh;
+    const float c = acc0[r] + acc1[r];
+    if (row < 27) {
+      if (col < 27) {
+        if (want_h) E.H[row][col] = E.M[row][col] + c;
+      } else if (col == 27) {
+        E.g[row] = E.p[row] + c;
+      }
+    }
+  }
+  SYNC();
 }
 
-DEV void chol_solve_wave(EnvSh& E, float* v) {  // v <- H^{-1} v using the factor in E.H
+// out <- H^{-1} v, H = E.H (27 x 27 SPD, full).  The factor lives in registers: lane j holds
+// row j of L (h[m] = L[j][m], m <= j) and column j of L (c[i] = L[i][j], i >= j); cross-lane
+// values move with v_readlane / v_writelane, so there is no LDS round trip and no barrier.
+DEV void chol_solve_reg(EnvSh& E, const float* v, float* out) {
+  const int j = LANE;
+  float h[27], c[27];
+#pragma unroll
+  for (int i = 0; i < 27; i++) {
+    h[i] = j < 27 ? E.H[j][i] : 0.f;
+    c[i] = 0.f;
+  }
+#pragma unroll
   for (int k = 0; k < 27; k++) {
-    if (LANE == 0) v[k] /= E.H[k][k];
-    SYNC();
-    if (LANE > k && LANE < 27) v[LANE] -= E.H[LANE][k] * v[k];
-    SYNC();
+    const float sd = sqrtf(fmaxf(readlane_f(h[k], k), 1e-20f));
+    const float inv = 1.f / sd;
+    const float l = j == k ? sd : h[k] * inv;  // lane j >= k: L[j][k]
+    h[k] = l;
+    c[k] = j == k ? sd : c[k];
+#pragma unroll
+    for (int i = k + 1; i < 27; i++) {
+      const float li = readlane_f(l, i);
+      h[i] = fmaf(-li, l, h[i]);
+      c[i] = j == k ? li : c[i];
+    }
   }
-  for (int k = 26; k >= 0; k--) {
-    if (LANE == 0) v[k] /= E.H[k][k];
-    SYNC();
-    if (LANE < k) v[LANE] -= E.H[k][LANE] * v[k];
-    SYNC();
+  float y = j < 27 ? v[j] : 0.f;
+#pragma unroll
+  for (int k = 0; k < 27; k++) {  // L y = v
+    const float yk = readlane_f(y / h[k], k);
+    y = j == k ? yk : (j > k ? fmaf(-h[k], yk, y) : y);
   }
+#pragma unroll
+  for (int k = 26; k >= 0; k--) {  // L' z = y
+    const float zk = readlane_f(y / c[k], k);
+    y = j == k ? zk : (j < k ? fmaf(-c[k], zk, y) : y);
+  }
+  SYNC();
+  if (j < 27) out[j] = y;
+  SYNC();
 }
 
 DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
@@ -724,40 +786,13 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
       E.s[i] = ((h >> 8) || v < 0.f) ? E.D[i] : 0.f;
     }
     SYNC();
-    float ga = 0.f;
-    if (LANE < 27) {
-      const int ba = dof_blk(LANE);
-      for (int b = 0; b < 27; b++) ga += E.M[LANE][b] * (E.x[b] - E.qacc_s[b]);
-      for (int i = 0; i < nefc; i++) {
-        const float wi = E.s[i];
-        if (wi == 0.f) continue;
-        const int h = E.hdr[i];
-        if ((h & 15) != ba && ((h >> 4) & 15) != ba) continue;
-        ga += wi * E.r[i] * E.J[i][row_slot(h, LANE)];
-      }
-      E.g[LANE] = ga;
-    }
-    resid = sqrtf(wave_sum(LANE < 27 ? ga * ga : 0.f)) / scale;
+    hess_grad_mfma(E, nefc, true);
+    const float ga = LANE < 27 ? E.g[LANE] : 0.f;
+    resid = sqrtf(wave_sum(ga * ga)) / scale;
     if (resid < tol) break;
-    for (int e = LANE; e < 378; e += WG) {  // H = M + J' W J (lower triangle), block-sparse rows
-      int a, b;
-      tri_index(e, a, b);
-      const int ba = dof_blk(a), bb = dof_blk(b);
-      float hs = E.M[a][b];
-      for (int i = 0; i < nefc; i++) {
-        const float wi = E.s[i];
-        if (wi == 0.f) continue;
-        const int h = E.hdr[i], h0 = h & 15, h1 = (h >> 4) & 15;
-        if ((h0 != ba && h1 != ba) || (h0 != bb && h1 != bb)) continue;
-        hs += wi * E.J[i][row_slot(h, a)] * E.J[i][row_slot(h, b)];
-      }
-      E.H[a][b] = hs;
-    }
-    SYNC();
-    chol_wave(E);
     if (LANE < 27) E.p[LANE] = -E.g[LANE];
     SYNC();
-    chol_solve_wave(E, E.p);
+    chol_solve_reg(E, E.p, E.p);
     // exact line search on phi(a) = cost(x + a p): phi' is piecewise linear and increasing
     for (int i = LANE; i < nefc; i += WG) E.s[i] = row_dot(E.J[i], E.hdr[i], E.p);
     float c0 = 0.f, c1 = 0.f;
@@ -983,16 +1018,35 @@ DEV void ik_lane0(EnvSh& E) {
 }
 
 // ============================================================================ one mj_step
+DEV unsigned long long tick() { return __builtin_amdgcn_s_memtime(); }
+
 DEV void mj_step_wave(const MMXState& S, EnvSh& E, float* stats) {
+  unsigned long long t0 = tick(), t1;
   if (LANE == 0) kinematics_lane0(E);
   SYNC();
+  t1 = tick();
+  stats[STAT_T_KIN] += (float)(t1 - t0);
+  t0 = t1;
   dynamics_wave(E);
+  t1 = tick();
+  stats[STAT_T_DYN] += (float)(t1 - t0);
+  t0 = t1;
   collide_wave(E, false);
+  t1 = tick();
+  stats[STAT_T_COL] += (float)(t1 - t0);
+  t0 = t1;
   make_constraints_wave(E);
+  t1 = tick();
+  stats[STAT_T_CON] += (float)(t1 - t0);
+  t0 = t1;
   float resid = 0.f;
   const int it = newton_wave(E, S.solver_max_iter, S.solver_tol, resid);
+  t1 = tick();
+  stats[STAT_T_SOLVE] += (float)(t1 - t0);
+  t0 = t1;
   if (LANE == 0) {
     integrate_lane0(E);
+    stats[STAT_T_INT] += (float)(tick() - t0);
     stats[STAT_NEFC] += (float)E.nefc;
     stats[STAT_NCON] += (float)E.ncon;
     stats[STAT_SOLVER_ITER] += (float)it;
@@ -1407,10 +1461,13 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_env_step_kernel(MMXState S,
   }
   SYNC();
   for (int sub = 0; sub < MMX_NSUBSTEP; sub++) {
+    const unsigned long long t0 = tick();
     if (LANE == 0) ik_lane0(E);  // IK on the kinematics left by the previous position stage
     SYNC();
+    stats[STAT_T_IK] += (float)(tick() - t0);
     mj_step_wave(S, E, stats);
   }
+  const unsigned long long t_end = tick();
   store_contacts(S, i, E);
   // mj_forward position stage (gym_env.py:560): kinematics + contacts for the staged penalty
   if (LANE == 0) {
@@ -1457,6 +1514,7 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_env_step_kernel(MMXState S,
       EPI(EPI_ERROR) = 0;
       reset_lane0(S, i, E, -1);
     }
+    stats[STAT_T_END] += (float)(tick() - t_end);
 #pragma unroll
     for (int k = 0; k < STAT_N; k++) S.stats[(size_t)i * STAT_N + k] = stats[k];
   }

@@ -117,6 +117,7 @@ def rollout_speed(N=4096, steps=20):
     env.reset(seed=[_lib.episode_seed(42, i) for i in range(N)])
     env.rollout_expert(2)
     torch.cuda.synchronize()
+    env.clear_stats()
     t = time.time()
     env.rollout_expert(steps)
     torch.cuda.synchronize()
@@ -128,6 +129,8 @@ if __name__ == "__main__":
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     for name, fn in [("phys1", lambda: physics_parity(1)), ("phys16", lambda: physics_parity(16)),
                      ("gym", gym_parity), ("expert", expert_success), ("speed", rollout_speed)]:
+        if len(sys.argv) > 1 and name not in sys.argv[1:]:
+            continue
         t = time.time()
         try:
             out[name] = fn()
