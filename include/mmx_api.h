@@ -75,9 +75,10 @@ typedef struct {
                                 episodes, rng_has32 */
   float* episode_f;          /* [N][28] T_init(12), hwm(5), target_kp(4), fsm_target(3), transit(3), return */
   float* kin;                /* [N][54] hand pos/mat + arm joint axes/anchors of the last position stage */
-  float* stats;              /* [N][13] sum nefc, sum ncon, sum solver iterations, substeps, max residual,
+  float* stats;              /* [N][17] sum nefc, sum ncon, sum solver iterations, substeps, max residual,
                                 then shader-clock cycles spent per phase: ik, kinematics, dynamics,
-                                collision, constraints, solver, integrate, step end (reward/obs/reset) */
+                                collision, constraints, solver, integrate, step end (reward/obs/reset),
+                                4 sub-phase probes (cycle fields: diagnostic build only, else 0) */
   float* contacts;           /* [N][64][12] dist, pos3, normal3, mu3, dim, geom1, geom2 (last substep) */
 } mmx_buffers;
 

@@ -1,43 +1,65 @@
-"""Build libmmx.so (HIP kernels + C-ABI) in-tree for gfx950 with hipcc."""
+"""Build libmmx.so (HIP kernels + C-ABI) in-tree for gfx950 with hipcc.
+
+Two variants share the sources: ``libmmx.so`` (the product) and ``libmmx_prof.so``, the same
+code compiled with ``-DMMX_PHASE_CLOCK`` so the kernels add per-phase shader-clock cycles into
+the stats buffer (selected at load time with ``MMX_PROFILE=1``; never used by the bench).
+"""
 from __future__ import annotations
 
 import os
 import subprocess
+from concurrent.futures import ThreadPoolExecutor
 
 PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libmmx.so")
+LIB_PROF = os.path.join(PKG, "libmmx_prof.so")
 SOURCES = ["mmx_kernels.hip", "mmx_api.cpp"]
-HEADERS = ["mmx_model_gen.h", "mmx_state.h", "mmx_device.h", "mmx_geom.h", os.path.join("..", "..", "include", "mmx_api.h")]
+HEADERS = ["mmx_model_gen.h", "mmx_state.h", "mmx_device.h", "mmx_geom.h",
+           os.path.join("..", "..", "include", "mmx_api.h")]
 ARCH = os.environ.get("MMX_OFFLOAD_ARCH", "gfx950")
 
 
-def _stale() -> bool:
-    if not os.path.exists(LIB):
+def lib_path(profile: bool = False) -> str:
+    return LIB_PROF if profile else LIB
+
+
+def _stale(lib: str) -> bool:
+    if not os.path.exists(lib):
         return True
-    t = os.path.getmtime(LIB)
+    t = os.path.getmtime(lib)
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
     return any(os.path.getmtime(d) > t for d in deps if os.path.exists(d))
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and not _stale():
-        return LIB
+def _compile(src: str, profile: bool, verbose: bool) -> str:
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    objs = []
-    for src in SOURCES:
-        obj = os.path.join(CSRC, os.path.splitext(src)[0] + ".o")
-        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", os.path.join(CSRC, src), "-o", obj]
-        if src.endswith(".cpp"):
-            cmd.insert(1, "-xhip")
-        if verbose:
-            print(" ".join(cmd))
-        subprocess.check_call(cmd)
-        objs.append(obj)
-    cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
+    obj = os.path.join(CSRC, os.path.splitext(src)[0] + ("_prof" if profile else "") + ".o")
+    cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", os.path.join(CSRC, src), "-o", obj]
+    if profile:
+        cmd.insert(1, "-DMMX_PHASE_CLOCK=1")
+    if src.endswith(".cpp"):
+        cmd.insert(1, "-xhip")
+    if verbose:
+        print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
-    return LIB
+    return obj
+
+
+def build(force: bool = False, verbose: bool = False, profile: bool | None = False) -> str:
+    """Build one variant (profile=False/True) or both (profile=None); returns the product path."""
+    variants = [False, True] if profile is None else [profile]
+    variants = [v for v in variants if force or _stale(lib_path(v))]
+    if variants:
+        jobs = [(src, v) for v in variants for src in SOURCES]
+        with ThreadPoolExecutor(max_workers=len(jobs)) as ex:
+            objs = list(ex.map(lambda j: _compile(j[0], j[1], verbose), jobs))
+        hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+        for v in variants:
+            mine = [o for o, (_, vv) in zip(objs, jobs) if vv == v]
+            subprocess.check_call([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib_path(v)] + mine)
+    return lib_path(bool(profile))
 
 
 if __name__ == "__main__":
-    print(build(force=True, verbose=True))
+    print(build(force=True, verbose=True, profile=None))

@@ -17,11 +17,12 @@ from . import _build
 
 NQ, NV, NU, NOBS = 30, 27, 8, 85
 MAXCON, CON_F = 64, 12
-EPI_N, EPF_N, KIN_N, STAT_N = 14, 28, 54, 13
+EPI_N, EPF_N, KIN_N, STAT_N = 14, 28, 54, 17
 EPI_FIELDS = ("obj", "bin", "step_count", "flags", "fsm_state", "fsm_task_index", "fsm_settle", "fsm_gripper_open",
               "fsm_has_target", "env_error", "ncon", "nefc", "episodes", "rng_has32")
 STAT_FIELDS = ("sum_nefc", "sum_ncon", "sum_solver_iter", "substeps", "max_resid", "cyc_ik", "cyc_kinematics",
-               "cyc_dynamics", "cyc_collision", "cyc_constraints", "cyc_solver", "cyc_integrate", "cyc_step_end")
+               "cyc_dynamics", "cyc_collision", "cyc_constraints", "cyc_solver", "cyc_integrate", "cyc_step_end",
+               "cyc_aux0", "cyc_aux1", "cyc_aux2", "cyc_aux3")
 ACTION_MODES = ("abs_pos", "ee_pos_quat_g", "ee_pos_rot6d_g", "ee_pos_quat_g_rel", "ee_pos_rot6d_g_rel")
 ACTION_DIMS = (4, 8, 10, 8, 10)
 REWARD_TYPES = ("dense", "sparse", "staged")
@@ -60,11 +61,13 @@ def load(build_if_missing: bool = True):
     global _lib
     if _lib is not None:
         return _lib
-    if not os.path.exists(_build.LIB):
+    profile = os.environ.get("MMX_PROFILE", "0") not in ("", "0")
+    path = _build.lib_path(profile)
+    if not os.path.exists(path):
         if not build_if_missing:
-            raise RuntimeError(f"libmmx.so missing at {_build.LIB}; run __graft_entry__.build()")
-        _build.build()
-    L = C.CDLL(_build.LIB)
+            raise RuntimeError(f"{os.path.basename(path)} missing at {path}; run __graft_entry__.build()")
+        _build.build(profile=profile)
+    L = C.CDLL(path)
     vp, u8p, i32p, u64p, fp = C.c_void_p, C.POINTER(C.c_uint8), C.POINTER(C.c_int32), C.POINTER(C.c_uint64), C.POINTER(C.c_float)
     L.mmx_config_default.argtypes = [C.POINTER(MMXConfig)]
     L.mmx_create.argtypes = [C.POINTER(MMXConfig), C.POINTER(vp)]

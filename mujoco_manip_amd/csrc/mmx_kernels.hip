@@ -45,21 +45,28 @@ struct EnvSh {
   float Ic[12][10];  // composite inertias (m, h, J) of arm bodies
   float M[27][LD];
   float L[45];       // packed lower Cholesky of the arm block
-  float H[27][LD];   // Newton Hessian / Cholesky factor; collision sort scratch
   float qfrc[LD], qacc_s[LD], x[LD], g[LD], p[LD];
   float bias[9];
   float con[MMX_MAXCON][CON_F];
   int conkey[MMX_MAXCON];
   // constraint rows in block format: a row touches at most two dof blocks (arm = 9 dofs,
-  // cube k = 6 dofs); J[i][0..n0) holds block b0's columns, J[i][n0..n0+n1) block b1's
-  float J[MMX_MAXEFC][15];
-  int hdr[MMX_MAXEFC];  // b0 | b1 << 4 | eq << 8 (block 15 = none)
-  float aref[MMX_MAXEFC], D[MMX_MAXEFC], r[MMX_MAXEFC], s[MMX_MAXEFC];
+  // cube k = 6 dofs); J[i][0..n0) holds block b0's columns, J[i][n0..n0+n1) block b1's;
+  // J doubles as the contact-sort scratch in collide_wave (rows are built after it)
+  alignas(16) float J[MMX_MAXEFC][16];  // slot 15 (and any slot past the row's width) = 0
+  // (+8 pad: the MFMA pass reads whole 4-row groups past nefc)
+  alignas(16) int hdr[MMX_MAXEFC + 8];  // b0 | b1 << 4 | eq << 8 (block 15 = none)
+  alignas(16) float r[MMX_MAXEFC + 8], s[MMX_MAXEFC + 8];
+  float aref[MMX_MAXEFC], D[MMX_MAXEFC];
+  float Lrow[27][27];  // Newton Cholesky factor, row-major (read back as columns)
   int bpscan[MMX_NBODYPAIR + 1];
   float obs[MMX_NOBS + 3];
   int ncon, nefc, flags, iters;
   int act_unclamped[8];
+  float stats[STAT_N];  // lane 0 accumulates; loaded / stored with the env record
 };
+// The workgroup's env lives in one file-scope LDS object: the non-inlined substep function below
+// reaches it by symbol (LDS address space), not through a generic pointer.
+static __shared__ EnvSh g_E;
 enum { SHF_ROBOT_OBST = 1, SHF_CON_OVF = 2, SHF_EFC_OVF = 4, SHF_NAN = 8 };
 
 DEV int body_slot(int b) { return b <= 11 ? b - 1 : b - 5; }
@@ -74,17 +81,6 @@ DEV int row_slot(int h, int a) {
   if (ba == b0) return a - blk_d0(b0);
   if (ba == b1) return blk_size(b0) + a - blk_d0(b1);
   return -1;
-}
-DEV float row_dot(const float* Jr, int h, const float* x) {
-  const int b0 = h & 15, b1 = (h >> 4) & 15;
-  float s = 0.f;
-  const int n0 = blk_size(b0), d0 = blk_d0(b0);
-  for (int k = 0; k < n0; k++) s += Jr[k] * x[d0 + k];
-  if (b1 != BLK_NONE) {
-    const int d1 = blk_d0(b1);
-    for (int k = 0; k < 6; k++) s += Jr[n0 + k] * x[d1 + k];
-  }
-  return s;
 }
 DEV bool arm_anc(int d, int b) { return d <= 6 ? (b >= d + 2 && b <= 11) : (d == 7 ? b == 10 : b == 11); }
 DEV V3 body_x(const EnvSh& E, int b) {
@@ -101,11 +97,42 @@ DEV M3 body_R(const EnvSh& E, int b) {
 }
 DEV SV load_S(const EnvSh& E, int d) { return SV{V3{E.S[d][0], E.S[d][1], E.S[d][2]}, V3{E.S[d][3], E.S[d][4], E.S[d][5]}}; }
 
+// ---------------------------------------------------------------- phase clock (diagnostic build)
+// Built with -DMMX_PHASE_CLOCK (libmmx_prof.so) the kernels add the shader-clock cycles
+// (s_memtime) of each phase into stats[STAT_T_*]; the product build compiles them away.
+#ifdef MMX_PHASE_CLOCK
+#define CLK_DECL unsigned long long clk_t0_ = __builtin_amdgcn_s_memtime()
+#define CLK(st, k)                                                  \
+  do {                                                              \
+    const unsigned long long clk_t1_ = __builtin_amdgcn_s_memtime(); \
+    if (LANE == 0) (st)[k] += (float)(clk_t1_ - clk_t0_);           \
+    clk_t0_ = clk_t1_;                                              \
+  } while (0)
+#else
+#define CLK_DECL \
+  do {           \
+  } while (0)
+#define CLK(st, k) \
+  do {             \
+  } while (0)
+#endif
+
 // ---------------------------------------------------------------- wave primitives
+// wave64 sum: DPP butterflies inside each row of 16 lanes, then the four row sums in a fixed
+// order (bit-identical in every lane, no LDS traffic)
+template <int CTRL>
+DEV float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
 DEV float wave_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);  // row_half_mirror
+  v += dpp_f<0x140>(v);  // row_mirror
+  return (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)) +
+          __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16))) +
+         (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)) +
+          __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48)));
 }
 DEV int wave_scan_incl(int v) {
 #pragma unroll
@@ -496,7 +523,7 @@ DEV void collide_wave(EnvSh& E, bool only_ro) {
   SYNC();
   if (only_ro) return;
   const int n = min(E.ncon, MMX_MAXCON);
-  float* tmp = &E.H[0][0];
+  float* tmp = &E.J[0][0];
   if (LANE < n) {
     const int key = E.conkey[LANE];
     int rank = 0;
@@ -539,10 +566,12 @@ DEV void finish_row(EnvSh& E, int row, const float* Jd, int b0, int b1, float po
                     const float* solimp, int is_eq) {
   const int n0 = blk_size(b0), d0 = blk_d0(b0);
   for (int k = 0; k < n0; k++) E.J[row][k] = Jd[d0 + k];
+  int k = n0;
   if (b1 != BLK_NONE) {
     const int d1 = blk_d0(b1);
-    for (int k = 0; k < 6; k++) E.J[row][n0 + k] = Jd[d1 + k];
+    for (; k < n0 + 6; k++) E.J[row][k] = Jd[d1 + k - n0];
   }
+  for (; k < 16; k++) E.J[row][k] = 0.f;
   E.hdr[row] = b0 | (b1 << 4) | (is_eq << 8);
   float vel = 0.f;
 #pragma unroll
@@ -655,165 +684,249 @@ DEV void make_constraints_wave(EnvSh& E) {
 // ============================================================================ Newton solver (wave)
 // Primal Newton with exact line search (MuJoCo's default solver): minimise
 //   0.5 (x - xs)' M (x - xs) + sum_i s_i(J_i x - aref_i),  s_i = 0.5 D_i r^2 on active rows.
-DEV float cost_wave(const EnvSh& E, const float* x) {
-  float c = 0.f;
-  if (LANE < 27) {
-    float mdx = 0.f;
-    for (int b = 0; b < 27; b++) mdx += E.M[LANE][b] * (x[b] - E.qacc_s[b]);
-    c = 0.5f * (x[LANE] - E.qacc_s[LANE]) * mdx;
-  }
-  for (int i = LANE; i < E.nefc; i += WG) {
-    const int h = E.hdr[i];
-    const float v = row_dot(E.J[i], h, x) - E.aref[i];
-    if ((h >> 8) || v < 0.f) c += 0.5f * E.D[i] * v * v;
-  }
-  return wave_sum(c);
-}
-
+// Lane l owns constraint rows l + 64 q (q < RPL): their residual, search-direction projection,
+// D and equality flag stay in registers through the line search.  The Hessian and gradient come
+// from one MFMA pass (hess_grad_mfma) straight into registers; the Cholesky factorisation and
+// both triangular solves run in registers (chol_solve_reg): no LDS matrix, no barrier.
+#define RPL ((MMX_MAXEFC + WG - 1) / WG)
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 DEV float readlane_f(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
 
+// J_i . x for a block-format row (slots past the row's width hold zeros)
+DEV float row_dot16(const EnvSh& E, int i, const float* x) {
+  const int h = E.hdr[i], b0 = h & 15, b1 = (h >> 4) & 15;
+  const int d0 = blk_d0(b0), n0 = blk_size(b0), d1 = b1 == BLK_NONE ? 0 : blk_d0(b1);
+  const float4* Jr = reinterpret_cast<const float4*>(E.J[i]);
+  float jv[16];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const float4 v = Jr[q];
+    jv[4 * q] = v.x;
+    jv[4 * q + 1] = v.y;
+    jv[4 * q + 2] = v.z;
+    jv[4 * q + 3] = v.w;
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < 15; k++) {
+    const int idx = min(k < n0 ? d0 + k : d1 + k - n0, 26);
+    s = fmaf(jv[k], x[idx], s);
+  }
+  return s;
+}
+
+// cost at two candidate points (warm start, qacc_smooth) in one pass
+DEV void cost2_wave(const EnvSh& E, const float* xa, const float* xb, float& ca, float& cb) {
+  float c0 = 0.f, c1 = 0.f;
+  if (LANE < 27) {
+    float ma = 0.f, mb = 0.f;
+#pragma unroll
+    for (int b = 0; b < 27; b++) {
+      const float m = E.M[LANE][b];
+      ma = fmaf(m, xa[b] - E.qacc_s[b], ma);
+      mb = fmaf(m, xb[b] - E.qacc_s[b], mb);
+    }
+    c0 = 0.5f * (xa[LANE] - E.qacc_s[LANE]) * ma;
+    c1 = 0.5f * (xb[LANE] - E.qacc_s[LANE]) * mb;
+  }
+#pragma unroll
+  for (int q = 0; q < RPL; q++) {
+    const int i = LANE + WG * q;
+    if (i < E.nefc) {
+      const bool eq = (E.hdr[i] >> 8) != 0;
+      const float va = row_dot16(E, i, xa) - E.aref[i], vb = row_dot16(E, i, xb) - E.aref[i];
+      if (eq || va < 0.f) c0 += 0.5f * E.D[i] * va * va;
+      if (eq || vb < 0.f) c1 += 0.5f * E.D[i] * vb * vb;
+    }
+  }
+  ca = wave_sum(c0);
+  cb = wave_sum(c1);
+}
+
 // J' W [J | r] on the matrix cores: A = J' (dof x row), B = W [J | r] (row x 28), K = rows, two
 // rows per v_mfma_f32_32x32x2_f32 (lane l supplies row t + (l >> 5), dof / column l & 31, for
-// both operands).  Writes the Hessian H = M + J'WJ (full, 27 x 27) and the gradient
-// g = M (x - xs) + J'W r.  Two accumulators interleave the dependent 64-cycle MFMA chain.
-DEV void hess_grad_mfma(EnvSh& E, int nefc, bool want_h) {
+// both operands; loads are unconditional so unrolled steps batch them).  Returns, in lane j < 27,
+// row j of H = M + J'WJ in hrow[0..27) and g_j = (M (x - xs) + J'W r)_j.
+DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow) {
   const int col = LANE & 31, kh = LANE >> 5;
-  const int ba = col < 27 ? dof_blk(col) : -1;
+  // this lane's dof: block and offset inside the block (none for the padding columns 27..31)
+  const int ba = col < 27 ? dof_blk(col) : -1, ob = col < 27 ? col - blk_d0(ba) : 0;
+  // K order: lane half kh walks rows [kh * hh, kh * hh + hh) in groups of 4 (vector loads of the
+  // row headers / weights / residuals, four independent J gathers, four MFMAs)
+  const int hh = ((nefc + 7) >> 3) << 2;
   f32x16 acc0 = {}, acc1 = {};
-  for (int t = 0; t < nefc; t += 4) {
-    float a[2], b[2];
+  for (int t = 0; t < hh; t += 4) {
+    const int i0 = kh * hh + t;
+    const int4 h4 = *reinterpret_cast<const int4*>(&E.hdr[i0]);
+    const float4 w4 = *reinterpret_cast<const float4*>(&E.s[i0]);
+    const float4 r4 = *reinterpret_cast<const float4*>(&E.r[i0]);
+    const int hv[4] = {h4.x, h4.y, h4.z, h4.w};
+    const float wv[4] = {w4.x, w4.y, w4.z, w4.w}, rv[4] = {r4.x, r4.y, r4.z, r4.w};
+    float jv[4];
 #pragma unroll
-    for (int u = 0; u < 2; u++) {
-      const int i = t + 2 * u + kh;
-      a[u] = 0.f;
-      b[u] = 0.f;
-      if (i < nefc) {
-        const float w = E.s[i];
-        if (col < 27) {
-          const int h = E.hdr[i], b0 = h & 15, b1 = (h >> 4) & 15;
-          const int sl = ba == b0 ? col - blk_d0(b0) : (ba == b1 ? blk_size(b0) + col - blk_d0(b1) : -1);
-          a[u] = sl >= 0 ? E.J[i][sl] : 0.f;
-          b[u] = w * a[u];
-        } else if (col == 27) {
-          b[u] = w * E.r[i];
-        }
-      }
+    for (int u = 0; u < 4; u++) {
+      const int b0 = hv[u] & 15, b1 = (hv[u] >> 4) & 15;
+      const int sl = ba == b0 ? ob : (ba == b1 ? (b0 == 0 ? 9 : 6) + ob : 15);
+      jv[u] = E.J[min(i0 + u, MMX_MAXEFC - 1)][min(sl, 15)];
+    }
+    float a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const bool valid = i0 + u < nefc;
+      a[u] = valid ? jv[u] : 0.f;
+      b[u] = valid ? wv[u] * (col < 27 ? jv[u] : (col == 27 ? rv[u] : 0.f)) : 0.f;
     }
     acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0], b[0], acc0, 0, 0, 0);
     acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1], b[1], acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[2], b[2], acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[3], b[3], acc1, 0, 0, 0);
   }
-  float mdx = 0.f;  // (M (x - xs))[col]; M is symmetric
-  if (col < 27 && kh == 0) {
-    for (int b = 0; b < 27; b++) mdx += E.M[col][b] * (E.x[b] - E.qacc_s[b]);
-    E.p[col] = mdx;  // staging
+  const int jc = min(LANE, 26);
+  float mdx = 0.f;
+#pragma unroll
+  for (int b = 0; b < 27; b++) mdx = fmaf(E.M[jc][b], E.x[b] - E.qacc_s[b], mdx);
+  float c[16];
+#pragma unroll
+  for (int r = 0; r < 16; r++) c[r] = acc0[r] + acc1[r];
+  if (col == 27) {  // gradient column: its rows sit in lanes 27 and 59 -> LDS
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const int row = (r & 3) + 8 * (r >> 2) + 4 * kh;
+      if (row < 27) E.g[row] = c[r];
+    }
   }
-  SYNC();
+  // lane j < 32 holds C[rows 8m + 0..3][j]; its partner lane j + 32 holds rows 8m + 4..7
 #pragma unroll
   for (int r = 0; r < 16; r++) {
-    const int row = (r & 3) + 8 * (r >> 2) + 4 * kh;
-    const float c = acc0[r] + acc1[r];
-    if (row < 27) {
-      if (col < 27) {
-        if (want_h) E.H[row][col] = E.M[row][col] + c;
-      } else if (col == 27) {
-        E.g[row] = E.p[row] + c;
-      }
-    }
+    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(c[r]), __float_as_uint(c[r]), false, false);
+    const int row = (r & 3) + 8 * (r >> 2);
+    hrow[row] = c[r];
+    hrow[row + 4] = __uint_as_float(sw[1]);
   }
+#pragma unroll
+  for (int i = 0; i < 27; i++) hrow[i] += E.M[jc][i];
   SYNC();
+  const float g = LANE < 27 ? E.g[LANE] + mdx : 0.f;
+  SYNC();
+  return g;
 }
 
-// out <- H^{-1} v, H = E.H (27 x 27 SPD, full).  The factor lives in registers: lane j holds
-// row j of L (h[m] = L[j][m], m <= j) and column j of L (c[i] = L[i][j], i >= j); cross-lane
-// values move with v_readlane / v_writelane, so there is no LDS round trip and no barrier.
-DEV void chol_solve_reg(EnvSh& E, const float* v, float* out) {
+// Returns (H^{-1} v)_j in lane j for H given by rows hrow (lane j = row j, j < 27) and v_j.  The
+// factor stays in registers: lane j holds row j of L (h[m] = L[j][m], m <= j) and column j of L
+// (c[i] = L[i][j], i >= j); cross-lane values move with v_readlane.
+DEV float chol_solve_reg(EnvSh& E, const float* hrow, float v) {
   const int j = LANE;
-  float h[27], c[27];
+  float h[27], dinv[27];
 #pragma unroll
-  for (int i = 0; i < 27; i++) {
-    h[i] = j < 27 ? E.H[j][i] : 0.f;
-    c[i] = 0.f;
-  }
+  for (int i = 0; i < 27; i++) h[i] = hrow[i];
 #pragma unroll
   for (int k = 0; k < 27; k++) {
-    const float sd = sqrtf(fmaxf(readlane_f(h[k], k), 1e-20f));
-    const float inv = 1.f / sd;
+    const float d = fmaxf(readlane_f(h[k], k), 1e-20f);
+    const float sd = __builtin_amdgcn_sqrtf(d), inv = __builtin_amdgcn_rcpf(sd);
+    dinv[k] = inv;
     const float l = j == k ? sd : h[k] * inv;  // lane j >= k: L[j][k]
     h[k] = l;
-    c[k] = j == k ? sd : c[k];
 #pragma unroll
-    for (int i = k + 1; i < 27; i++) {
-      const float li = readlane_f(l, i);
-      h[i] = fmaf(-li, l, h[i]);
-      c[i] = j == k ? li : c[i];
-    }
+    for (int i = k + 1; i < 27; i++) h[i] = fmaf(-readlane_f(l, i), l, h[i]);
   }
-  float y = j < 27 ? v[j] : 0.f;
+  float y = j < 27 ? v : 0.f;
 #pragma unroll
   for (int k = 0; k < 27; k++) {  // L y = v
-    const float yk = readlane_f(y / h[k], k);
+    const float yk = readlane_f(y, k) * dinv[k];
     y = j == k ? yk : (j > k ? fmaf(-h[k], yk, y) : y);
   }
+  // columns of L for the transposed solve: rows out to LDS, columns back in
+  const int jc = min(j, 26);
+  if (j < 27) {
+#pragma unroll
+    for (int m = 0; m < 27; m++) E.Lrow[j][m] = h[m];
+  }
+  SYNC();
+  float c[27];
+#pragma unroll
+  for (int k = 0; k < 27; k++) c[k] = E.Lrow[k][jc];  // L[k][j]
 #pragma unroll
   for (int k = 26; k >= 0; k--) {  // L' z = y
-    const float zk = readlane_f(y / c[k], k);
+    const float zk = readlane_f(y, k) * dinv[k];
     y = j == k ? zk : (j < k ? fmaf(-c[k], zk, y) : y);
   }
   SYNC();
-  if (j < 27) out[j] = y;
-  SYNC();
+  return y;
 }
 
 DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
+  float* stats = E.stats;
+  CLK_DECL;
   const int nefc = E.nefc;
-  // start from the cheaper of qacc_smooth and the warm start (as MuJoCo does)
-  const float c_ws = cost_wave(E, E.ws);
-  const float c_s = cost_wave(E, E.qacc_s);
+  // start from the cheaper of the warm start and qacc_smooth (as MuJoCo does)
+  float c_ws, c_s;
+  cost2_wave(E, E.ws, E.qacc_s, c_ws, c_s);
   if (LANE < 27) E.x[LANE] = c_ws < c_s ? E.ws[LANE] : E.qacc_s[LANE];
   float scale = LANE < 27 ? E.qfrc[LANE] * E.qfrc[LANE] : 0.f;
   scale = sqrtf(wave_sum(scale)) + 1.f;
+  float rr[RPL], jp[RPL], dd[RPL];
+  bool eq[RPL];
+#pragma unroll
+  for (int q = 0; q < RPL; q++) {
+    const int i = LANE + WG * q;
+    dd[q] = i < nefc ? E.D[i] : 0.f;
+    eq[q] = i < nefc && (E.hdr[i] >> 8) != 0;
+    rr[q] = 0.f;
+    jp[q] = 0.f;
+  }
   SYNC();
   int it = 0;
   resid = 0.f;
+  CLK(stats, STAT_T_AUX3);
   for (; it < max_iter; it++) {
-    // residuals; the active weight is folded into s[] (reused below for the line search)
-    for (int i = LANE; i < nefc; i += WG) {
-      const int h = E.hdr[i];
-      const float v = row_dot(E.J[i], h, E.x) - E.aref[i];
-      E.r[i] = v;
-      E.s[i] = ((h >> 8) || v < 0.f) ? E.D[i] : 0.f;
+    // residuals r = J x - aref and active weights s (LDS copies feed the MFMA pass)
+#pragma unroll
+    for (int q = 0; q < RPL; q++) {
+      const int i = LANE + WG * q;
+      if (i < nefc) {
+        const float v = row_dot16(E, i, E.x) - E.aref[i];
+        rr[q] = v;
+        E.r[i] = v;
+        E.s[i] = (eq[q] || v < 0.f) ? dd[q] : 0.f;
+      }
     }
     SYNC();
-    hess_grad_mfma(E, nefc, true);
-    const float ga = LANE < 27 ? E.g[LANE] : 0.f;
-    resid = sqrtf(wave_sum(ga * ga)) / scale;
+    CLK(stats, STAT_T_AUX0);
+    float hrow[32];
+    const float g = hess_grad_mfma(E, nefc, hrow);
+    resid = sqrtf(wave_sum(g * g)) / scale;
+    CLK(stats, STAT_T_AUX1);
     if (resid < tol) break;
-    if (LANE < 27) E.p[LANE] = -E.g[LANE];
+    const float pj = chol_solve_reg(E, hrow, -g);
+    if (LANE < 27) E.p[LANE] = pj;
     SYNC();
-    chol_solve_reg(E, E.p, E.p);
+    CLK(stats, STAT_T_AUX2);
     // exact line search on phi(a) = cost(x + a p): phi' is piecewise linear and increasing
-    for (int i = LANE; i < nefc; i += WG) E.s[i] = row_dot(E.J[i], E.hdr[i], E.p);
+#pragma unroll
+    for (int q = 0; q < RPL; q++) {
+      const int i = LANE + WG * q;
+      jp[q] = i < nefc ? row_dot16(E, i, E.p) : 0.f;
+    }
     float c0 = 0.f, c1 = 0.f;
     if (LANE < 27) {
       float mp = 0.f;
-      for (int b = 0; b < 27; b++) mp += E.M[LANE][b] * E.p[b];
+#pragma unroll
+      for (int b = 0; b < 27; b++) mp = fmaf(E.M[LANE][b], E.p[b], mp);
       c0 = mp * (E.x[LANE] - E.qacc_s[LANE]);
-      c1 = mp * E.p[LANE];
+      c1 = mp * pj;
     }
-    SYNC();
     c0 = wave_sum(c0);
     c1 = wave_sum(c1);
     float alpha = 1.f, lo = 0.f, hi = 3e38f;
     for (int ls = 0; ls < 24; ls++) {
       float d1 = 0.f, d2 = 0.f;
-      for (int i = LANE; i < nefc; i += WG) {
-        const float v = E.r[i] + alpha * E.s[i];
-        if ((E.hdr[i] >> 8) || v < 0.f) {
-          d1 += E.D[i] * E.s[i] * v;
-          d2 += E.D[i] * E.s[i] * E.s[i];
-        }
+#pragma unroll
+      for (int q = 0; q < RPL; q++) {
+        const float v = fmaf(alpha, jp[q], rr[q]);
+        const float dj = (eq[q] || v < 0.f) ? dd[q] * jp[q] : 0.f;
+        d1 = fmaf(dj, v, d1);
+        d2 = fmaf(dj, jp[q], d2);
       }
       d1 = wave_sum(d1) + c0 + alpha * c1;
       d2 = wave_sum(d2) + c1;
@@ -827,10 +940,11 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
       }
       alpha = na;
     }
+    CLK(stats, STAT_T_AUX3);
     float stepn = 0.f;
     if (LANE < 27) {
-      E.x[LANE] += alpha * E.p[LANE];
-      stepn = alpha * alpha * E.p[LANE] * E.p[LANE];
+      E.x[LANE] += alpha * pj;
+      stepn = alpha * alpha * pj * pj;
     }
     SYNC();
     stepn = sqrtf(wave_sum(stepn));
@@ -1018,35 +1132,24 @@ DEV void ik_lane0(EnvSh& E) {
 }
 
 // ============================================================================ one mj_step
-DEV unsigned long long tick() { return __builtin_amdgcn_s_memtime(); }
-
-DEV void mj_step_wave(const MMXState& S, EnvSh& E, float* stats) {
-  unsigned long long t0 = tick(), t1;
+DEV void mj_step_wave(int max_iter, float tol, EnvSh& E) {
+  float* stats = E.stats;
+  CLK_DECL;
   if (LANE == 0) kinematics_lane0(E);
   SYNC();
-  t1 = tick();
-  stats[STAT_T_KIN] += (float)(t1 - t0);
-  t0 = t1;
+  CLK(stats, STAT_T_KIN);
   dynamics_wave(E);
-  t1 = tick();
-  stats[STAT_T_DYN] += (float)(t1 - t0);
-  t0 = t1;
+  CLK(stats, STAT_T_DYN);
   collide_wave(E, false);
-  t1 = tick();
-  stats[STAT_T_COL] += (float)(t1 - t0);
-  t0 = t1;
+  CLK(stats, STAT_T_COL);
   make_constraints_wave(E);
-  t1 = tick();
-  stats[STAT_T_CON] += (float)(t1 - t0);
-  t0 = t1;
+  CLK(stats, STAT_T_CON);
   float resid = 0.f;
-  const int it = newton_wave(E, S.solver_max_iter, S.solver_tol, resid);
-  t1 = tick();
-  stats[STAT_T_SOLVE] += (float)(t1 - t0);
-  t0 = t1;
+  const int it = newton_wave(E, max_iter, tol, resid);
+  CLK(stats, STAT_T_SOLVE);
   if (LANE == 0) {
     integrate_lane0(E);
-    stats[STAT_T_INT] += (float)(tick() - t0);
+    CLK(stats, STAT_T_INT);
     stats[STAT_NEFC] += (float)E.nefc;
     stats[STAT_NCON] += (float)E.ncon;
     stats[STAT_SOLVER_ITER] += (float)it;
@@ -1054,6 +1157,18 @@ DEV void mj_step_wave(const MMXState& S, EnvSh& E, float* stats) {
     stats[STAT_RESID] = fmaxf(stats[STAT_RESID], resid);
   }
   SYNC();
+}
+
+// One substep = [IK] + mj_step, kept out of line: every phase's loop invariants are recomputed
+// per call instead of being hoisted across all 16 substeps, which would pin registers for the
+// whole kernel and serialise the phases' LDS loads.
+__device__ __attribute__((noinline)) void substep(int max_iter, float tol, int with_ik) {
+  EnvSh& E = g_E;
+  CLK_DECL;
+  if (with_ik && LANE == 0) ik_lane0(E);  // IK on the kinematics left by the previous position stage
+  SYNC();
+  CLK(E.stats, STAT_T_IK);
+  mj_step_wave(max_iter, tol, E);
 }
 
 // ============================================================================ RNG (numpy PCG64)
@@ -1412,6 +1527,7 @@ DEV void load_env(const MMXState& S, int i, EnvSh& E) {
   if (LANE < 8) E.ctrl[LANE] = S.ctrl[(size_t)i * 8 + LANE];
   if (LANE < KIN_N) E.kin[LANE] = S.kin[(size_t)i * KIN_N + LANE];
   if (LANE < 4) E.target[LANE] = S.target[(size_t)i * 4 + LANE];
+  if (LANE < STAT_N) E.stats[LANE] = S.stats[(size_t)i * STAT_N + LANE];
   if (LANE == 0) {
     E.flags = 0;
     E.ncon = 0;
@@ -1429,6 +1545,7 @@ DEV void store_env(const MMXState& S, int i, const EnvSh& E) {
   if (LANE < 8) S.ctrl[(size_t)i * 8 + LANE] = E.ctrl[LANE];
   if (LANE < KIN_N) S.kin[(size_t)i * KIN_N + LANE] = E.kin[LANE];
   if (LANE < 4) S.target[(size_t)i * 4 + LANE] = E.target[LANE];
+  if (LANE < STAT_N) S.stats[(size_t)i * STAT_N + LANE] = E.stats[LANE];
 }
 DEV void store_obs(const MMXState& S, int i, const EnvSh& E) {
   SYNC();
@@ -1445,29 +1562,21 @@ DEV void store_contacts(const MMXState& S, int i, const EnvSh& E) {
 // plans first (plan(16)) and its abs_pos action is used (scripts/generate_dataset.py:140-190), so
 // an expert rollout costs one launch per env step.
 extern "C" __global__ void __launch_bounds__(WG) mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert) {
-  __shared__ EnvSh E;
+  EnvSh& E = g_E;
   __shared__ float act[12];
   const int i = blockIdx.x;
   if (i >= S.N) return;
   load_env(S, i, E);
-  float stats[STAT_N];
   if (LANE == 0) {
-#pragma unroll
-    for (int k = 0; k < STAT_N; k++) stats[k] = S.stats[(size_t)i * STAT_N + k];
     if (expert) expert_plan(S, i, obj_pos(E, EPI(EPI_OBJ)), hand_pos(E), MMX_NSUBSTEP, act);
     else
       for (int k = 0; k < adim && k < 12; k++) act[k] = action[(size_t)i * adim + k];
     decode_lane0(S, i, E, act);
   }
   SYNC();
-  for (int sub = 0; sub < MMX_NSUBSTEP; sub++) {
-    const unsigned long long t0 = tick();
-    if (LANE == 0) ik_lane0(E);  // IK on the kinematics left by the previous position stage
-    SYNC();
-    stats[STAT_T_IK] += (float)(tick() - t0);
-    mj_step_wave(S, E, stats);
-  }
-  const unsigned long long t_end = tick();
+  for (int sub = 0; sub < MMX_NSUBSTEP; sub++) substep(S.solver_max_iter, S.solver_tol, 1);
+  float* stats = E.stats;
+  CLK_DECL;
   store_contacts(S, i, E);
   // mj_forward position stage (gym_env.py:560): kinematics + contacts for the staged penalty
   if (LANE == 0) {
@@ -1514,9 +1623,7 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_env_step_kernel(MMXState S,
       EPI(EPI_ERROR) = 0;
       reset_lane0(S, i, E, -1);
     }
-    stats[STAT_T_END] += (float)(tick() - t_end);
-#pragma unroll
-    for (int k = 0; k < STAT_N; k++) S.stats[(size_t)i * STAT_N + k] = stats[k];
+    CLK(stats, STAT_T_END);
   }
   store_env(S, i, E);
   store_obs(S, i, E);
@@ -1524,23 +1631,14 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_env_step_kernel(MMXState S,
 
 // n raw mj_step substeps (optionally each preceded by the IK toward the stored target)
 extern "C" __global__ void __launch_bounds__(WG) mmx_physics_kernel(MMXState S, int n, int with_ik) {
-  __shared__ EnvSh E;
+  EnvSh& E = g_E;
   const int i = blockIdx.x;
   if (i >= S.N) return;
   load_env(S, i, E);
-  float stats[STAT_N];
-  if (LANE == 0)
-#pragma unroll
-    for (int k = 0; k < STAT_N; k++) stats[k] = S.stats[(size_t)i * STAT_N + k];
-  for (int sub = 0; sub < n; sub++) {
-    if (with_ik && LANE == 0) ik_lane0(E);
-    SYNC();
-    mj_step_wave(S, E, stats);
-  }
+  SYNC();
+  for (int sub = 0; sub < n; sub++) substep(S.solver_max_iter, S.solver_tol, with_ik);
   store_contacts(S, i, E);
   if (LANE == 0) {
-#pragma unroll
-    for (int k = 0; k < STAT_N; k++) S.stats[(size_t)i * STAT_N + k] = stats[k];
     EPI(EPI_NCON) = E.ncon;
     EPI(EPI_NEFC) = E.nefc;
     if (E.flags & SHF_NAN) EPI(EPI_ERROR) |= ERR_NAN;
@@ -1550,7 +1648,7 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_physics_kernel(MMXState S, 
 
 // mj_forward position stage only (kinematics -> IK cache) + observation refresh
 extern "C" __global__ void __launch_bounds__(WG) mmx_forward_kernel(MMXState S) {
-  __shared__ EnvSh E;
+  EnvSh& E = g_E;
   const int i = blockIdx.x;
   if (i >= S.N) return;
   load_env(S, i, E);
@@ -1563,7 +1661,7 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_forward_kernel(MMXState S) 
 }
 
 extern "C" __global__ void __launch_bounds__(WG) mmx_reset_kernel(MMXState S, const unsigned char* mask, const int* task) {
-  __shared__ EnvSh E;
+  EnvSh& E = g_E;
   const int i = blockIdx.x;
   if (i >= S.N) return;
   if (mask && !mask[i]) return;

@@ -51,10 +51,12 @@ enum { ERR_CON_OVERFLOW = 1, ERR_EFC_OVERFLOW = 2, ERR_NAN = 4, ERR_SAMPLING = 8
 // contact record fields
 enum { CON_DIST = 0, CON_POS = 1, CON_N = 4, CON_MU0 = 7, CON_MU1, CON_MU2, CON_DIM, CON_G1, CON_G2, CON_F };
 // statistics accumulated per env (over substeps since the last clear)
-// (STAT_T_*: shader-clock cycles per phase, read by lane 0 with s_memtime, summed over substeps)
+// (STAT_T_*: shader-clock cycles per phase, read with s_memtime and summed over substeps; only the
+//  diagnostic build libmmx_prof.so, compiled with -DMMX_PHASE_CLOCK, fills them)
 enum {
   STAT_NEFC = 0, STAT_NCON, STAT_SOLVER_ITER, STAT_SUBSTEPS, STAT_RESID,
   STAT_T_IK, STAT_T_KIN, STAT_T_DYN, STAT_T_COL, STAT_T_CON, STAT_T_SOLVE, STAT_T_INT, STAT_T_END,
+  STAT_T_AUX0, STAT_T_AUX1, STAT_T_AUX2, STAT_T_AUX3,  // sub-phase probes (see the kernel source)
   STAT_N
 };
 

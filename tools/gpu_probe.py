@@ -140,5 +140,5 @@ if __name__ == "__main__":
             out[name] = {"error": repr(ex), "tb": traceback.format_exc()}
         out[name + "_secs"] = time.time() - t
         print(name, json.dumps(out[name])[:600], flush=True)
-        with open(os.path.join(REPO, "gpurun_out", "probe.json"), "w") as f:
+        with open(os.path.join(REPO, "gpurun_out", "probe_prof.json" if os.environ.get("MMX_PROFILE", "0") not in ("", "0") else "probe.json"), "w") as f:
             json.dump(out, f, indent=1)
