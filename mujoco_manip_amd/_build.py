@@ -38,6 +38,7 @@ def _compile(src: str, profile: bool, verbose: bool) -> str:
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", os.path.join(CSRC, src), "-o", obj]
     if profile:
         cmd.insert(1, "-DMMX_PHASE_CLOCK=1")
+        cmd.insert(1, f"-DMMX_PROBE={int(os.environ.get('MMX_PROBE', '1'))}")
     if src.endswith(".cpp"):
         cmd.insert(1, "-xhip")
     if verbose:

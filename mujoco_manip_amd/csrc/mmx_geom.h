@@ -221,14 +221,69 @@ DEV void box_box(Sink& cs, const Geom& G1, const Geom& G2) {
   }
 }
 
-// ---------------------------------------------------------------- GJK + EPA
+// ---------------------------------------------------------------- GJK + EPA (wave-cooperative)
+// One geom pair at a time per wave: every lane runs the same, uniform GJK/EPA control flow; the
+// mesh support query is split over the lanes (hull vertices strided by lane, then a DPP arg-max
+// whose ties resolve to the lowest vertex index, as the serial scan does); the EPA polytope lives
+// in LDS scratch supplied by the caller.  Must be called with all 64 lanes active.
+template <int CTRL>
+DEV float gdpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL>
+DEV int gdpp_i(int v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+}
+DEV void argmax_merge(float& v, int& i, float v2, int i2) {
+  const bool take = v2 > v || (v2 == v && i2 < i);
+  v = take ? v2 : v;
+  i = take ? i2 : i;
+}
+template <int CTRL>
+DEV void argmax_dpp(float& v, int& i) {
+  argmax_merge(v, i, gdpp_f<CTRL>(v), gdpp_i<CTRL>(i));
+}
+DEV void wave_argmax(float& v, int& i) {
+  argmax_dpp<0xB1>(v, i);   // quad_perm [1,0,3,2]
+  argmax_dpp<0x4E>(v, i);   // quad_perm [2,3,0,1]
+  argmax_dpp<0x141>(v, i);  // row_half_mirror
+  argmax_dpp<0x140>(v, i);  // row_mirror
+  float bv = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+  int bi = __builtin_amdgcn_readlane(i, 0);
+#pragma unroll
+  for (int r = 1; r < 4; r++)
+    argmax_merge(bv, bi, __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16 * r)),
+                 __builtin_amdgcn_readlane(i, 16 * r));
+  v = bv;
+  i = bi;
+}
+DEV V3 support_wave(const Geom& G, V3 dir) {
+  if (G.type != GT_MESH) return support(G, dir);
+  const V3 dl = mulT(G.R, dir);
+  const int m = MMX_geom_mesh[G.g];
+  const int a = MMX_mesh_vertadr[m], nvert = MMX_mesh_vertnum[m];
+  float best = -3.0e38f;
+  int bi = 0x7fffffff;
+  for (int v = (int)threadIdx.x; v < nvert; v += 64) {
+    const int q = 3 * (a + v);
+    const float s = MMX_mesh_vert[q] * dl.x + MMX_mesh_vert[q + 1] * dl.y + MMX_mesh_vert[q + 2] * dl.z;
+    if (s > best) {
+      best = s;
+      bi = v;
+    }
+  }
+  wave_argmax(best, bi);
+  const int q = 3 * (a + bi);
+  return G.x + mul(G.R, V3{MMX_mesh_vert[q], MMX_mesh_vert[q + 1], MMX_mesh_vert[q + 2]});
+}
+
 struct SVx {
   V3 w, a, b;
 };
 DEV SVx mk_sv(const Geom& A, const Geom& B, V3 dir) {
   SVx s;
-  s.a = support(A, dir);
-  s.b = support(B, -dir);
+  s.a = support_wave(A, dir);
+  s.b = support_wave(B, -dir);
   s.w = s.a - s.b;
   return s;
 }
@@ -301,7 +356,9 @@ DEV bool gjk(const Geom& A, const Geom& B, SVx* S, int& n) {
     if (norm(dir) < 1e-12f) return true;
     const SVx P = mk_sv(A, B, dir);
     if (dot(P.w, dir) < 0.f) return false;
-    for (int k = n; k > 0; k--) S[k] = S[k - 1];
+#pragma unroll
+    for (int k = 3; k > 0; k--)  // static indices keep the simplex in registers
+      if (k <= n) S[k] = S[k - 1];
     S[0] = P;
     n++;
     const bool hit = n == 2 ? gjk_line(S, n, dir) : (n == 3 ? gjk_tri(S, n, dir) : gjk_tet(S, n, dir));
@@ -328,8 +385,9 @@ DEV bool epa_face(const SVx* V, EFace& f, int a, int b, int c) {
   f.d = dot(f.n, V[a].w);
   return true;
 }
-DEV bool epa(const Geom& A, const Geom& B, SVx* V, int nv, V3& nrm, float& depth, V3& pa, V3& pb) {
-  EFace F[EPA_MAXF];
+// V, F, edges: LDS scratch (EPA_MAXV SVx, EPA_MAXF EFace, 3 EPA_MAXF edge pairs)
+DEV bool epa(const Geom& A, const Geom& B, SVx* V, int nv, V3& nrm, float& depth, V3& pa, V3& pb, EFace* F,
+             int (*edges)[2]) {
   int nf = 0;
   const V3 dirs[6] = {V3{1.f, 0.f, 0.f}, V3{-1.f, 0.f, 0.f}, V3{0.f, 1.f, 0.f},
                       V3{0.f, -1.f, 0.f}, V3{0.f, 0.f, 1.f}, V3{0.f, 0.f, -1.f}};
@@ -375,7 +433,6 @@ DEV bool epa(const Geom& A, const Geom& B, SVx* V, int nv, V3& nrm, float& depth
     const SVx P = mk_sv(A, B, F[best].n);
     const float dist = dot(P.w, F[best].n);
     if (dist - F[best].d < 1e-6f * (1.f + fabsf(dist)) || nv >= EPA_MAXV) break;
-    int edges[EPA_MAXF * 3][2];
     int ne = 0, m = 0;
     for (int k = 0; k < nf; k++) {
       const EFace f = F[k];
@@ -425,17 +482,25 @@ DEV bool epa(const Geom& A, const Geom& B, SVx* V, int nv, V3& nrm, float& depth
   return true;
 }
 
+#define EPA_SCRATCH_FLOATS (9 * EPA_MAXV + 7 * EPA_MAXF + 6 * EPA_MAXF)
+// scr: EPA_SCRATCH_FLOATS of LDS; emits at most one contact (lane 0)
 template <class Sink>
-DEV void convex_convex(Sink& cs, const Geom& A, const Geom& B) {
-  SVx V[EPA_MAXV];
+DEV void convex_convex(Sink& cs, const Geom& A, const Geom& B, float* scr) {
+  SVx S[4];
   int n = 0;
-  if (!gjk(A, B, V, n)) return;
+  if (!gjk(A, B, S, n)) return;
+  SVx* V = reinterpret_cast<SVx*>(scr);
+  EFace* F = reinterpret_cast<EFace*>(scr + 9 * EPA_MAXV);
+  int(*edges)[2] = reinterpret_cast<int(*)[2]>(scr + 9 * EPA_MAXV + 7 * EPA_MAXF);
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    if (k < n) V[k] = S[k];
   V3 nrm, pa, pb;
   float depth;
-  if (!epa(A, B, V, n, nrm, depth, pa, pb)) return;
+  if (!epa(A, B, V, n, nrm, depth, pa, pb, F, edges)) return;
   if (depth < 0.f) return;
   // Minkowski A-B face normal n: translating B by +depth n separates -> normal A->B is n
-  cs.add(A.g, B.g, -depth, (pa + pb) * 0.5f, nrm);
+  if (threadIdx.x == 0) cs.add(A.g, B.g, -depth, (pa + pb) * 0.5f, nrm);
 }
 
 // soft-constraint impedance d(pos) (MuJoCo solimp: dmin, dmax, width, midpoint, power)

@@ -58,7 +58,6 @@ struct EnvSh {
   alignas(16) float r[MMX_MAXEFC + 8], s[MMX_MAXEFC + 8];
   float aref[MMX_MAXEFC], D[MMX_MAXEFC];
   float Lrow[27][27];  // Newton Cholesky factor, row-major (read back as columns)
-  int bpscan[MMX_NBODYPAIR + 1];
   float obs[MMX_NOBS + 3];
   int ncon, nefc, flags, iters;
   int act_unclamped[8];
@@ -116,6 +115,15 @@ DEV SV load_S(const EnvSh& E, int d) { return SV{V3{E.S[d][0], E.S[d][1], E.S[d]
   do {             \
   } while (0)
 #endif
+// sub-phase probes into STAT_T_AUX0..3: MMX_PROBE selects the phase they instrument
+// (1 solver, 2 collision, 3 constraints)
+#ifndef MMX_PROBE
+#define MMX_PROBE 1
+#endif
+#define PROBE(set, st, k)            \
+  do {                               \
+    if (MMX_PROBE == (set)) CLK(st, k); \
+  } while (0)
 
 // ---------------------------------------------------------------- wave primitives
 // wave64 sum: DPP butterflies inside each row of 16 lanes, then the four row sums in a fixed
@@ -447,83 +455,153 @@ struct WaveSink {
   }
 };
 
-DEV bool bodypair_pass(const EnvSh& E, int bp, bool only_ro) {
-  const int b1 = MMX_bodypair[4 * bp], b2 = MMX_bodypair[4 * bp + 1], start = MMX_bodypair[4 * bp + 2];
-  if (only_ro) {
-    const int c1 = MMX_geom_class[MMX_bodypair_geoms[2 * start]], c2 = MMX_geom_class[MMX_bodypair_geoms[2 * start + 1]];
-    if (!((c1 == 1 && c2 == 2) || (c1 == 2 && c2 == 1))) return false;
+// LDS scratch layout of the collision phase (inside E.J, which is rebuilt after collision)
+#define COL_GX 0      // [NGEOM][16] world pose (x3, R9), rbound, type
+#define COL_CAND 768  // [COL_LIST] candidate pairs after the sphere test
+#define COL_LIST 784
+#define COL_CLS (COL_CAND + COL_LIST)  // 3 x [COL_LIST] pairs per narrowphase class
+#define COL_SORT (COL_CLS + 3 * COL_LIST)
+static_assert(COL_SORT + MMX_MAXCON * CON_F <= MMX_MAXEFC * 16, "collision scratch exceeds E.J");
+static_assert(MMX_NGEOM * 16 <= COL_CAND && MMX_NPAIR <= COL_LIST, "collision scratch layout");
+static_assert(EPA_SCRATCH_FLOATS <= 3 * COL_LIST, "EPA scratch exceeds the consumed lists");
+
+DEV Geom geom_lds(const float* gx, int g) {
+  const float* o = gx + 16 * g;
+  Geom G;
+  G.g = g;
+  G.type = __float_as_int(o[13]);
+  G.x = V3{o[0], o[1], o[2]};
+#pragma unroll
+  for (int k = 0; k < 9; k++) G.R.m[k] = o[3 + k];
+  return G;
+}
+// geoms of pair p ordered by type (plane first), as the narrowphase dispatch expects
+DEV void pair_geoms(const float* gx, int p, int& g1, int& g2) {
+  g1 = MMX_bodypair_geoms[2 * p];
+  g2 = MMX_bodypair_geoms[2 * p + 1];
+  if (__float_as_int(gx[16 * g1 + 13]) > __float_as_int(gx[16 * g2 + 13])) {
+    const int t = g1;
+    g1 = g2;
+    g2 = t;
   }
-  if (b1 != 0 && b2 != 0) {
-    const float r1 = MMX_body_bsphere[4 * b1 + 3], r2 = MMX_body_bsphere[4 * b2 + 3];
-    const V3 l1 = V3{MMX_body_bsphere[4 * b1], MMX_body_bsphere[4 * b1 + 1], MMX_body_bsphere[4 * b1 + 2]};
-    const V3 l2 = V3{MMX_body_bsphere[4 * b2], MMX_body_bsphere[4 * b2 + 1], MMX_body_bsphere[4 * b2 + 2]};
-    const V3 c1 = MMX_body_static[b1] ? l1 : body_x(E, b1) + mul(body_R(E, b1), l1);
-    const V3 c2 = MMX_body_static[b2] ? l2 : body_x(E, b2) + mul(body_R(E, b2), l2);
-    const V3 dd = c2 - c1;
-    return dot(dd, dd) <= (r1 + r2) * (r1 + r2);
-  }
-  const int bo = b1 == 0 ? b2 : b1;  // world body = floor plane z = 0
-  const V3 l = V3{MMX_body_bsphere[4 * bo], MMX_body_bsphere[4 * bo + 1], MMX_body_bsphere[4 * bo + 2]};
-  const V3 c = body_x(E, bo) + mul(body_R(E, bo), l);
-  return c.z <= MMX_body_bsphere[4 * bo + 3];
+}
+DEV bool robot_obstacle(int g1, int g2) {
+  const int c1 = MMX_geom_class[g1], c2 = MMX_geom_class[g2];
+  return (c1 == 1 && c2 == 2) || (c1 == 2 && c2 == 1);
+}
+// stream compaction of one wave's flags into list[base...]; returns the new length
+DEV int wave_compact(bool keep, int* list, int base, int val) {
+  const unsigned long long m = __ballot(keep);
+  const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+  if (keep) list[base + pos] = val;
+  return base + __popcll(m);
 }
 
-DEV void narrowphase(WaveSink& cs, const EnvSh& E, int p) {
-  int g1 = MMX_bodypair_geoms[2 * p], g2 = MMX_bodypair_geoms[2 * p + 1];
-  int t1 = MMX_geom_type[g1], t2 = MMX_geom_type[g2];
-  if (t1 > t2) {
-    int t = g1; g1 = g2; g2 = t;
-    t = t1; t1 = t2; t2 = t;
-  }
-  const Geom A = geom_pose(E, g1), B = geom_pose(E, g2);
-  if (t1 == GT_PLANE) {
-    if (dot(B.x - A.x, col(A.R, 2)) > MMX_geom_rbound[g2]) return;
-    if (t2 == GT_BOX) plane_box(cs, A, B);
-    else if (t2 == GT_MESH) plane_convex(cs, A, B);
-    return;
-  }
-  const V3 dd = B.x - A.x;
-  const float rb = MMX_geom_rbound[g1] + MMX_geom_rbound[g2];
-  if (dot(dd, dd) > rb * rb) return;
-  if (!obb_overlap(A, B)) return;
-  if (t1 == GT_BOX && t2 == GT_BOX) box_box(cs, A, B);
-  else convex_convex(cs, A, B);
-}
-
-// broadphase over body pairs (lanes), scan of candidate geom-pair counts, narrowphase over the
-// flattened geom-pair task list (lanes), then a deterministic rank sort of the contacts.
+// Collision in coherent stages: (1) world poses of all geoms into LDS, one lane per geom;
+// (2) bounding-sphere / plane-distance prune of all pairs, compacted with ballots; (3) OBB prune
+// and split by narrowphase class; (4) one pass per class (plane-convex/box, box-box, GJK/EPA), so
+// lanes of a pass run the same code; (5) deterministic rank sort of the contacts by pair key.
+// Every prune is conservative, so the contact set equals the all-pairs narrowphase.
 DEV void collide_wave(EnvSh& E, bool only_ro) {
+  float* stats = E.stats;
+  CLK_DECL;
   if (LANE == 0) {
     E.ncon = 0;
     E.flags &= ~(SHF_ROBOT_OBST | SHF_CON_OVF);
   }
-  int carry = 0;
-  for (int base = 0; base < MMX_NBODYPAIR; base += WG) {
-    const int bp = base + LANE;
-    int cnt = 0;
-    if (bp < MMX_NBODYPAIR && bodypair_pass(E, bp, only_ro)) cnt = MMX_bodypair[4 * bp + 3];
-    const int incl = wave_scan_incl(cnt);
-    if (bp < MMX_NBODYPAIR) E.bpscan[bp] = carry + incl - cnt;
-    carry += __shfl(incl, 63, 64);
+  float* scr = &E.J[0][0];
+  float* gx = scr + COL_GX;
+  int* cand = reinterpret_cast<int*>(scr + COL_CAND);
+  int* cls = reinterpret_cast<int*>(scr + COL_CLS);
+  if (LANE < MMX_NGEOM) {
+    const Geom G = geom_pose(E, LANE);
+    float* o = gx + 16 * LANE;
+    o[0] = G.x.x; o[1] = G.x.y; o[2] = G.x.z;
+#pragma unroll
+    for (int k = 0; k < 9; k++) o[3 + k] = G.R.m[k];
+    o[12] = MMX_geom_rbound[LANE];
+    o[13] = __int_as_float(G.type);
   }
-  if (LANE == 0) E.bpscan[MMX_NBODYPAIR] = carry;
   SYNC();
-  const int T = carry;
-  for (int t = LANE; t < T; t += WG) {
-    int lo = 0, hi = MMX_NBODYPAIR;  // largest bp with bpscan[bp] <= t
-    while (hi - lo > 1) {
-      const int mid = (lo + hi) >> 1;
-      if (E.bpscan[mid] <= t) lo = mid;
-      else hi = mid;
+  int nc = 0;
+  for (int base = 0; base < MMX_NPAIR; base += WG) {
+    const int p = base + LANE;
+    bool keep = false;
+    if (p < MMX_NPAIR) {
+      int g1, g2;
+      pair_geoms(gx, p, g1, g2);
+      if (!only_ro || robot_obstacle(g1, g2)) {
+        const float* o1 = gx + 16 * g1;
+        const float* o2 = gx + 16 * g2;
+        const V3 d = V3{o2[0] - o1[0], o2[1] - o1[1], o2[2] - o1[2]};
+        if (__float_as_int(o1[13]) == GT_PLANE) {
+          keep = d.x * o1[5] + d.y * o1[8] + d.z * o1[11] <= o2[12];  // distance above the plane
+        } else {
+          const float rb = o1[12] + o2[12];
+          keep = dot(d, d) <= rb * rb;
+        }
+      }
     }
-    const int p = MMX_bodypair[4 * lo + 2] + (t - E.bpscan[lo]);
-    WaveSink cs{&E, p * 8, !only_ro};
-    narrowphase(cs, E, p);
+    nc = wave_compact(keep, cand, nc, p);
   }
   SYNC();
+  PROBE(2, stats, STAT_T_AUX0);
+  int ncls[3] = {0, 0, 0};
+  for (int base = 0; base < nc; base += WG) {
+    const int k = base + LANE;
+    int c = -1, p = 0;
+    if (k < nc) {
+      p = cand[k];
+      int g1, g2;
+      pair_geoms(gx, p, g1, g2);
+      const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
+      if (A.type == GT_PLANE) c = 0;
+      else if (obb_overlap(A, B)) c = (A.type == GT_BOX && B.type == GT_BOX) ? 1 : 2;
+    }
+#pragma unroll
+    for (int q = 0; q < 3; q++) ncls[q] = wave_compact(c == q, cls + q * COL_LIST, ncls[q], p);
+  }
+  SYNC();
+  PROBE(2, stats, STAT_T_AUX0);
+  if (MMX_PROBE == 4 && LANE == 0) {
+    stats[STAT_T_AUX0] += (float)nc;
+    stats[STAT_T_AUX1] += (float)ncls[1];
+    stats[STAT_T_AUX2] += (float)ncls[2];
+    stats[STAT_T_AUX3] += (float)ncls[0];
+  }
+#pragma unroll
+  for (int q = 0; q < 2; q++) {  // lane per pair
+    for (int k = LANE; k < ncls[q]; k += WG) {
+      const int p = cls[q * COL_LIST + k];
+      int g1, g2;
+      pair_geoms(gx, p, g1, g2);
+      const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
+      WaveSink cs{&E, p * 8, !only_ro};
+      if (q == 0) {
+        if (B.type == GT_BOX) plane_box(cs, A, B);
+        else if (B.type == GT_MESH) plane_convex(cs, A, B);
+      } else {
+        box_box(cs, A, B);
+      }
+    }
+    SYNC();
+    PROBE(2, stats, STAT_T_AUX1 + q);
+  }
+  // GJK / EPA pairs: the whole wave on one pair at a time (EPA polytope in the consumed
+  // candidate / class-0 / class-1 lists)
+  for (int k = 0; k < ncls[2]; k++) {
+    const int p = cls[2 * COL_LIST + k];
+    int g1, g2;
+    pair_geoms(gx, p, g1, g2);
+    const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
+    WaveSink cs{&E, p * 8, !only_ro};
+    convex_convex(cs, A, B, scr + COL_CAND);
+  }
+  SYNC();
+  PROBE(2, stats, STAT_T_AUX3);
   if (only_ro) return;
   const int n = min(E.ncon, MMX_MAXCON);
-  float* tmp = &E.J[0][0];
+  float* tmp = scr + COL_SORT;
   if (LANE < n) {
     const int key = E.conkey[LANE];
     int rank = 0;
@@ -586,6 +664,8 @@ DEV void finish_row(EnvSh& E, int row, const float* Jd, int b0, int b1, float po
 }
 
 DEV void make_constraints_wave(EnvSh& E) {
+  float* stats = E.stats;
+  CLK_DECL;
   const float def_ref[2] = {0.02f, 1.0f};
   const float def_imp[5] = {0.9f, 0.95f, 0.001f, 0.5f, 2.0f};
   const int ncon = E.ncon;
@@ -610,6 +690,7 @@ DEV void make_constraints_wave(EnvSh& E) {
     E.nefc = min(total, MMX_MAXEFC);
     if (total > MMX_MAXEFC) E.flags |= SHF_EFC_OVF;
   }
+  PROBE(3, stats, STAT_T_AUX0);
   float Jd[27];
   if (LANE == 0 && row < MMX_MAXEFC) {  // finger equality (panda.xml:261)
 #pragma unroll
@@ -634,6 +715,7 @@ DEV void make_constraints_wave(EnvSh& E) {
       }
     }
   }
+  PROBE(3, stats, STAT_T_AUX1);
   if (LANE < ncon) {
     const float* c = E.con[LANE];
     const float dist = c[CON_DIST];
@@ -679,6 +761,7 @@ DEV void make_constraints_wave(EnvSh& E) {
     }
   }
   SYNC();
+  PROBE(3, stats, STAT_T_AUX2);
 }
 
 // ============================================================================ Newton solver (wave)
@@ -878,7 +961,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
   SYNC();
   int it = 0;
   resid = 0.f;
-  CLK(stats, STAT_T_AUX3);
+  PROBE(1, stats, STAT_T_AUX3);
   for (; it < max_iter; it++) {
     // residuals r = J x - aref and active weights s (LDS copies feed the MFMA pass)
 #pragma unroll
@@ -892,16 +975,16 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
       }
     }
     SYNC();
-    CLK(stats, STAT_T_AUX0);
+    PROBE(1, stats, STAT_T_AUX0);
     float hrow[32];
     const float g = hess_grad_mfma(E, nefc, hrow);
     resid = sqrtf(wave_sum(g * g)) / scale;
-    CLK(stats, STAT_T_AUX1);
+    PROBE(1, stats, STAT_T_AUX1);
     if (resid < tol) break;
     const float pj = chol_solve_reg(E, hrow, -g);
     if (LANE < 27) E.p[LANE] = pj;
     SYNC();
-    CLK(stats, STAT_T_AUX2);
+    PROBE(1, stats, STAT_T_AUX2);
     // exact line search on phi(a) = cost(x + a p): phi' is piecewise linear and increasing
 #pragma unroll
     for (int q = 0; q < RPL; q++) {
@@ -940,7 +1023,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
       }
       alpha = na;
     }
-    CLK(stats, STAT_T_AUX3);
+    PROBE(1, stats, STAT_T_AUX3);
     float stepn = 0.f;
     if (LANE < 27) {
       E.x[LANE] += alpha * pj;
