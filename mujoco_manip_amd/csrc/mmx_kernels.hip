@@ -616,60 +616,121 @@ DEV void collide_wave(EnvSh& E, bool only_ro) {
 }
 
 // ============================================================================ constraints (wave)
-// J (dense 27) of a point on body b projected on (u: linear, w: angular), accumulated with sign sg
-DEV void body_jac_proj(const EnvSh& E, int b, V3 p, V3 u, V3 w, float sg, float* J) {
-  const int blk = body_block(b);
-  if (blk == 0) {
-#pragma unroll
-    for (int d = 0; d < 9; d++) {
-      if (!arm_anc(d, b)) continue;
-      const SV s = load_S(E, d);
-      J[d] += sg * (dot(u, s.v + cross(s.w, p)) + dot(w, s.w));
-    }
-  } else if (blk > 0) {
-    const int d0 = 9 + 6 * (blk - 1);
-    const V3 x = body_x(E, b);
-    const M3 R = body_R(E, b);
-    J[d0] += sg * u.x; J[d0 + 1] += sg * u.y; J[d0 + 2] += sg * u.z;
-#pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const V3 r = col(R, k);
-      J[d0 + 3 + k] += sg * (dot(u, cross(r, p - x)) + dot(w, r));
-    }
-  }
-}
-
-// compress a dense 27-column row into block format and compute its impedance terms
-DEV void finish_row(EnvSh& E, int row, const float* Jd, int b0, int b1, float pos, float diag, const float* solref,
-                    const float* solimp, int is_eq) {
-  const int n0 = blk_size(b0), d0 = blk_d0(b0);
-  for (int k = 0; k < n0; k++) E.J[row][k] = Jd[d0 + k];
-  int k = n0;
-  if (b1 != BLK_NONE) {
-    const int d1 = blk_d0(b1);
-    for (; k < n0 + 6; k++) E.J[row][k] = Jd[d1 + k - n0];
-  }
-  for (; k < 16; k++) E.J[row][k] = 0.f;
-  E.hdr[row] = b0 | (b1 << 4) | (is_eq << 8);
-  float vel = 0.f;
-#pragma unroll
-  for (int d = 0; d < 27; d++) vel += Jd[d] * E.qvel[d];
+// Soft-constraint reference terms of a row: K, B from solref, impedance from solimp (MuJoCo
+// mj_makeImpedance); D = 1 / R with R = (1 - imp) / imp * diag.
+DEV void row_ref(const float* solref, const float* solimp, float pos, float& imp_ratio, float& kid, float& B) {
   const float imp = impedance(solimp, pos);
   const float dmax = fminf(fmaxf(solimp[1], 1e-4f), 0.9999f);
   const float tc = fmaxf(solref[0], 2.f * kDt), dr = solref[1];
-  const float K = 1.f / (dmax * dmax * tc * tc * dr * dr), B = 2.f / (dmax * tc);
-  const float R = fmaxf((1.f - imp) / imp * diag, 1e-15f);
-  E.aref[row] = -B * vel - K * imp * pos;
-  E.D[row] = 1.f / R;
+  const float K = 1.f / (dmax * dmax * tc * tc * dr * dr);
+  B = 2.f / (dmax * tc);
+  imp_ratio = (1.f - imp) / imp;
+  kid = K * imp * pos;
+}
+DEV void store_row(EnvSh& E, int row, const float* jv, int hdr, float vel, float imp_ratio, float kid, float B,
+                   float diag) {
+  float4* Jr = reinterpret_cast<float4*>(E.J[row]);
+#pragma unroll
+  for (int q = 0; q < 4; q++) Jr[q] = make_float4(jv[4 * q], jv[4 * q + 1], jv[4 * q + 2], jv[4 * q + 3]);
+  E.hdr[row] = hdr;
+  E.aref[row] = -B * vel - kid;
+  E.D[row] = 1.f / fmaxf(imp_ratio * diag, 1e-15f);
 }
 
+// per-contact row generator, written by the contact's lane and read by its rows' lanes
+// (kept in E.r / E.s, which the solver overwrites later)
+enum { CG_T1 = 0, CG_IMPR = 3, CG_KID, CG_B, CG_TRAN, CG_ROT, CG_MU0, CG_MU1, CG_N };
+
+// one pyramid row (rr) of contact c, built straight into block format: an arm block entry is
+// the motion subspace of dof d seen at the contact point, a cube block the free-body Jacobian
+DEV void contact_row(EnvSh& E, int row, int c, int rr) {
+  const float* cc = E.con[c];
+  float cgv[CG_N];
+#pragma unroll
+  for (int k = 0; k < CG_N; k++) cgv[k] = k < 5 ? E.r[5 * c + k] : E.s[5 * c + k - 5];
+  const V3 p = V3{cc[CON_POS], cc[CON_POS + 1], cc[CON_POS + 2]};
+  const V3 n = V3{cc[CON_N], cc[CON_N + 1], cc[CON_N + 2]};
+  const int dim = (int)cc[CON_DIM];
+  const int b1 = MMX_geom_body[(int)cc[CON_G1]], b2 = MMX_geom_body[(int)cc[CON_G2]];
+  const V3 t1 = V3{cgv[CG_T1], cgv[CG_T1 + 1], cgv[CG_T1 + 2]};
+  V3 u = n, w = V3{0.f, 0.f, 0.f};
+  float diag = cgv[CG_TRAN];
+  if (dim > 1) {  // pyramid edge J_n +/- mu_k J_k
+    const int k = rr >> 1;
+    const float mu = k < 2 ? cgv[CG_MU0] : cgv[CG_MU1];
+    const float sg = (rr & 1) ? -mu : mu;
+    if (k == 0) u = n + t1 * sg;
+    else if (k == 1) u = n + cross(n, t1) * sg;
+    else w = n * sg;
+    diag = cgv[CG_TRAN] + mu * mu * (k < 2 ? cgv[CG_TRAN] : cgv[CG_ROT]);
+  }
+  const int k1 = body_block(b1), k2 = body_block(b2);
+  int rb0 = k1 >= 0 ? k1 : k2, rb1 = (k1 >= 0 && k2 >= 0 && k2 != k1) ? k2 : BLK_NONE;
+  if (rb1 != BLK_NONE && rb1 < rb0) {
+    const int t = rb0;
+    rb0 = rb1;
+    rb1 = t;
+  }
+  float vel = 0.f;
+  float arm[9];
+#pragma unroll
+  for (int d = 0; d < 9; d++) {  // body 2 counts +, body 1 counts -
+    const float coef = (arm_anc(d, b2) ? 1.f : 0.f) - (arm_anc(d, b1) ? 1.f : 0.f);
+    const SV sd = load_S(E, d);
+    arm[d] = coef * (dot(u, sd.v + cross(sd.w, p)) + dot(w, sd.w));
+    vel = fmaf(arm[d], E.qvel[d], vel);
+  }
+  float cubeA[6], cubeB[6];  // blocks rb0 (when a cube) and rb1
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+    cubeA[j] = 0.f;
+    cubeB[j] = 0.f;
+  }
+#pragma unroll
+  for (int side = 0; side < 2; side++) {
+    const int b = side ? b2 : b1, blk = side ? k2 : k1;
+    if (blk > 0) {
+      const float sg = side ? 1.f : -1.f;
+      const V3 x = body_x(E, b);
+      const M3 R = body_R(E, b);
+      float cv[6] = {sg * u.x, sg * u.y, sg * u.z, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        const V3 rk = col(R, k);
+        cv[3 + k] = sg * (dot(u, cross(rk, p - x)) + dot(w, rk));
+      }
+      const int d0 = blk_d0(blk);
+      const bool toA = blk == rb0;
+#pragma unroll
+      for (int j = 0; j < 6; j++) {
+        cubeA[j] += toA ? cv[j] : 0.f;
+        cubeB[j] += toA ? 0.f : cv[j];
+        vel = fmaf(cv[j], E.qvel[d0 + j], vel);
+      }
+    }
+  }
+  float jv[16];
+  const bool armrow = rb0 == 0;
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    const float va = j < 9 ? arm[j] : (j < 15 ? cubeB[j - 9] : 0.f);
+    const float vc = j < 6 ? cubeA[j] : (j < 12 ? cubeB[j - 6] : 0.f);
+    jv[j] = armrow ? va : vc;
+  }
+  store_row(E, row, jv, rb0 | (rb1 << 4), vel, cgv[CG_IMPR], cgv[CG_KID], cgv[CG_B], diag);
+}
+
+// Constraint rows in MuJoCo's order per lane scan: finger equality (lane 0), joint limits
+// (lanes 0..8), contact pyramids (lane c = contact c).  Equality and limit rows are written by
+// their lanes; contact rows are spread over all lanes through a row -> (contact, edge) map.
 DEV void make_constraints_wave(EnvSh& E) {
   float* stats = E.stats;
   CLK_DECL;
   const float def_ref[2] = {0.02f, 1.0f};
   const float def_imp[5] = {0.9f, 0.95f, 0.001f, 0.5f, 2.0f};
   const int ncon = E.ncon;
-  // rows owned by this lane: lane 0 the equality, lanes 0..8 joint limits, lanes < ncon contacts
+  int* rowmap = reinterpret_cast<int*>(&E.Lrow[0][0]);  // Lrow is free until the solver
+  static_assert(27 * 27 >= MMX_MAXEFC, "rowmap scratch");
   int nlim = 0, ncr = 0, dim = 0;
   bool lo_act = false, hi_act = false;
   if (LANE < 9) {
@@ -686,79 +747,74 @@ DEV void make_constraints_wave(EnvSh& E) {
   const int incl = wave_scan_incl(mine);
   const int total = __shfl(incl, 63, 64);
   int row = incl - mine;
+  const int nefc = min(total, MMX_MAXEFC);
   if (LANE == 0) {
-    E.nefc = min(total, MMX_MAXEFC);
+    E.nefc = nefc;
     if (total > MMX_MAXEFC) E.flags |= SHF_EFC_OVF;
   }
   PROBE(3, stats, STAT_T_AUX0);
-  float Jd[27];
+  float jv[16];
   if (LANE == 0 && row < MMX_MAXEFC) {  // finger equality (panda.xml:261)
 #pragma unroll
-    for (int d = 0; d < 27; d++) Jd[d] = 0.f;
-    Jd[7] = 1.f;
-    Jd[8] = -1.f;
-    finish_row(E, row, Jd, 0, BLK_NONE, E.qpos[7] - E.qpos[8], MMX_dof_invweight0[7] + MMX_dof_invweight0[8],
-               MMX_eq_solref, MMX_eq_solimp, 1);
+    for (int j = 0; j < 16; j++) jv[j] = j == 7 ? 1.f : (j == 8 ? -1.f : 0.f);
+    float ir, kid, B;
+    row_ref(MMX_eq_solref, MMX_eq_solimp, E.qpos[7] - E.qpos[8], ir, kid, B);
+    store_row(E, row, jv, 0 | (BLK_NONE << 4) | (1 << 8), E.qvel[7] - E.qvel[8], ir, kid, B,
+              MMX_dof_invweight0[7] + MMX_dof_invweight0[8]);
+    rowmap[row] = -1;
     row++;
   }
   if (LANE < 9) {
     const float q = E.qpos[LANE];
+#pragma unroll
     for (int side = 0; side < 2; side++) {
       const bool act = side == 0 ? lo_act : hi_act;
       if (act && row < MMX_MAXEFC) {
+        const float sg = side == 0 ? 1.f : -1.f;
 #pragma unroll
-        for (int d = 0; d < 27; d++) Jd[d] = 0.f;
-        Jd[LANE] = side == 0 ? 1.f : -1.f;
+        for (int j = 0; j < 16; j++) jv[j] = j == LANE ? sg : 0.f;
         const float dist = side == 0 ? q - MMX_jnt_range[2 * LANE] : MMX_jnt_range[2 * LANE + 1] - q;
-        finish_row(E, row, Jd, 0, BLK_NONE, dist, MMX_dof_invweight0[LANE], def_ref, def_imp, 0);
+        float ir, kid, B;
+        row_ref(def_ref, def_imp, dist, ir, kid, B);
+        store_row(E, row, jv, 0 | (BLK_NONE << 4), sg * E.qvel[LANE], ir, kid, B, MMX_dof_invweight0[LANE]);
+        rowmap[row] = -1;
         row++;
       }
     }
   }
   PROBE(3, stats, STAT_T_AUX1);
-  if (LANE < ncon) {
+  if (LANE < ncon) {  // contact generator: frame, mixed parameters, reference terms
     const float* c = E.con[LANE];
-    const float dist = c[CON_DIST];
-    const V3 p = V3{c[CON_POS], c[CON_POS + 1], c[CON_POS + 2]};
     const V3 n = V3{c[CON_N], c[CON_N + 1], c[CON_N + 2]};
-    const float mu[3] = {c[CON_MU0], c[CON_MU0], c[CON_MU1]};
     const int g1 = (int)c[CON_G1], g2 = (int)c[CON_G2];
     const int b1 = MMX_geom_body[g1], b2 = MMX_geom_body[g2];
     const V3 y = (n.y < 0.5f && n.y > -0.5f) ? V3{0.f, 1.f, 0.f} : V3{0.f, 0.f, 1.f};  // mju_makeFrame
     const V3 t1 = normalize(y - n * dot(n, y));
-    const V3 t2 = cross(n, t1);
     float solref[2], solimp[5];
 #pragma unroll
     for (int k = 0; k < 2; k++) solref[k] = 0.5f * (MMX_geom_solref[2 * g1 + k] + MMX_geom_solref[2 * g2 + k]);
 #pragma unroll
     for (int k = 0; k < 5; k++) solimp[k] = 0.5f * (MMX_geom_solimp[5 * g1 + k] + MMX_geom_solimp[5 * g2 + k]);
-    const float tran = MMX_body_invweight0[2 * b1] + MMX_body_invweight0[2 * b2];
-    const float rot = MMX_body_invweight0[2 * b1 + 1] + MMX_body_invweight0[2 * b2 + 1];
-    // dof blocks of the row: sorted, deduplicated, static bodies contribute none
-    const int k1 = body_block(b1), k2 = body_block(b2);
-    int rb0 = k1 >= 0 ? k1 : k2, rb1 = (k1 >= 0 && k2 >= 0 && k2 != k1) ? k2 : BLK_NONE;
-    if (rb1 != BLK_NONE && rb1 < rb0) {
-      const int t = rb0;
-      rb0 = rb1;
-      rb1 = t;
-    }
-    for (int rr = 0; rr < ncr && row < MMX_MAXEFC; rr++, row++) {
-      V3 u = n, w = V3{0.f, 0.f, 0.f};
-      float diag = tran;
-      if (dim > 1) {  // pyramid edge J_n +/- mu_k J_k
-        const int k = rr >> 1;
-        const float sg = (rr & 1) ? -mu[k] : mu[k];
-        if (k == 0) u = n + t1 * sg;
-        else if (k == 1) u = n + t2 * sg;
-        else w = n * sg;
-        diag = tran + mu[k] * mu[k] * (k < 2 ? tran : rot);
-      }
+    float cgv[CG_N];
+    cgv[CG_T1] = t1.x;
+    cgv[CG_T1 + 1] = t1.y;
+    cgv[CG_T1 + 2] = t1.z;
+    row_ref(solref, solimp, c[CON_DIST], cgv[CG_IMPR], cgv[CG_KID], cgv[CG_B]);
+    cgv[CG_TRAN] = MMX_body_invweight0[2 * b1] + MMX_body_invweight0[2 * b2];
+    cgv[CG_ROT] = MMX_body_invweight0[2 * b1 + 1] + MMX_body_invweight0[2 * b2 + 1];
+    cgv[CG_MU0] = c[CON_MU0];
+    cgv[CG_MU1] = c[CON_MU1];
 #pragma unroll
-      for (int d = 0; d < 27; d++) Jd[d] = 0.f;
-      body_jac_proj(E, b1, p, u, w, -1.f, Jd);
-      body_jac_proj(E, b2, p, u, w, 1.f, Jd);
-      finish_row(E, row, Jd, rb0, rb1, dist, diag, solref, solimp, 0);
+    for (int k = 0; k < CG_N; k++) {
+      if (k < 5) E.r[5 * LANE + k] = cgv[k];
+      else E.s[5 * LANE + k - 5] = cgv[k];
     }
+    for (int rr = 0; rr < ncr && row < MMX_MAXEFC; rr++, row++) rowmap[row] = LANE | (rr << 8);
+  }
+  SYNC();
+  for (int r = LANE; r < nefc; r += WG) {
+    const int m = rowmap[r];
+    if (m >= 0) contact_row(E, r, m & 255, m >> 8);
   }
   SYNC();
   PROBE(3, stats, STAT_T_AUX2);
