@@ -1298,18 +1298,6 @@ DEV void mj_step_wave(int max_iter, float tol, EnvSh& E) {
   SYNC();
 }
 
-// One substep = [IK] + mj_step, kept out of line: every phase's loop invariants are recomputed
-// per call instead of being hoisted across all 16 substeps, which would pin registers for the
-// whole kernel and serialise the phases' LDS loads.
-__device__ __attribute__((noinline)) void substep(int max_iter, float tol, int with_ik) {
-  EnvSh& E = g_E;
-  CLK_DECL;
-  if (with_ik && LANE == 0) ik_lane0(E);  // IK on the kinematics left by the previous position stage
-  SYNC();
-  CLK(E.stats, STAT_T_IK);
-  mj_step_wave(max_iter, tol, E);
-}
-
 // ============================================================================ RNG (numpy PCG64)
 struct Pcg {
   unsigned long long shi, slo, ihi, ilo;
@@ -1697,23 +1685,21 @@ DEV void store_contacts(const MMXState& S, int i, const EnvSh& E) {
 }
 
 // ============================================================================ kernels
-// One env per 64-lane workgroup: the full PickPlaceGymEnv.step.  With expert != 0 the FSM expert
-// plans first (plan(16)) and its abs_pos action is used (scripts/generate_dataset.py:140-190), so
-// an expert rollout costs one launch per env step.
-extern "C" __global__ void __launch_bounds__(WG) mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert) {
-  EnvSh& E = g_E;
-  __shared__ float act[12];
-  const int i = blockIdx.x;
-  if (i >= S.N) return;
-  load_env(S, i, E);
-  if (LANE == 0) {
-    if (expert) expert_plan(S, i, obj_pos(E, EPI(EPI_OBJ)), hand_pos(E), MMX_NSUBSTEP, act);
-    else
-      for (int k = 0; k < adim && k < 12; k++) act[k] = action[(size_t)i * adim + k];
-    decode_lane0(S, i, E, act);
-  }
-  SYNC();
-  for (int sub = 0; sub < MMX_NSUBSTEP; sub++) substep(S.solver_max_iter, S.solver_tol, 1);
+// One env per 64-lane workgroup.  mmx_env_step_kernel (below) is the product path: a whole gym
+// step per launch.  mmx_substep_kernel runs ONE substep per launch (the physics-level parity
+// harness, mmx_physics_step, and a gym step split over 16 launches when mode has SS_GYM): the
+// first launch decodes the action (or runs the FSM expert's plan(16)), the last runs the
+// mj_forward position stage, reward, observation and autoreset (gym_env.py:536-581).
+enum { SS_FIRST = 1, SS_LAST = 2, SS_EXPERT = 4, SS_IK = 8, SS_GYM = 16 };
+
+DEV void fold_flags(const MMXState& S, int i, const EnvSh& E) {  // lane 0
+  if (E.flags & SHF_CON_OVF) EPI(EPI_ERROR) |= ERR_CON_OVERFLOW;
+  if (E.flags & SHF_EFC_OVF) EPI(EPI_ERROR) |= ERR_EFC_OVERFLOW;
+  if (E.flags & SHF_NAN) EPI(EPI_ERROR) |= ERR_NAN;
+}
+
+// end of PickPlaceGymEnv.step: position stage, staged-penalty contact scan, reward, obs, autoreset
+DEV void step_end(const MMXState& S, int i, EnvSh& E, bool expert) {
   float* stats = E.stats;
   CLK_DECL;
   store_contacts(S, i, E);
@@ -1752,9 +1738,7 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_env_step_kernel(MMXState S,
     S.done[3 * (size_t)i + 1] = truncated;
     S.done[3 * (size_t)i + 2] = succ_flag;
     EPF(EPF_EP_RETURN) += r;
-    if (E.flags & SHF_CON_OVF) EPI(EPI_ERROR) |= ERR_CON_OVERFLOW;
-    if (E.flags & SHF_EFC_OVF) EPI(EPI_ERROR) |= ERR_EFC_OVERFLOW;
-    if (E.flags & SHF_NAN) EPI(EPI_ERROR) |= ERR_NAN;
+    fold_flags(S, i, E);
     obs_lane0(S, i, E);
     const bool fsm_done = EPI(EPI_FSM_STATE) == 10;
     const bool err = (EPI(EPI_ERROR) & ERR_NAN) != 0;
@@ -1764,24 +1748,76 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_env_step_kernel(MMXState S,
     }
     CLK(stats, STAT_T_END);
   }
-  store_env(S, i, E);
   store_obs(S, i, E);
 }
 
-// n raw mj_step substeps (optionally each preceded by the IK toward the stored target)
-extern "C" __global__ void __launch_bounds__(WG) mmx_physics_kernel(MMXState S, int n, int with_ik) {
+extern "C" __global__ void __launch_bounds__(WG) mmx_substep_kernel(MMXState S, const float* action, int adim, int mode) {
   EnvSh& E = g_E;
+  __shared__ float act[12];
   const int i = blockIdx.x;
   if (i >= S.N) return;
   load_env(S, i, E);
-  SYNC();
-  for (int sub = 0; sub < n; sub++) substep(S.solver_max_iter, S.solver_tol, with_ik);
-  store_contacts(S, i, E);
-  if (LANE == 0) {
-    EPI(EPI_NCON) = E.ncon;
-    EPI(EPI_NEFC) = E.nefc;
-    if (E.flags & SHF_NAN) EPI(EPI_ERROR) |= ERR_NAN;
+  if ((mode & SS_FIRST) && (mode & SS_GYM) && LANE == 0) {
+    if (mode & SS_EXPERT) expert_plan(S, i, obj_pos(E, EPI(EPI_OBJ)), hand_pos(E), MMX_NSUBSTEP, act);
+    else
+      for (int k = 0; k < adim && k < 12; k++) act[k] = action[(size_t)i * adim + k];
+    decode_lane0(S, i, E, act);
   }
+  SYNC();
+  {
+    float* stats = E.stats;
+    CLK_DECL;
+    if ((mode & SS_IK) && LANE == 0) ik_lane0(E);  // IK on the kinematics of the previous position stage
+    SYNC();
+    CLK(stats, STAT_T_IK);
+  }
+  mj_step_wave(S.solver_max_iter, S.solver_tol, E);
+  if ((mode & SS_LAST) && (mode & SS_GYM)) {
+    step_end(S, i, E, (mode & SS_EXPERT) != 0);
+  } else {
+    if (mode & SS_LAST) store_contacts(S, i, E);
+    if (LANE == 0) {
+      fold_flags(S, i, E);
+      if (mode & SS_LAST) {
+        EPI(EPI_NCON) = E.ncon;
+        EPI(EPI_NEFC) = E.nefc;
+      }
+    }
+  }
+  store_env(S, i, E);
+}
+
+// One substep = IK + mj_step, kept out of line: nothing is hoisted across the 16 iterations of
+// the env-step loop (hoisted invariants would pin registers for the whole kernel and serialise
+// the phases' LDS loads); the price is the callee-saved register spill / fill per call.
+__device__ __attribute__((noinline)) void substep(int max_iter, float tol) {
+  EnvSh& E = g_E;
+  float* stats = E.stats;
+  CLK_DECL;
+  if (LANE == 0) ik_lane0(E);  // IK on the kinematics left by the previous position stage
+  SYNC();
+  CLK(stats, STAT_T_IK);
+  mj_step_wave(max_iter, tol, E);
+}
+
+// The whole PickPlaceGymEnv.step in ONE launch per env step (product path): the 16 substeps
+// loop inside the workgroup, so per-env cost variation averages out over the step instead of
+// stretching 16 separate launch tails (measured: one launch per substep ran 40 % slower).
+extern "C" __global__ void __launch_bounds__(WG) mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert) {
+  EnvSh& E = g_E;
+  __shared__ float act[12];
+  const int i = blockIdx.x;
+  if (i >= S.N) return;
+  load_env(S, i, E);
+  if (LANE == 0) {
+    if (expert) expert_plan(S, i, obj_pos(E, EPI(EPI_OBJ)), hand_pos(E), MMX_NSUBSTEP, act);
+    else
+      for (int k = 0; k < adim && k < 12; k++) act[k] = action[(size_t)i * adim + k];
+    decode_lane0(S, i, E, act);
+  }
+  SYNC();
+  for (int sub = 0; sub < MMX_NSUBSTEP; sub++) substep(S.solver_max_iter, S.solver_tol);
+  step_end(S, i, E, expert != 0);
   store_env(S, i, E);
 }
 
@@ -1843,7 +1879,10 @@ extern "C" hipError_t mmx_launch_expert(const MMXState* S, int n, float* action,
   return hipGetLastError();
 }
 extern "C" hipError_t mmx_launch_physics(const MMXState* S, int n, int with_ik, hipStream_t st) {
-  hipLaunchKernelGGL(mmx_physics_kernel, dim3(S->N), dim3(WG), 0, st, *S, n, with_ik);
+  for (int sub = 0; sub < n; sub++) {
+    const int mode = (with_ik ? SS_IK : 0) | (sub == n - 1 ? SS_LAST : 0);
+    hipLaunchKernelGGL(mmx_substep_kernel, dim3(S->N), dim3(WG), 0, st, *S, nullptr, 0, mode);
+  }
   return hipGetLastError();
 }
 extern "C" hipError_t mmx_launch_forward(const MMXState* S, hipStream_t st) {
