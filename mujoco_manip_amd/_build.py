@@ -18,6 +18,8 @@ SOURCES = ["mmx_kernels.hip", "mmx_api.cpp"]
 HEADERS = ["mmx_model_gen.h", "mmx_state.h", "mmx_device.h", "mmx_geom.h",
            os.path.join("..", "..", "include", "mmx_api.h")]
 ARCH = os.environ.get("MMX_OFFLOAD_ARCH", "gfx950")
+# extra device-compiler flags (experiments only; the committed build uses none)
+FLAGS = os.environ.get("MMX_EXTRA_FLAGS", "").split()
 
 
 def lib_path(profile: bool = False) -> str:
@@ -36,6 +38,7 @@ def _compile(src: str, profile: bool, verbose: bool) -> str:
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     obj = os.path.join(CSRC, os.path.splitext(src)[0] + ("_prof" if profile else "") + ".o")
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", os.path.join(CSRC, src), "-o", obj]
+    cmd[1:1] = FLAGS
     if profile:
         cmd.insert(1, "-DMMX_PHASE_CLOCK=1")
         cmd.insert(1, f"-DMMX_PROBE={int(os.environ.get('MMX_PROBE', '1'))}")

@@ -1790,7 +1790,11 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_substep_kernel(MMXState S, 
 // One substep = IK + mj_step, kept out of line: nothing is hoisted across the 16 iterations of
 // the env-step loop (hoisted invariants would pin registers for the whole kernel and serialise
 // the phases' LDS loads); the price is the callee-saved register spill / fill per call.
+#ifdef MMX_INLINE_SUBSTEP
+DEV void substep(int max_iter, float tol) {
+#else
 __device__ __attribute__((noinline)) void substep(int max_iter, float tol) {
+#endif
   EnvSh& E = g_E;
   float* stats = E.stats;
   CLK_DECL;
