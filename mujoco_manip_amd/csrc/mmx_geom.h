@@ -119,8 +119,12 @@ DEV int clip_poly(const V3* in, int n, V3* out, V3 a, float b) {
 
 // box-box: 15-axis SAT; face contacts clip the incident face against the reference face
 // (<= 8 points), edge-edge contacts give one point at the midpoint of the closest points.
+DEV V3 sel3(V3 a0, V3 a1, V3 a2, int k) { return k == 0 ? a0 : (k == 1 ? a1 : a2); }
+DEV float self3(float a0, float a1, float a2, int k) { return k == 0 ? a0 : (k == 1 ? a1 : a2); }
+
+// poly, tmp: 8 V3 each of per-lane LDS scratch (a quad clipped by 4 half-planes has <= 8 corners)
 template <class Sink>
-DEV void box_box(Sink& cs, const Geom& G1, const Geom& G2) {
+DEV void box_box(Sink& cs, const Geom& G1, const Geom& G2, V3* poly, V3* tmp) {
   const float* h1 = &MMX_geom_size[3 * G1.g];
   const float* h2 = &MMX_geom_size[3 * G2.g];
   const V3 A[3] = {col(G1.R, 0), col(G1.R, 1), col(G1.R, 2)};
@@ -168,7 +172,7 @@ DEV void box_box(Sink& cs, const Geom& G1, const Geom& G2) {
       if (k != ei) ca = ca + A[k] * (dot(A[k], L) >= 0.f ? h1[k] : -h1[k]);
       if (k != ej) cb = cb + B[k] * (dot(B[k], L) >= 0.f ? -h2[k] : h2[k]);
     }
-    const V3 ua = A[ei], ub = B[ej], w = ca - cb;
+    const V3 ua = sel3(A[0], A[1], A[2], ei), ub = sel3(B[0], B[1], B[2], ej), w = ca - cb;
     const float bb = dot(ua, ub), dd = dot(ua, w), ee = dot(ub, w);
     const float den = 1.f - bb * bb;
     float ta = den > 1e-9f ? (bb * ee - dd) / den : 0.f;
@@ -178,42 +182,44 @@ DEV void box_box(Sink& cs, const Geom& G1, const Geom& G2) {
     cs.add(G1.g, G2.g, -best_edge, ((ca + ua * ta) + (cb + ub * tb)) * 0.5f, L);
     return;
   }
+  // face contact: every per-axis pick is a select over the three axes (no dynamically indexed
+  // private arrays -> no scratch); the polygons live in the caller's per-lane LDS buffers
   const bool ref1 = face_axis < 3;
   const int k = ref1 ? face_axis : face_axis - 3;
-  const V3* Rr = ref1 ? A : B;
-  const V3* Ri = ref1 ? B : A;
-  const float* hr = ref1 ? h1 : h2;
-  const float* hi = ref1 ? h2 : h1;
+  const V3 Rr0 = ref1 ? A[0] : B[0], Rr1 = ref1 ? A[1] : B[1], Rr2 = ref1 ? A[2] : B[2];
+  const V3 Ri0 = ref1 ? B[0] : A[0], Ri1 = ref1 ? B[1] : A[1], Ri2 = ref1 ? B[2] : A[2];
+  const float hr0 = ref1 ? h1[0] : h2[0], hr1 = ref1 ? h1[1] : h2[1], hr2 = ref1 ? h1[2] : h2[2];
+  const float hi0 = ref1 ? h2[0] : h1[0], hi1 = ref1 ? h2[1] : h1[1], hi2 = ref1 ? h2[2] : h1[2];
   const V3 pr = ref1 ? G1.x : G2.x, pi = ref1 ? G2.x : G1.x;
-  V3 nref = Rr[k];
+  V3 nref = sel3(Rr0, Rr1, Rr2, k);
   if (dot(nref, pi - pr) < 0.f) nref = -nref;
   int bj = 0;
   float bdot = 0.f;
-#pragma unroll
-  for (int j = 0; j < 3; j++) {
-    const float t = fabsf(dot(Ri[j], nref));
-    if (t > bdot) {
-      bdot = t;
-      bj = j;
-    }
+  {
+    const float t0 = fabsf(dot(Ri0, nref)), t1 = fabsf(dot(Ri1, nref)), t2 = fabsf(dot(Ri2, nref));
+    if (t0 > bdot) { bdot = t0; bj = 0; }
+    if (t1 > bdot) { bdot = t1; bj = 1; }
+    if (t2 > bdot) { bdot = t2; bj = 2; }
   }
-  V3 ni = Ri[bj];
+  V3 ni = sel3(Ri0, Ri1, Ri2, bj);
   if (dot(ni, nref) > 0.f) ni = -ni;
-  const V3 ci = pi + ni * hi[bj];
-  const int u = (bj + 1) % 3, v = (bj + 2) % 3;
-  V3 poly[16], tmp[16];
+  const V3 ci = pi + ni * self3(hi0, hi1, hi2, bj);
+  const int u = bj == 2 ? 0 : bj + 1, v = bj == 0 ? 2 : bj - 1;
+  const V3 Ru = sel3(Ri0, Ri1, Ri2, u) * self3(hi0, hi1, hi2, u);
+  const V3 Rv = sel3(Ri0, Ri1, Ri2, v) * self3(hi0, hi1, hi2, v);
   int np = 4;
-  poly[0] = ci + Ri[u] * hi[u] + Ri[v] * hi[v];
-  poly[1] = ci - Ri[u] * hi[u] + Ri[v] * hi[v];
-  poly[2] = ci - Ri[u] * hi[u] - Ri[v] * hi[v];
-  poly[3] = ci + Ri[u] * hi[u] - Ri[v] * hi[v];
-  const V3 cr = pr + nref * hr[k];
-  const int ru = (k + 1) % 3, rv = (k + 2) % 3;
-  const V3 ax0 = Rr[ru], ax1 = Rr[rv];
-  np = clip_poly(poly, np, tmp, ax0, dot(ax0, cr) + hr[ru]);
-  np = clip_poly(tmp, np, poly, -ax0, dot(-ax0, cr) + hr[ru]);
-  np = clip_poly(poly, np, tmp, ax1, dot(ax1, cr) + hr[rv]);
-  np = clip_poly(tmp, np, poly, -ax1, dot(-ax1, cr) + hr[rv]);
+  poly[0] = ci + Ru + Rv;
+  poly[1] = ci - Ru + Rv;
+  poly[2] = ci - Ru - Rv;
+  poly[3] = ci + Ru - Rv;
+  const V3 cr = pr + nref * self3(hr0, hr1, hr2, k);
+  const int ru = k == 2 ? 0 : k + 1, rv = k == 0 ? 2 : k - 1;
+  const V3 ax0 = sel3(Rr0, Rr1, Rr2, ru), ax1 = sel3(Rr0, Rr1, Rr2, rv);
+  const float hru = self3(hr0, hr1, hr2, ru), hrv = self3(hr0, hr1, hr2, rv);
+  np = clip_poly(poly, np, tmp, ax0, dot(ax0, cr) + hru);
+  np = clip_poly(tmp, np, poly, -ax0, dot(-ax0, cr) + hru);
+  np = clip_poly(poly, np, tmp, ax1, dot(ax1, cr) + hrv);
+  np = clip_poly(tmp, np, poly, -ax1, dot(-ax1, cr) + hrv);
   const V3 nout = ref1 ? nref : -nref;
   for (int c = 0; c < np; c++) {
     const float depth = -dot(poly[c] - cr, nref);

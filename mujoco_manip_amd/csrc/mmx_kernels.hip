@@ -457,13 +457,14 @@ struct WaveSink {
 
 // LDS scratch layout of the collision phase (inside E.J, which is rebuilt after collision)
 #define COL_GX 0      // [NGEOM][16] world pose (x3, R9), rbound, type
-#define COL_CAND 768  // [COL_LIST] candidate pairs after the sphere test
+#define COL_CAND 768  // [COL_LIST] candidate pairs (pair | class << 12) after the sphere test
 #define COL_LIST 784
-#define COL_CLS (COL_CAND + COL_LIST)  // 3 x [COL_LIST] pairs per narrowphase class
-#define COL_SORT (COL_CLS + 3 * COL_LIST)
-static_assert(COL_SORT + MMX_MAXCON * CON_F <= MMX_MAXEFC * 16, "collision scratch exceeds E.J");
-static_assert(MMX_NGEOM * 16 <= COL_CAND && MMX_NPAIR <= COL_LIST, "collision scratch layout");
-static_assert(EPA_SCRATCH_FLOATS <= 3 * COL_LIST, "EPA scratch exceeds the consumed lists");
+#define COL_WORK (COL_CAND + COL_LIST)  // narrowphase work space: box-box polygons, EPA polytope,
+#define COL_POLY 48                     // then the contact sort (each used after the previous)
+static_assert(COL_WORK + WG * COL_POLY <= MMX_MAXEFC * 16, "box-box polygons exceed E.J");
+static_assert(COL_WORK + EPA_SCRATCH_FLOATS <= MMX_MAXEFC * 16, "EPA scratch exceeds E.J");
+static_assert(COL_WORK + MMX_MAXCON * CON_F <= MMX_MAXEFC * 16, "contact sort exceeds E.J");
+static_assert(MMX_NGEOM * 16 <= COL_CAND && MMX_NPAIR <= COL_LIST && MMX_NPAIR < 4096, "collision scratch layout");
 
 DEV Geom geom_lds(const float* gx, int g) {
   const float* o = gx + 16 * g;
@@ -476,14 +477,11 @@ DEV Geom geom_lds(const float* gx, int g) {
   return G;
 }
 // geoms of pair p ordered by type (plane first), as the narrowphase dispatch expects
+// (MMX_pair_packed is MMX_bodypair_geoms pre-sorted by the model compiler)
 DEV void pair_geoms(const float* gx, int p, int& g1, int& g2) {
-  g1 = MMX_bodypair_geoms[2 * p];
-  g2 = MMX_bodypair_geoms[2 * p + 1];
-  if (__float_as_int(gx[16 * g1 + 13]) > __float_as_int(gx[16 * g2 + 13])) {
-    const int t = g1;
-    g1 = g2;
-    g2 = t;
-  }
+  const int pk = MMX_pair_packed[p];
+  g1 = pk & 255;
+  g2 = pk >> 8;
 }
 DEV bool robot_obstacle(int g1, int g2) {
   const int c1 = MMX_geom_class[g1], c2 = MMX_geom_class[g2];
@@ -512,7 +510,6 @@ DEV void collide_wave(EnvSh& E, bool only_ro) {
   float* scr = &E.J[0][0];
   float* gx = scr + COL_GX;
   int* cand = reinterpret_cast<int*>(scr + COL_CAND);
-  int* cls = reinterpret_cast<int*>(scr + COL_CLS);
   if (LANE < MMX_NGEOM) {
     const Geom G = geom_pose(E, LANE);
     float* o = gx + 16 * LANE;
@@ -523,13 +520,22 @@ DEV void collide_wave(EnvSh& E, bool only_ro) {
     o[13] = __int_as_float(G.type);
   }
   SYNC();
+  PROBE(2, stats, STAT_T_AUX0);
+  // (2) sphere / plane-distance prune of all pairs: unrolled so the pair-table loads issue together
+  constexpr int NPASS = (MMX_NPAIR + WG - 1) / WG;
+  int pg[NPASS];  // all pair-table loads in flight at once
+#pragma unroll
+  for (int q = 0; q < NPASS; q++) {
+    const int p = min(q * WG + LANE, MMX_NPAIR - 1);
+    pg[q] = MMX_pair_packed[p];
+  }
   int nc = 0;
-  for (int base = 0; base < MMX_NPAIR; base += WG) {
-    const int p = base + LANE;
+#pragma unroll
+  for (int q = 0; q < NPASS; q++) {
+    const int p = q * WG + LANE;
     bool keep = false;
     if (p < MMX_NPAIR) {
-      int g1, g2;
-      pair_geoms(gx, p, g1, g2);
+      const int g1 = pg[q] & 255, g2 = pg[q] >> 8;
       if (!only_ro || robot_obstacle(g1, g2)) {
         const float* o1 = gx + 16 * g1;
         const float* o2 = gx + 16 * g2;
@@ -545,63 +551,74 @@ DEV void collide_wave(EnvSh& E, bool only_ro) {
     nc = wave_compact(keep, cand, nc, p);
   }
   SYNC();
-  PROBE(2, stats, STAT_T_AUX0);
+  PROBE(2, stats, STAT_T_AUX1);
+  // (3) OBB prune; the class (0 plane, 1 box-box, 2 GJK, 3 pruned) is stored with the pair
   int ncls[3] = {0, 0, 0};
   for (int base = 0; base < nc; base += WG) {
     const int k = base + LANE;
-    int c = -1, p = 0;
+    int c = 3;
     if (k < nc) {
-      p = cand[k];
+      const int p = cand[k];
       int g1, g2;
       pair_geoms(gx, p, g1, g2);
       const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
       if (A.type == GT_PLANE) c = 0;
       else if (obb_overlap(A, B)) c = (A.type == GT_BOX && B.type == GT_BOX) ? 1 : 2;
+      cand[k] = p | (c << 12);
     }
 #pragma unroll
-    for (int q = 0; q < 3; q++) ncls[q] = wave_compact(c == q, cls + q * COL_LIST, ncls[q], p);
+    for (int q = 0; q < 3; q++) ncls[q] += __popcll(__ballot(c == q));
   }
   SYNC();
-  PROBE(2, stats, STAT_T_AUX0);
   if (MMX_PROBE == 4 && LANE == 0) {
     stats[STAT_T_AUX0] += (float)nc;
     stats[STAT_T_AUX1] += (float)ncls[1];
     stats[STAT_T_AUX2] += (float)ncls[2];
     stats[STAT_T_AUX3] += (float)ncls[0];
   }
+  PROBE(2, stats, STAT_T_AUX2);
+  // (4) narrowphase, one pass per class over the candidate list: lanes of a class run together
+  V3* poly = reinterpret_cast<V3*>(scr + COL_WORK + COL_POLY * LANE);
 #pragma unroll
   for (int q = 0; q < 2; q++) {  // lane per pair
-    for (int k = LANE; k < ncls[q]; k += WG) {
-      const int p = cls[q * COL_LIST + k];
+    if (ncls[q] == 0) continue;
+    for (int base = 0; base < nc; base += WG) {
+      const int k = base + LANE;
+      const int e = k < nc ? cand[k] : (3 << 12);
+      if ((e >> 12) == q) {
+        const int p = e & 4095;
+        int g1, g2;
+        pair_geoms(gx, p, g1, g2);
+        const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
+        WaveSink cs{&E, p * 8, !only_ro};
+        if (q == 0) {
+          if (B.type == GT_BOX) plane_box(cs, A, B);
+          else if (B.type == GT_MESH) plane_convex(cs, A, B);
+        } else {
+          box_box(cs, A, B, poly, poly + 8);
+        }
+      }
+    }
+    SYNC();
+  }
+  // GJK / EPA pairs: the whole wave on one pair at a time (EPA polytope in the work space)
+  if (ncls[2] > 0) {
+    for (int k = 0; k < nc; k++) {
+      const int e = cand[k];
+      if ((e >> 12) != 2) continue;
+      const int p = e & 4095;
       int g1, g2;
       pair_geoms(gx, p, g1, g2);
       const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
       WaveSink cs{&E, p * 8, !only_ro};
-      if (q == 0) {
-        if (B.type == GT_BOX) plane_box(cs, A, B);
-        else if (B.type == GT_MESH) plane_convex(cs, A, B);
-      } else {
-        box_box(cs, A, B);
-      }
+      convex_convex(cs, A, B, scr + COL_WORK);
     }
-    SYNC();
-    PROBE(2, stats, STAT_T_AUX1 + q);
-  }
-  // GJK / EPA pairs: the whole wave on one pair at a time (EPA polytope in the consumed
-  // candidate / class-0 / class-1 lists)
-  for (int k = 0; k < ncls[2]; k++) {
-    const int p = cls[2 * COL_LIST + k];
-    int g1, g2;
-    pair_geoms(gx, p, g1, g2);
-    const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
-    WaveSink cs{&E, p * 8, !only_ro};
-    convex_convex(cs, A, B, scr + COL_CAND);
   }
   SYNC();
   PROBE(2, stats, STAT_T_AUX3);
   if (only_ro) return;
   const int n = min(E.ncon, MMX_MAXCON);
-  float* tmp = scr + COL_SORT;
+  float* tmp = scr + COL_WORK;
   if (LANE < n) {
     const int key = E.conkey[LANE];
     int rank = 0;

@@ -650,7 +650,17 @@ def device_tables(model, P, R):
     L.append(f"#define {P}NBODYPAIR {len(bp)}\n")
     L.append(c_array(f"{P}bodypair", "int", bp))
     L.append(c_array(f"{P}bodypair_geoms", "int", pl))
+    # the same pairs packed g1 | g2 << 8 with the lower geom type first (narrowphase dispatch order)
+    L.append(c_array(f"{P}pair_packed", "int", [pack_pair(a, b, model) for a, b in pl]))
     return L
+
+
+def pack_pair(a, b, model):
+    col, geoms = model["col_geoms"], model["geoms"]
+    ta, tb = GEOM_TYPE[geoms[col[a]]["type"]], GEOM_TYPE[geoms[col[b]]["type"]]
+    if ta > tb:
+        a, b = b, a
+    return a | (b << 8)
 
 
 def emit_header(model, path, real, prefix, guard):
