@@ -106,7 +106,7 @@ DEV void plane_convex(Sink& cs, const Geom& P, const Geom& C) {
 DEV int clip_poly(const V3* in, int n, V3* out, V3 a, float b) {
   int m = 0;
   for (int k = 0; k < n; k++) {
-    const V3 p = in[k], q = in[(k + 1) % n];
+    const V3 p = in[k], q = in[k + 1 == n ? 0 : k + 1];
     const float dp = dot(p, a) - b, dq = dot(q, a) - b;
     if (dp <= 0.f) out[m++] = p;
     if ((dp < 0.f && dq > 0.f) || (dp > 0.f && dq < 0.f)) {

@@ -217,6 +217,87 @@ DEV void kinematics_lane0(EnvSh& E) {
   for (int k = 0; k < 9; k++) E.kin[KIN_HAND_MAT + k] = E.bR[hs][k];
 }
 
+// Wave form of kinematics_lane0: one lane per body.  Each arm body first builds its local
+// transform (static offset x joint), then the chain is composed by pointer jumping (4 rounds
+// cover the 10-deep finger chain): T_b <- T_anc(b) o T_b, anc(b) <- anc(anc(b)).  Cubes read their
+// free joints directly.  Results equal kinematics_lane0 up to fp32 association order.
+DEV void kinematics_wave(EnvSh& E) {
+  float* T = &E.Lrow[0][0];  // [12][8] scan scratch: q (4), p (3), ancestor (Lrow is free here)
+  const int b = LANE + 1;    // lanes 0..10 -> arm bodies 1..11
+  Q4 q = Q4{1.f, 0.f, 0.f, 0.f};
+  V3 p = V3{0.f, 0.f, 0.f};
+  int anc = 0;
+  if (LANE < 11) {
+    p = V3{MMX_body_pos[3 * b], MMX_body_pos[3 * b + 1], MMX_body_pos[3 * b + 2]};
+    q = Q4{MMX_body_quat[4 * b], MMX_body_quat[4 * b + 1], MMX_body_quat[4 * b + 2], MMX_body_quat[4 * b + 3]};
+    const int j = MMX_body_jnt[b];
+    if (j >= 0) {
+      const V3 axl = V3{MMX_jnt_axis[3 * j], MMX_jnt_axis[3 * j + 1], MMX_jnt_axis[3 * j + 2]};
+      const float qv = E.qpos[j];
+      if (MMX_jnt_type[j] == 3) q = qmul(q, qaxisangle(axl, qv));  // hinge
+      else p = p + mul(qmat(qnormalize(q)), axl) * qv;             // slide along the joint axis
+    }
+    anc = MMX_body_parent[b];
+  }
+#pragma unroll
+  for (int round = 0; round < 4; round++) {
+    if (LANE < 11) {
+      float* t = T + 8 * b;
+      t[0] = q.w; t[1] = q.x; t[2] = q.y; t[3] = q.z;
+      t[4] = p.x; t[5] = p.y; t[6] = p.z;
+      t[7] = __int_as_float(anc);
+    }
+    SYNC();
+    if (LANE < 11 && anc != 0) {
+      const float* t = T + 8 * anc;
+      const Q4 qa = Q4{t[0], t[1], t[2], t[3]};
+      const V3 pa = V3{t[4], t[5], t[6]};
+      const int aa = __float_as_int(t[7]);
+      p = pa + mul(qmat(qa), p);
+      q = qnormalize(qmul(qa, q));
+      anc = aa;
+    }
+    SYNC();
+  }
+  if (LANE < 11) {
+    q = qnormalize(q);
+    const M3 R = qmat(q);
+    const int s = b - 1;
+    E.bx[s][0] = p.x; E.bx[s][1] = p.y; E.bx[s][2] = p.z;
+#pragma unroll
+    for (int k = 0; k < 9; k++) E.bR[s][k] = R.m[k];
+    const int j = MMX_body_jnt[b];
+    if (j >= 0) {
+      const V3 axw = mul(R, V3{MMX_jnt_axis[3 * j], MMX_jnt_axis[3 * j + 1], MMX_jnt_axis[3 * j + 2]});
+      if (MMX_jnt_type[j] == 3) {
+        const V3 lin = cross(p, axw);
+        E.S[j][0] = axw.x; E.S[j][1] = axw.y; E.S[j][2] = axw.z;
+        E.S[j][3] = lin.x; E.S[j][4] = lin.y; E.S[j][5] = lin.z;
+        if (j < 7) {
+          E.kin[KIN_AXIS + 3 * j] = axw.x; E.kin[KIN_AXIS + 3 * j + 1] = axw.y; E.kin[KIN_AXIS + 3 * j + 2] = axw.z;
+          E.kin[KIN_ANCHOR + 3 * j] = p.x; E.kin[KIN_ANCHOR + 3 * j + 1] = p.y; E.kin[KIN_ANCHOR + 3 * j + 2] = p.z;
+        }
+      } else {
+        E.S[j][0] = 0.f; E.S[j][1] = 0.f; E.S[j][2] = 0.f;
+        E.S[j][3] = axw.x; E.S[j][4] = axw.y; E.S[j][5] = axw.z;
+      }
+    }
+    if (b == MMX_BODY_HAND) {
+      E.kin[KIN_HAND_POS] = p.x; E.kin[KIN_HAND_POS + 1] = p.y; E.kin[KIN_HAND_POS + 2] = p.z;
+#pragma unroll
+      for (int k = 0; k < 9; k++) E.kin[KIN_HAND_MAT + k] = R.m[k];
+    }
+  } else if (LANE < 14) {  // cubes: free joints
+    const int c = LANE - 11, qa = 9 + 7 * c;
+    const M3 R = qmat(qnormalize(Q4{E.qpos[qa + 3], E.qpos[qa + 4], E.qpos[qa + 5], E.qpos[qa + 6]}));
+    const int s = 11 + c;
+    E.bx[s][0] = E.qpos[qa]; E.bx[s][1] = E.qpos[qa + 1]; E.bx[s][2] = E.qpos[qa + 2];
+#pragma unroll
+    for (int k = 0; k < 9; k++) E.bR[s][k] = R.m[k];
+  }
+  SYNC();
+}
+
 // ============================================================================ dynamics
 DEV RI body_inertia(const EnvSh& E, int b) {
   const V3 x = body_x(E, b);
@@ -294,6 +375,58 @@ DEV void rne_lane0(EnvSh& E) {
   for (int b = 2; b <= 11; b++) ri_store(E.Ic[b], Ib[b]);
 }
 
+// Wave form of rne_lane0: one lane per moving arm body (2..11).  A body's velocity and
+// acceleration are running sums over the joints on its root path (arm_anc), its force is local;
+// subtree sums of force and inertia (the backward pass and the composite inertia) are gathers
+// over descendants.  Scratch in E.Lrow: per body frc (6) + inertia (10), then subtree force (6).
+DEV void rne_wave(EnvSh& E) {
+  float* F = &E.Lrow[0][0];
+  const int b = LANE + 2;
+  if (LANE < 10) {
+    const RI Ib = body_inertia(E, b);
+    SV vel = SV{V3{0.f, 0.f, 0.f}, V3{0.f, 0.f, 0.f}};
+    SV acc = SV{V3{0.f, 0.f, 0.f}, V3{0.f, 0.f, -MMX_GRAVITY_Z}};  // base acceleration = -gravity
+#pragma unroll
+    for (int d = 0; d < 9; d++) {
+      if (arm_anc(d, b)) {
+        const SV vj = load_S(E, d) * E.qvel[d];
+        acc = acc + cross_motion(vel, vj);
+        vel = vel + vj;
+      }
+    }
+    const SV f = rimul(Ib, acc) + cross_force(vel, rimul(Ib, vel));
+    float* o = F + 16 * b;
+    o[0] = f.w.x; o[1] = f.w.y; o[2] = f.w.z; o[3] = f.v.x; o[4] = f.v.y; o[5] = f.v.z;
+    ri_store(o + 6, Ib);
+  }
+  SYNC();
+  if (LANE < 10) {  // subtree sums: b is an ancestor-or-self of k
+    float fs[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, is[10];
+#pragma unroll
+    for (int m = 0; m < 10; m++) is[m] = 0.f;
+#pragma unroll
+    for (int k = 11; k >= 2; k--) {
+      const bool in = b <= 9 ? k >= b : k == b;
+      const float* o = F + 16 * k;
+#pragma unroll
+      for (int m = 0; m < 6; m++) fs[m] += in ? o[m] : 0.f;
+#pragma unroll
+      for (int m = 0; m < 10; m++) is[m] += in ? o[6 + m] : 0.f;
+    }
+#pragma unroll
+    for (int m = 0; m < 10; m++) E.Ic[b][m] = is[m];
+    float* o = F + 16 * 12 + 6 * b;
+#pragma unroll
+    for (int m = 0; m < 6; m++) o[m] = fs[m];
+  }
+  SYNC();
+  if (LANE < 9) {
+    const float* o = F + 16 * 12 + 6 * MMX_jnt_body[LANE];
+    E.bias[LANE] = sdot(load_S(E, LANE), SV{V3{o[0], o[1], o[2]}, V3{o[3], o[4], o[5]}});
+  }
+  SYNC();
+}
+
 DEV void chol9(float* L) {
 #pragma unroll
   for (int j = 0; j < 9; j++) {
@@ -330,7 +463,7 @@ DEV void chol9_solve(const float* L, float* x) {
 
 // whole wave: mass matrix (CRBA entries in parallel), smooth forces, qacc_smooth
 DEV void dynamics_wave(EnvSh& E) {
-  if (LANE == 0) rne_lane0(E);
+  rne_wave(E);
   for (int idx = LANE; idx < 27 * LD; idx += WG) (&E.M[0][0])[idx] = 0.f;
   SYNC();
   if (LANE < 45) {
@@ -431,9 +564,19 @@ struct WaveSink {
   EnvSh* E;
   int key;
   bool store;
-  DEV void add(int g1, int g2, float dist, V3 pos, V3 nrm) {
+  // pair constants, loaded once per pair (MuJoCo mixing: friction max, condim max)
+  bool ro;
+  float mu0, mu1, mu2, dim;
+  DEV WaveSink(EnvSh* e, int p, bool st, int g1, int g2) : E(e), key(p * 8), store(st) {
     const int c1 = MMX_geom_class[g1], c2 = MMX_geom_class[g2];
-    if ((c1 == 1 && c2 == 2) || (c1 == 2 && c2 == 1)) atomicOr(&E->flags, (int)SHF_ROBOT_OBST);
+    ro = (c1 == 1 && c2 == 2) || (c1 == 2 && c2 == 1);
+    mu0 = fmaxf(MMX_geom_friction[3 * g1], MMX_geom_friction[3 * g2]);
+    mu1 = fmaxf(MMX_geom_friction[3 * g1 + 1], MMX_geom_friction[3 * g2 + 1]);
+    mu2 = fmaxf(MMX_geom_friction[3 * g1 + 2], MMX_geom_friction[3 * g2 + 2]);
+    dim = (float)max(MMX_geom_condim[g1], MMX_geom_condim[g2]);
+  }
+  DEV void add(int g1, int g2, float dist, V3 pos, V3 nrm) {
+    if (ro) atomicOr(&E->flags, (int)SHF_ROBOT_OBST);
     if (!store) return;
     const int slot = atomicAdd(&E->ncon, 1);
     if (slot >= MMX_MAXCON) {
@@ -445,10 +588,10 @@ struct WaveSink {
     c[CON_DIST] = dist;
     c[CON_POS] = pos.x; c[CON_POS + 1] = pos.y; c[CON_POS + 2] = pos.z;
     c[CON_N] = nrm.x; c[CON_N + 1] = nrm.y; c[CON_N + 2] = nrm.z;
-    c[CON_MU0] = fmaxf(MMX_geom_friction[3 * g1], MMX_geom_friction[3 * g2]);
-    c[CON_MU1] = fmaxf(MMX_geom_friction[3 * g1 + 1], MMX_geom_friction[3 * g2 + 1]);
-    c[CON_MU2] = fmaxf(MMX_geom_friction[3 * g1 + 2], MMX_geom_friction[3 * g2 + 2]);
-    c[CON_DIM] = (float)max(MMX_geom_condim[g1], MMX_geom_condim[g2]);
+    c[CON_MU0] = mu0;
+    c[CON_MU1] = mu1;
+    c[CON_MU2] = mu2;
+    c[CON_DIM] = dim;
     c[CON_G1] = (float)g1;
     c[CON_G2] = (float)g2;
     E->conkey[slot] = key++;
@@ -577,6 +720,7 @@ DEV void collide_wave(EnvSh& E, bool only_ro) {
     stats[STAT_T_AUX3] += (float)ncls[0];
   }
   PROBE(2, stats, STAT_T_AUX2);
+  PROBE(5, stats, STAT_T_AUX3);
   // (4) narrowphase, one pass per class over the candidate list: lanes of a class run together
   V3* poly = reinterpret_cast<V3*>(scr + COL_WORK + COL_POLY * LANE);
 #pragma unroll
@@ -590,7 +734,7 @@ DEV void collide_wave(EnvSh& E, bool only_ro) {
         int g1, g2;
         pair_geoms(gx, p, g1, g2);
         const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
-        WaveSink cs{&E, p * 8, !only_ro};
+        WaveSink cs(&E, p, !only_ro, g1, g2);
         if (q == 0) {
           if (B.type == GT_BOX) plane_box(cs, A, B);
           else if (B.type == GT_MESH) plane_convex(cs, A, B);
@@ -600,6 +744,8 @@ DEV void collide_wave(EnvSh& E, bool only_ro) {
       }
     }
     SYNC();
+    if (q == 0) PROBE(5, stats, STAT_T_AUX0);
+    else PROBE(5, stats, STAT_T_AUX1);
   }
   // GJK / EPA pairs: the whole wave on one pair at a time (EPA polytope in the work space)
   if (ncls[2] > 0) {
@@ -610,12 +756,13 @@ DEV void collide_wave(EnvSh& E, bool only_ro) {
       int g1, g2;
       pair_geoms(gx, p, g1, g2);
       const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
-      WaveSink cs{&E, p * 8, !only_ro};
+      WaveSink cs(&E, p, !only_ro, g1, g2);
       convex_convex(cs, A, B, scr + COL_WORK);
     }
   }
   SYNC();
   PROBE(2, stats, STAT_T_AUX3);
+  PROBE(5, stats, STAT_T_AUX2);
   if (only_ro) return;
   const int n = min(E.ncon, MMX_MAXCON);
   float* tmp = scr + COL_WORK;
@@ -630,6 +777,7 @@ DEV void collide_wave(EnvSh& E, bool only_ro) {
   for (int k = LANE; k < n * CON_F; k += WG) (&E.con[0][0])[k] = tmp[k];
   if (LANE == 0) E.ncon = n;
   SYNC();
+  PROBE(5, stats, STAT_T_AUX3);
 }
 
 // ============================================================================ constraints (wave)
@@ -1291,8 +1439,7 @@ DEV void ik_lane0(EnvSh& E) {
 DEV void mj_step_wave(int max_iter, float tol, EnvSh& E) {
   float* stats = E.stats;
   CLK_DECL;
-  if (LANE == 0) kinematics_lane0(E);
-  SYNC();
+  kinematics_wave(E);
   CLK(stats, STAT_T_KIN);
   dynamics_wave(E);
   CLK(stats, STAT_T_DYN);
@@ -1724,9 +1871,8 @@ DEV void step_end(const MMXState& S, int i, EnvSh& E, bool expert) {
   if (LANE == 0) {
     EPI(EPI_NCON) = E.ncon;
     EPI(EPI_NEFC) = E.nefc;
-    kinematics_lane0(E);
   }
-  SYNC();
+  kinematics_wave(E);
   if (S.reward_type == 2) collide_wave(E, true);
   if (LANE == 0) {
     EPI(EPI_STEP) += 1;
