@@ -44,7 +44,6 @@ struct EnvSh {
   float S[9][6];
   float Ic[12][10];  // composite inertias (m, h, J) of arm bodies
   float M[27][LD];
-  float L[45];       // packed lower Cholesky of the arm block
   float qfrc[LD], qacc_s[LD], x[LD], g[LD], p[LD];
   float bias[9];
   float con[MMX_MAXCON][CON_F];
@@ -427,38 +426,46 @@ DEV void rne_wave(EnvSh& E) {
   SYNC();
 }
 
-DEV void chol9(float* L) {
+
+// (A^{-1} v)_j in lane j for a small SPD A given by rows (lane j holds row j in arow[0..N)).
+// Right-looking Cholesky with v_readlane broadcasts; lane k keeps column k of L (selects) for
+// the transposed solve.  eps: pivot floor.
+template <int N>
+DEV float chol_solve_small(const float* arow, float v, float eps) {
+  const int j = LANE;
+  float h[N], c[N], dinv[N];
 #pragma unroll
-  for (int j = 0; j < 9; j++) {
-    float s = L[LT(j, j)];
+  for (int i = 0; i < N; i++) {
+    h[i] = arow[i];
+    c[i] = 0.f;
+  }
 #pragma unroll
-    for (int k = 0; k < j; k++) s -= L[LT(j, k)] * L[LT(j, k)];
-    const float d = sqrtf(fmaxf(s, 1e-12f)), inv = 1.0f / d;
-    L[LT(j, j)] = d;
+  for (int k = 0; k < N; k++) {
+    const float sd = sqrtf(fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(h[k]), k)), eps));
+    const float inv = 1.f / sd;
+    dinv[k] = inv;
+    const float l = j == k ? sd : h[k] * inv;
+    h[k] = l;
+    c[k] = j == k ? sd : c[k];
 #pragma unroll
-    for (int r = j + 1; r < 9; r++) {
-      float t = L[LT(r, j)];
-#pragma unroll
-      for (int k = 0; k < j; k++) t -= L[LT(r, k)] * L[LT(j, k)];
-      L[LT(r, j)] = t * inv;
+    for (int i = k + 1; i < N; i++) {
+      const float li = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l), i));
+      h[i] = fmaf(-li, l, h[i]);
+      c[i] = j == k ? li : c[i];
     }
   }
-}
-DEV void chol9_solve(const float* L, float* x) {
+  float y = j < N ? v : 0.f;
 #pragma unroll
-  for (int r = 0; r < 9; r++) {
-    float s = x[r];
-#pragma unroll
-    for (int k = 0; k < r; k++) s -= L[LT(r, k)] * x[k];
-    x[r] = s / L[LT(r, r)];
+  for (int k = 0; k < N; k++) {
+    const float yk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(y), k)) * dinv[k];
+    y = j == k ? yk : (j > k ? fmaf(-h[k], yk, y) : y);
   }
 #pragma unroll
-  for (int r = 8; r >= 0; r--) {
-    float s = x[r];
-#pragma unroll
-    for (int k = r + 1; k < 9; k++) s -= L[LT(k, r)] * x[k];
-    x[r] = s / L[LT(r, r)];
+  for (int k = N - 1; k >= 0; k--) {
+    const float zk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(y), k)) * dinv[k];
+    y = j == k ? zk : (j < k ? fmaf(-c[k], zk, y) : y);
   }
+  return y;
 }
 
 // whole wave: mass matrix (CRBA entries in parallel), smooth forces, qacc_smooth
@@ -482,57 +489,50 @@ DEV void dynamics_wave(EnvSh& E) {
     E.M[9 + k][9 + k] = rr < 3 ? MMX_body_mass[b] : MMX_body_inertia[9 * b + 4 * (rr - 3)];
   }
   SYNC();
-  if (LANE == 0) {
-    // smooth force: passive damping - bias + actuation (arm), gravity + gyroscopic (cubes)
-    float qfrc[9];
+  // smooth force: passive damping - bias + actuation (arm; one lane per actuator, then per dof),
+  // gravity + gyroscopic (cubes, one lane each); arm qacc_smooth = M_arm^{-1} qfrc by a register
+  // Cholesky (rows in lanes 0..8)
+  float* af = &E.Lrow[0][0];  // actuator forces (Lrow is free after the RNE)
+  if (LANE < 8) {
+    const int a = LANE;
+    const float c = fminf(fmaxf(E.ctrl[a], MMX_act_ctrlrange[2 * a]), MMX_act_ctrlrange[2 * a + 1]);
+    const int j = MMX_act_trn_joint[a];
     const float tlen = MMX_tendon_coef[0] * E.qpos[7] + MMX_tendon_coef[1] * E.qpos[8];
     const float tvel = MMX_tendon_coef[0] * E.qvel[7] + MMX_tendon_coef[1] * E.qvel[8];
-#pragma unroll
-    for (int d = 0; d < 9; d++) qfrc[d] = -MMX_dof_damping[d] * E.qvel[d] - E.bias[d];
-#pragma unroll
-    for (int a = 0; a < 8; a++) {
-      const float c = fminf(fmaxf(E.ctrl[a], MMX_act_ctrlrange[2 * a]), MMX_act_ctrlrange[2 * a + 1]);
-      const int j = MMX_act_trn_joint[a];
-      const float len = j >= 0 ? E.qpos[j] : tlen, vel = j >= 0 ? E.qvel[j] : tvel;
-      float f = MMX_act_gain[a] * c + MMX_act_bias[3 * a] + MMX_act_bias[3 * a + 1] * len + MMX_act_bias[3 * a + 2] * vel;
-      E.act_unclamped[a] = f > MMX_act_forcerange[2 * a] && f < MMX_act_forcerange[2 * a + 1];
-      f = fminf(fmaxf(f, MMX_act_forcerange[2 * a]), MMX_act_forcerange[2 * a + 1]);
-      if (j >= 0) qfrc[j] += f;
-      else {
-        qfrc[7] += MMX_tendon_coef[0] * f;
-        qfrc[8] += MMX_tendon_coef[1] * f;
-      }
-    }
-    float L[45];
-#pragma unroll
-    for (int d = 0; d < 9; d++)
-#pragma unroll
-      for (int e = 0; e <= d; e++) L[LT(d, e)] = E.M[d][e];
-    chol9(L);
-#pragma unroll
-    for (int k = 0; k < 45; k++) E.L[k] = L[k];
-    float xs[9];
-#pragma unroll
-    for (int d = 0; d < 9; d++) xs[d] = qfrc[d];
-    chol9_solve(L, xs);
-#pragma unroll
-    for (int d = 0; d < 9; d++) {
-      E.qfrc[d] = qfrc[d];
-      E.qacc_s[d] = xs[d];
-    }
-#pragma unroll
-    for (int c = 0; c < 3; c++) {  // free body with com at the origin: gravity + w x (I w)
-      const int b = 16 + c, da = 9 + 6 * c;
-      const float I0 = MMX_body_inertia[9 * b], I1 = MMX_body_inertia[9 * b + 4], I2 = MMX_body_inertia[9 * b + 8];
-      const V3 w = V3{E.qvel[da + 3], E.qvel[da + 4], E.qvel[da + 5]};
-      const V3 gyro = cross(w, V3{I0 * w.x, I1 * w.y, I2 * w.z});
-      const float m = MMX_body_mass[b];
-      E.qfrc[da] = 0.f; E.qfrc[da + 1] = 0.f; E.qfrc[da + 2] = MMX_GRAVITY_Z * m;
-      E.qfrc[da + 3] = -gyro.x; E.qfrc[da + 4] = -gyro.y; E.qfrc[da + 5] = -gyro.z;
-      E.qacc_s[da] = 0.f; E.qacc_s[da + 1] = 0.f; E.qacc_s[da + 2] = MMX_GRAVITY_Z;
-      E.qacc_s[da + 3] = -gyro.x / I0; E.qacc_s[da + 4] = -gyro.y / I1; E.qacc_s[da + 5] = -gyro.z / I2;
-    }
+    const float len = j >= 0 ? E.qpos[j] : tlen, vel = j >= 0 ? E.qvel[j] : tvel;
+    float f = MMX_act_gain[a] * c + MMX_act_bias[3 * a] + MMX_act_bias[3 * a + 1] * len + MMX_act_bias[3 * a + 2] * vel;
+    E.act_unclamped[a] = f > MMX_act_forcerange[2 * a] && f < MMX_act_forcerange[2 * a + 1];
+    af[a] = fminf(fmaxf(f, MMX_act_forcerange[2 * a]), MMX_act_forcerange[2 * a + 1]);
   }
+  SYNC();
+  float qf = 0.f;
+  if (LANE < 9) {
+    const int d = LANE;
+    qf = -MMX_dof_damping[d] * E.qvel[d] - E.bias[d];
+#pragma unroll
+    for (int a = 0; a < 8; a++) {  // actuator order as the serial accumulation
+      const int j = MMX_act_trn_joint[a];
+      if (j >= 0) qf += j == d ? af[a] : 0.f;
+      else qf += d == 7 ? MMX_tendon_coef[0] * af[a] : (d == 8 ? MMX_tendon_coef[1] * af[a] : 0.f);
+    }
+    E.qfrc[d] = qf;
+  } else if (LANE < 12) {  // free body with com at the origin: gravity + w x (I w)
+    const int c = LANE - 9, b = 16 + c, da = 9 + 6 * c;
+    const float I0 = MMX_body_inertia[9 * b], I1 = MMX_body_inertia[9 * b + 4], I2 = MMX_body_inertia[9 * b + 8];
+    const V3 w = V3{E.qvel[da + 3], E.qvel[da + 4], E.qvel[da + 5]};
+    const V3 gyro = cross(w, V3{I0 * w.x, I1 * w.y, I2 * w.z});
+    const float m = MMX_body_mass[b];
+    E.qfrc[da] = 0.f; E.qfrc[da + 1] = 0.f; E.qfrc[da + 2] = MMX_GRAVITY_Z * m;
+    E.qfrc[da + 3] = -gyro.x; E.qfrc[da + 4] = -gyro.y; E.qfrc[da + 5] = -gyro.z;
+    E.qacc_s[da] = 0.f; E.qacc_s[da + 1] = 0.f; E.qacc_s[da + 2] = MMX_GRAVITY_Z;
+    E.qacc_s[da + 3] = -gyro.x / I0; E.qacc_s[da + 4] = -gyro.y / I1; E.qacc_s[da + 5] = -gyro.z / I2;
+  }
+  float arow[9];
+  const int jr = min(LANE, 8);
+#pragma unroll
+  for (int e = 0; e < 9; e++) arow[e] = E.M[jr][e];
+  const float xs = chol_solve_small<9>(arow, qf, 1e-12f);
+  if (LANE < 9) E.qacc_s[LANE] = xs;
   SYNC();
 }
 
@@ -1261,47 +1261,47 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
   return it;
 }
 
-// ============================================================================ implicitfast + advance (lane 0)
-DEV void integrate_lane0(EnvSh& E) {
-  // qfrc_constraint = M (qacc - qacc_smooth); arm: (M - h qDeriv) qacc = qfrc_smooth + qfrc_constraint
-  float rhs[9], MD[45];
+// ============================================================================ implicitfast + advance (wave)
+// Arm: (M - h qDeriv) qacc = qfrc_smooth + qfrc_constraint with qfrc_constraint = M (x - qacc_s),
+// qDeriv = -(damping + actuator kv where the force is unclamped), solved by a register Cholesky
+// (rows in lanes 0..8); free bodies take the solver's qacc.  Then semi-implicit Euler and
+// free-joint quaternion integration (one lane per cube).
+DEV void integrate_wave(EnvSh& E) {
+  const int d = min(LANE, 8);
+  float arow[9];
+  float rhs = E.qfrc[d];
 #pragma unroll
-  for (int r = 0; r < 9; r++) {
-    float sacc = 0.f;
-#pragma unroll
-    for (int c = 0; c < 9; c++) sacc += E.M[r][c] * (E.x[c] - E.qacc_s[c]);
-    rhs[r] = E.qfrc[r] + sacc;
+  for (int c = 0; c < 9; c++) {
+    arow[c] = E.M[d][c];
+    rhs += E.M[d][c] * (E.x[c] - E.qacc_s[c]);
   }
 #pragma unroll
-  for (int d = 0; d < 9; d++)
-#pragma unroll
-    for (int e = 0; e <= d; e++) MD[LT(d, e)] = E.M[d][e];
-#pragma unroll
-  for (int d = 0; d < 9; d++) MD[LT(d, d)] += kDt * MMX_dof_damping[d];
-#pragma unroll
-  for (int a = 0; a < 7; a++)
-    if (E.act_unclamped[a]) MD[LT(a, a)] -= kDt * MMX_act_bias[3 * a + 2];
-  if (E.act_unclamped[7]) {
-    const float bv = MMX_act_bias[3 * 7 + 2], c0 = MMX_tendon_coef[0], c1 = MMX_tendon_coef[1];
-    MD[LT(7, 7)] -= kDt * bv * c0 * c0;
-    MD[LT(8, 8)] -= kDt * bv * c1 * c1;
-    MD[LT(8, 7)] -= kDt * bv * c0 * c1;
+  for (int c = 0; c < 9; c++) {
+    float a = arow[c];
+    if (c == d) {
+      a += kDt * MMX_dof_damping[d];
+      if (d < 7 && E.act_unclamped[d]) a -= kDt * MMX_act_bias[3 * d + 2];
+    }
+    if (E.act_unclamped[7] && d >= 7 && c >= 7) {  // tendon actuator kv on the finger pair
+      const float bv = MMX_act_bias[3 * 7 + 2];
+      a -= kDt * bv * MMX_tendon_coef[d - 7] * MMX_tendon_coef[c - 7];
+    }
+    arow[c] = a;
   }
-  chol9(MD);
-  chol9_solve(MD, rhs);
+  const float qa_arm = chol_solve_small<9>(arow, rhs, 1e-12f);
   bool bad = false;
-#pragma unroll
-  for (int d = 0; d < 27; d++) {
-    const float qa = d < 9 ? rhs[d] : E.x[d];
-    E.ws[d] = E.x[d];  // warm start keeps the constraint solver's qacc
-    E.qvel[d] += kDt * qa;
-    bad |= !(fabsf(E.qvel[d]) < 1e10f);
+  if (LANE < 27) {
+    const float qa = LANE < 9 ? qa_arm : E.x[LANE];
+    E.ws[LANE] = E.x[LANE];  // warm start keeps the constraint solver's qacc
+    const float v = E.qvel[LANE] + kDt * qa;
+    E.qvel[LANE] = v;
+    bad = !(fabsf(v) < 1e10f);
+    if (LANE < 9) E.qpos[LANE] += kDt * v;
   }
-#pragma unroll
-  for (int d = 0; d < 9; d++) E.qpos[d] += kDt * E.qvel[d];
-#pragma unroll
-  for (int c = 0; c < 3; c++) {
-    const int qa = 9 + 7 * c, da = 9 + 6 * c;
+  if (__ballot(bad) != 0ull && LANE == 0) E.flags |= SHF_NAN;
+  SYNC();
+  if (LANE < 3) {
+    const int c = LANE, qa = 9 + 7 * c, da = 9 + 6 * c;
     E.qpos[qa] += kDt * E.qvel[da];
     E.qpos[qa + 1] += kDt * E.qvel[da + 1];
     E.qpos[qa + 2] += kDt * E.qvel[da + 2];
@@ -1312,8 +1312,10 @@ DEV void integrate_lane0(EnvSh& E) {
     q = qnormalize(q);
     E.qpos[qa + 3] = q.w; E.qpos[qa + 4] = q.x; E.qpos[qa + 5] = q.y; E.qpos[qa + 6] = q.z;
   }
-  if (bad) E.flags |= SHF_NAN;
+  SYNC();
 }
+
+// ============================================================================ implicitfast + advance (lane 0)
 
 // ============================================================================ IK (lane 0)
 DEV void orientation_error(const M3& Rc, V3& err) {  // controller.py:21-43, atan2 form for fp32
@@ -1450,9 +1452,9 @@ DEV void mj_step_wave(int max_iter, float tol, EnvSh& E) {
   float resid = 0.f;
   const int it = newton_wave(E, max_iter, tol, resid);
   CLK(stats, STAT_T_SOLVE);
+  integrate_wave(E);
+  CLK(stats, STAT_T_INT);
   if (LANE == 0) {
-    integrate_lane0(E);
-    CLK(stats, STAT_T_INT);
     stats[STAT_NEFC] += (float)E.nefc;
     stats[STAT_NCON] += (float)E.ncon;
     stats[STAT_SOLVER_ITER] += (float)it;
