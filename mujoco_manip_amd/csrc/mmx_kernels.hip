@@ -59,6 +59,7 @@ struct EnvSh {
   float Lrow[27][27];  // Newton Cholesky factor, row-major (read back as columns)
   float obs[MMX_NOBS + 3];
   int ncon, nefc, flags, iters;
+  int tbase[11];  // rows are grouped by block-pair type: type t owns rows [tbase[t], tbase[t+1])
   int act_unclamped[8];
   float stats[STAT_N];  // lane 0 accumulates; loaded / stored with the env record
 };
@@ -79,6 +80,13 @@ DEV int row_slot(int h, int a) {
   if (ba == b0) return a - blk_d0(b0);
   if (ba == b1) return blk_size(b0) + a - blk_d0(b1);
   return -1;
+}
+// block-pair row types: (0,-) (0,1) (0,2) (0,3) (1,-) (1,2) (1,3) (2,-) (2,3) (3,-)
+#define NTYPE 10
+static constexpr int kTB0[NTYPE] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
+static constexpr int kTB1[NTYPE] = {15, 1, 2, 3, 15, 2, 3, 15, 3, 15};
+DEV int row_type(int b0, int b1) {
+  return b0 == 0 ? (b1 == BLK_NONE ? 0 : b1) : (b0 == 1 ? (b1 == BLK_NONE ? 4 : 3 + b1) : (b0 == 2 ? (b1 == BLK_NONE ? 7 : 8) : 9));
 }
 DEV bool arm_anc(int d, int b) { return d <= 6 ? (b >= d + 2 && b <= 11) : (d == 7 ? b == 10 : b == 11); }
 DEV V3 body_x(const EnvSh& E, int b) {
@@ -141,13 +149,17 @@ DEV float wave_sum(float v) {
          (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)) +
           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48)));
 }
+// wave64 inclusive prefix sum: DPP row_shr butterflies inside each row of 16 lanes, then the
+// row totals (v_readlane) are added to the rows above
 DEV int wave_scan_incl(int v) {
-#pragma unroll
-  for (int o = 1; o < 64; o <<= 1) {
-    const int t = __shfl_up(v, o, 64);
-    if (LANE >= o) v += t;
-  }
-  return v;
+  v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+  v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+  v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+  v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+  const int r0 = __builtin_amdgcn_readlane(v, 15), r1 = __builtin_amdgcn_readlane(v, 31);
+  const int r2 = __builtin_amdgcn_readlane(v, 47);
+  const int row = LANE >> 4;
+  return v + (row == 0 ? 0 : (row == 1 ? r0 : (row == 2 ? r0 + r1 : r0 + r1 + r2)));
 }
 // triangular index e -> (a, b) with a >= b, e = a(a+1)/2 + b
 DEV void tri_index(int e, int& a, int& b) {
@@ -896,7 +908,7 @@ DEV void make_constraints_wave(EnvSh& E) {
   const int ncon = E.ncon;
   int* rowmap = reinterpret_cast<int*>(&E.Lrow[0][0]);  // Lrow is free until the solver
   static_assert(27 * 27 >= MMX_MAXEFC, "rowmap scratch");
-  int nlim = 0, ncr = 0, dim = 0;
+  int nlim = 0, ncr = 0, dim = 0, tc = -1;
   bool lo_act = false, hi_act = false;
   if (LANE < 9) {
     const float q = E.qpos[LANE];
@@ -907,16 +919,52 @@ DEV void make_constraints_wave(EnvSh& E) {
   if (LANE < ncon) {
     dim = (int)E.con[LANE][CON_DIM];
     ncr = dim == 1 ? 1 : 2 * (dim - 1);
+    const int k1 = body_block(MMX_geom_body[(int)E.con[LANE][CON_G1]]);
+    const int k2 = body_block(MMX_geom_body[(int)E.con[LANE][CON_G2]]);
+    int rb0 = k1 >= 0 ? k1 : k2, rb1 = (k1 >= 0 && k2 >= 0 && k2 != k1) ? k2 : BLK_NONE;
+    if (rb1 != BLK_NONE && rb1 < rb0) {
+      const int t = rb0;
+      rb0 = rb1;
+      rb1 = t;
+    }
+    tc = row_type(rb0, rb1);
   }
-  const int mine = (LANE == 0 ? 1 : 0) + nlim + ncr;
-  const int incl = wave_scan_incl(mine);
-  const int total = __shfl(incl, 63, 64);
-  int row = incl - mine;
+  // rows grouped by block-pair type (type-major, lane order inside a type): equality + limits
+  // are arm-only rows (type 0) and come first in type 0
+  const int acnt = (LANE == 0 ? 1 : 0) + nlim;
+  int arow = 0, brow = 0, base = 0;
+  // per-type prefix counts, three 10-bit fields per 32-bit scan (type totals <= MAXEFC < 1024)
+#pragma unroll
+  for (int t0 = 0; t0 < NTYPE; t0 += 3) {
+    int packed = 0;
+#pragma unroll
+    for (int f = 0; f < 3; f++) {
+      const int t = t0 + f;
+      const int cnt = t < NTYPE ? (t == 0 ? acnt : 0) + (tc == t ? ncr : 0) : 0;
+      packed |= cnt << (10 * f);
+    }
+    const int incl = wave_scan_incl(packed);
+    const int tot = __builtin_amdgcn_readlane(incl, 63);
+#pragma unroll
+    for (int f = 0; f < 3; f++) {
+      const int t = t0 + f;
+      if (t >= NTYPE) break;
+      const int cnt = (t == 0 ? acnt : 0) + (tc == t ? ncr : 0);
+      const int excl = ((incl >> (10 * f)) & 1023) - cnt;
+      if (t == 0) arow = base + excl;
+      if (tc == t) brow = base + excl + (t == 0 ? acnt : 0);
+      if (LANE == 0) E.tbase[t] = min(base, MMX_MAXEFC);
+      base += (tot >> (10 * f)) & 1023;
+    }
+  }
+  const int total = base;
   const int nefc = min(total, MMX_MAXEFC);
   if (LANE == 0) {
+    E.tbase[NTYPE] = nefc;
     E.nefc = nefc;
     if (total > MMX_MAXEFC) E.flags |= SHF_EFC_OVF;
   }
+  int row = arow;
   PROBE(3, stats, STAT_T_AUX0);
   float jv[16];
   if (LANE == 0 && row < MMX_MAXEFC) {  // finger equality (panda.xml:261)
@@ -974,7 +1022,7 @@ DEV void make_constraints_wave(EnvSh& E) {
       if (k < 5) E.r[5 * LANE + k] = cgv[k];
       else E.s[5 * LANE + k - 5] = cgv[k];
     }
-    for (int rr = 0; rr < ncr && row < MMX_MAXEFC; rr++, row++) rowmap[row] = LANE | (rr << 8);
+    for (int rr = 0; rr < ncr && brow + rr < MMX_MAXEFC; rr++) rowmap[brow + rr] = LANE | (rr << 8);
   }
   SYNC();
   for (int r = LANE; r < nefc; r += WG) {
@@ -1049,43 +1097,45 @@ DEV void cost2_wave(const EnvSh& E, const float* xa, const float* xb, float& ca,
 }
 
 // J' W [J | r] on the matrix cores: A = J' (dof x row), B = W [J | r] (row x 28), K = rows, two
-// rows per v_mfma_f32_32x32x2_f32 (lane l supplies row t + (l >> 5), dof / column l & 31, for
-// both operands; loads are unconditional so unrolled steps batch them).  Returns, in lane j < 27,
-// row j of H = M + J'WJ in hrow[0..27) and g_j = (M (x - xs) + J'W r)_j.
+// rows per v_mfma_f32_32x32x2_f32 (lane l supplies row 2m + (l >> 5) and dof / column l & 31 for
+// both operands).  Rows are grouped by block-pair type (make_constraints_wave), so inside a type
+// a lane's slot for its dof is fixed: every operand is one direct LDS read, and all types
+// accumulate into the same dof-space 32 x 32 tile (no scatter).  The gradient rides along as
+// column 27 (E.r holds w r).  Returns, in lane j < 27, row j of H = M + J'WJ in hrow[0..27) and
+// g_j = (M (x - xs) + J'W r)_j.
 DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow) {
+  float* stats = E.stats;
+  CLK_DECL;
   const int col = LANE & 31, kh = LANE >> 5;
-  // this lane's dof: block and offset inside the block (none for the padding columns 27..31)
   const int ba = col < 27 ? dof_blk(col) : -1, ob = col < 27 ? col - blk_d0(ba) : 0;
-  // K order: lane half kh walks rows [kh * hh, kh * hh + hh) in groups of 4 (vector loads of the
-  // row headers / weights / residuals, four independent J gathers, four MFMAs)
-  const int hh = ((nefc + 7) >> 3) << 2;
   f32x16 acc0 = {}, acc1 = {};
-  for (int t = 0; t < hh; t += 4) {
-    const int i0 = kh * hh + t;
-    const int4 h4 = *reinterpret_cast<const int4*>(&E.hdr[i0]);
-    const float4 w4 = *reinterpret_cast<const float4*>(&E.s[i0]);
-    const float4 r4 = *reinterpret_cast<const float4*>(&E.r[i0]);
-    const int hv[4] = {h4.x, h4.y, h4.z, h4.w};
-    const float wv[4] = {w4.x, w4.y, w4.z, w4.w}, rv[4] = {r4.x, r4.y, r4.z, r4.w};
-    float jv[4];
+  for (int t = 0; t < NTYPE; t++) {
+    const int r0 = E.tbase[t], r1 = E.tbase[t + 1];
+    if (r1 <= r0) continue;
+    const int b0 = kTB0[t], b1 = kTB1[t];
+    const int sl = ba == b0 ? ob : (ba == b1 ? blk_size(b0) + ob : 15);
+    for (int s0 = r0; s0 < r1; s0 += 8) {  // 4 MFMAs per trip, loads first
+      float jv[4], w[4], wr[4];
+      bool valid[4];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int b0 = hv[u] & 15, b1 = (hv[u] >> 4) & 15;
-      const int sl = ba == b0 ? ob : (ba == b1 ? (b0 == 0 ? 9 : 6) + ob : 15);
-      jv[u] = E.J[min(i0 + u, MMX_MAXEFC - 1)][min(sl, 15)];
-    }
-    float a[4], b[4];
+      for (int u = 0; u < 4; u++) {
+        const int r = s0 + 2 * u + kh;
+        valid[u] = r < r1;
+        const int rc = valid[u] ? r : r0;
+        jv[u] = E.J[rc][sl];
+        w[u] = E.s[rc];
+        wr[u] = E.r[rc];
+      }
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const bool valid = i0 + u < nefc;
-      a[u] = valid ? jv[u] : 0.f;
-      b[u] = valid ? wv[u] * (col < 27 ? jv[u] : (col == 27 ? rv[u] : 0.f)) : 0.f;
+      for (int u = 0; u < 4; u++) {
+        const float a = valid[u] ? jv[u] : 0.f;
+        const float b = valid[u] ? (col < 27 ? w[u] * jv[u] : (col == 27 ? wr[u] : 0.f)) : 0.f;
+        if (u & 1) acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc1, 0, 0, 0);
+        else acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc0, 0, 0, 0);
+      }
     }
-    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[0], b[0], acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[1], b[1], acc1, 0, 0, 0);
-    acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[2], b[2], acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[3], b[3], acc1, 0, 0, 0);
   }
+  PROBE(6, stats, STAT_T_AUX0);
   const int jc = min(LANE, 26);
   float mdx = 0.f;
 #pragma unroll
@@ -1113,6 +1163,7 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow) {
   SYNC();
   const float g = LANE < 27 ? E.g[LANE] + mdx : 0.f;
   SYNC();
+  PROBE(6, stats, STAT_T_AUX1);
   return g;
 }
 
@@ -1190,13 +1241,15 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
       const int i = LANE + WG * q;
       if (i < nefc) {
         const float v = row_dot16(E, i, E.x) - E.aref[i];
+        const float w = (eq[q] || v < 0.f) ? dd[q] : 0.f;
         rr[q] = v;
-        E.r[i] = v;
-        E.s[i] = (eq[q] || v < 0.f) ? dd[q] : 0.f;
+        E.r[i] = w * v;  // w r for the gradient
+        E.s[i] = w;
       }
     }
     SYNC();
     PROBE(1, stats, STAT_T_AUX0);
+    PROBE(6, stats, STAT_T_AUX2);
     float hrow[32];
     const float g = hess_grad_mfma(E, nefc, hrow);
     resid = sqrtf(wave_sum(g * g)) / scale;
