@@ -1096,75 +1096,83 @@ DEV void cost2_wave(const EnvSh& E, const float* xa, const float* xb, float& ca,
   cb = wave_sum(c1);
 }
 
-// J' W [J | r] on the matrix cores: A = J' (dof x row), B = W [J | r] (row x 28), K = rows, two
-// rows per v_mfma_f32_32x32x2_f32 (lane l supplies row 2m + (l >> 5) and dof / column l & 31 for
-// both operands).  Rows are grouped by block-pair type (make_constraints_wave), so inside a type
-// a lane's slot for its dof is fixed: every operand is one direct LDS read, and all types
-// accumulate into the same dof-space 32 x 32 tile (no scatter).  The gradient rides along as
-// column 27 (E.r holds w r).  Returns, in lane j < 27, row j of H = M + J'WJ in hrow[0..27) and
-// g_j = (M (x - xs) + J'W r)_j.
+// J'WJ and J'W r on the matrix cores, one block-pair row type at a time.  Rows of a type share
+// their slot -> dof map, so in slot space the type's contribution is a 16 x 16 tile
+// G = sum_k J_k' [w_k J_k | w_k r_k]: v_mfma_f32_16x16x4_f32 with A[slot i][row k] = J[k][i] and
+// B[row k][slot j] = w_k J[k][j], where slot 15 (always 0 in J) carries w_k r_k instead, so
+// G[:, 15] is the type's gradient.  Lane l supplies J[row + (l >> 4)][l & 15] for both operands:
+// a contiguous read of the block-format rows.  Each tile is staged in LDS and gathered by the
+// dof lanes into their Hessian row (static columns) and gradient.  Returns, in lane j < 27,
+// row j of H = M + J'WJ in hrow[0..27) and g_j = (M (x - xs) + J'W r)_j.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow) {
   float* stats = E.stats;
   CLK_DECL;
-  const int col = LANE & 31, kh = LANE >> 5;
-  const int ba = col < 27 ? dof_blk(col) : -1, ob = col < 27 ? col - blk_d0(ba) : 0;
-  f32x16 acc0 = {}, acc1 = {};
+  float* G = &E.Lrow[0][0];  // 16 x 16 staging tile (Lrow is free until the Cholesky)
+  const int col = LANE & 15, rk = LANE >> 4;
+  const int d = min(LANE, 26);
+  const int bd = dof_blk(d), od = d - blk_d0(bd);
+#pragma unroll
+  for (int i = 0; i < 27; i++) hrow[i] = E.M[d][i];
+  float gacc = 0.f;
+  PROBE(6, stats, STAT_T_AUX3);
   for (int t = 0; t < NTYPE; t++) {
     const int r0 = E.tbase[t], r1 = E.tbase[t + 1];
     if (r1 <= r0) continue;
-    const int b0 = kTB0[t], b1 = kTB1[t];
-    const int sl = ba == b0 ? ob : (ba == b1 ? blk_size(b0) + ob : 15);
-    for (int s0 = r0; s0 < r1; s0 += 8) {  // 4 MFMAs per trip, loads first
-      float jv[4], w[4], wr[4];
-      bool valid[4];
+    f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+    for (int s0 = r0; s0 < r1; s0 += 8) {  // 2 MFMA steps per trip, loads first
+      float jv[2], w[2], wr[2];
+      bool valid[2];
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
-        const int r = s0 + 2 * u + kh;
+      for (int u = 0; u < 2; u++) {
+        const int r = s0 + 4 * u + rk;
         valid[u] = r < r1;
         const int rc = valid[u] ? r : r0;
-        jv[u] = E.J[rc][sl];
+        jv[u] = E.J[rc][col];
         w[u] = E.s[rc];
         wr[u] = E.r[rc];
       }
 #pragma unroll
-      for (int u = 0; u < 4; u++) {
+      for (int u = 0; u < 2; u++) {
         const float a = valid[u] ? jv[u] : 0.f;
-        const float b = valid[u] ? (col < 27 ? w[u] * jv[u] : (col == 27 ? wr[u] : 0.f)) : 0.f;
-        if (u & 1) acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc1, 0, 0, 0);
-        else acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc0, 0, 0, 0);
+        const float b = valid[u] ? (col == 15 ? wr[u] : w[u] * jv[u]) : 0.f;
+        if (u) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc1, 0, 0, 0);
+        else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc0, 0, 0, 0);
       }
     }
+    PROBE(6, stats, STAT_T_AUX0);
+    // stage: lane l holds G[4 (l >> 4) + q][l & 15]
+#pragma unroll
+    for (int q = 0; q < 4; q++) G[16 * (4 * rk + q) + col] = acc0[q] + acc1[q];
+    SYNC();
+    // gather: dof lane d reads row sd of the tile; the type's two blocks land on static columns
+    // of hrow (uniform branches over the 4 possible blocks keep every register index static)
+    const int b0 = kTB0[t], b1 = kTB1[t];
+    const int n0 = blk_size(b0);
+    const int sd = bd == b0 ? od : (bd == b1 ? n0 + od : -1);
+    if (sd >= 0) {
+      const float* Gr = G + 16 * sd;
+#pragma unroll
+      for (int B = 0; B < 4; B++) {
+        const int nb = B == 0 ? 9 : 6, dB = B == 0 ? 0 : 9 + 6 * (B - 1);
+        if (B == b0) {
+#pragma unroll
+          for (int k = 0; k < nb; k++) hrow[dB + k] += Gr[k];
+        } else if (B == b1) {
+#pragma unroll
+          for (int k = 0; k < nb; k++) hrow[dB + k] += Gr[n0 + k];
+        }
+      }
+      gacc += Gr[15];
+    }
+    SYNC();
+    PROBE(6, stats, STAT_T_AUX1);
   }
-  PROBE(6, stats, STAT_T_AUX0);
-  const int jc = min(LANE, 26);
   float mdx = 0.f;
 #pragma unroll
-  for (int b = 0; b < 27; b++) mdx = fmaf(E.M[jc][b], E.x[b] - E.qacc_s[b], mdx);
-  float c[16];
-#pragma unroll
-  for (int r = 0; r < 16; r++) c[r] = acc0[r] + acc1[r];
-  if (col == 27) {  // gradient column: its rows sit in lanes 27 and 59 -> LDS
-#pragma unroll
-    for (int r = 0; r < 16; r++) {
-      const int row = (r & 3) + 8 * (r >> 2) + 4 * kh;
-      if (row < 27) E.g[row] = c[r];
-    }
-  }
-  // lane j < 32 holds C[rows 8m + 0..3][j]; its partner lane j + 32 holds rows 8m + 4..7
-#pragma unroll
-  for (int r = 0; r < 16; r++) {
-    const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(c[r]), __float_as_uint(c[r]), false, false);
-    const int row = (r & 3) + 8 * (r >> 2);
-    hrow[row] = c[r];
-    hrow[row + 4] = __uint_as_float(sw[1]);
-  }
-#pragma unroll
-  for (int i = 0; i < 27; i++) hrow[i] += E.M[jc][i];
-  SYNC();
-  const float g = LANE < 27 ? E.g[LANE] + mdx : 0.f;
-  SYNC();
-  PROBE(6, stats, STAT_T_AUX1);
-  return g;
+  for (int b = 0; b < 27; b++) mdx = fmaf(E.M[d][b], E.x[b] - E.qacc_s[b], mdx);
+  PROBE(6, stats, STAT_T_AUX2);
+  return LANE < 27 ? gacc + mdx : 0.f;
 }
 
 // Returns (H^{-1} v)_j in lane j for H given by rows hrow (lane j = row j, j < 27) and v_j.  The
@@ -1249,7 +1257,6 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
     }
     SYNC();
     PROBE(1, stats, STAT_T_AUX0);
-    PROBE(6, stats, STAT_T_AUX2);
     float hrow[32];
     const float g = hess_grad_mfma(E, nefc, hrow);
     resid = sqrtf(wave_sum(g * g)) / scale;

@@ -109,13 +109,13 @@ def expert_success(N=256, steps=150):
             "secs": time.time() - t, "solver": env.solver_stats()}
 
 
-def rollout_speed(N=4096, steps=20):
+def rollout_speed(N=4096, steps=100, warm=50):
     from mujoco_manip_amd.vec_env import PickPlaceVecEnv
 
     env = PickPlaceVecEnv(N, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
                           autoreset=True)
     env.reset(seed=[_lib.episode_seed(42, i) for i in range(N)])
-    env.rollout_expert(2)
+    env.rollout_expert(warm)  # bench-like state mix (50 warm-up steps)
     torch.cuda.synchronize()
     env.clear_stats()
     t = time.time()
