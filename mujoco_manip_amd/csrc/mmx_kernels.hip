@@ -107,12 +107,18 @@ DEV SV load_S(const EnvSh& E, int d) { return SV{V3{E.S[d][0], E.S[d][1], E.S[d]
 // Built with -DMMX_PHASE_CLOCK (libmmx_prof.so) the kernels add the shader-clock cycles
 // (s_memtime) of each phase into stats[STAT_T_*]; the product build compiles them away.
 #ifdef MMX_PHASE_CLOCK
-#define CLK_DECL unsigned long long clk_t0_ = __builtin_amdgcn_s_memtime()
-#define CLK(st, k)                                                  \
-  do {                                                              \
-    const unsigned long long clk_t1_ = __builtin_amdgcn_s_memtime(); \
-    if (LANE == 0) (st)[k] += (float)(clk_t1_ - clk_t0_);           \
-    clk_t0_ = clk_t1_;                                              \
+// volatile asm: the compiler may not move a stamp across the code it brackets
+__device__ __forceinline__ unsigned long long clk_now() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+#define CLK_DECL unsigned long long clk_t0_ = clk_now()
+#define CLK(st, k)                                                           \
+  do {                                                                       \
+    const unsigned long long clk_t1_ = clk_now();                            \
+    if (LANE == 0 && clk_t1_ > clk_t0_) (st)[k] += (float)(clk_t1_ - clk_t0_); \
+    clk_t0_ = clk_t1_;                                                       \
   } while (0)
 #else
 #define CLK_DECL \
@@ -1218,6 +1224,79 @@ DEV float chol_solve_reg(EnvSh& E, const float* hrow, float v) {
   return y;
 }
 
+// Arrow-ordered register Cholesky solve: pivots in the order cube 1, cube 2, cube 3, arm, and a
+// pivot only updates the blocks it is coupled to (cpl: 4 x 4 bit mask of block pairs sharing a
+// constraint row, plus the fill-in eliminating a block creates among the blocks after it).
+// Uncoupled cubes cost a 6 x 6 factorisation each instead of touching all 27 rows; a grasped cube
+// adds its 6 x 9 coupling to the arm.  Same layout as chol_solve_reg: lane j = dof j.
+DEV float chol_solve_arrow(EnvSh& E, const float* hrow, float v, int cpl) {
+  const int j = LANE;
+  const int pj = j < 9 ? j + 18 : (j < 27 ? j - 9 : 1000);  // elimination position of dof j
+  float h[27], dinv[27];
+#pragma unroll
+  for (int i = 0; i < 27; i++) h[i] = hrow[i];
+#pragma unroll
+  for (int pi = 0; pi < 27; pi++) {
+    const int p = pi < 18 ? pi + 9 : pi - 18;
+    const int bp = p < 9 ? 0 : 1 + (p - 9) / 6;
+    const float d = fmaxf(readlane_f(h[p], p), 1e-20f);
+    const float sd = __builtin_amdgcn_sqrtf(d), inv = __builtin_amdgcn_rcpf(sd);
+    dinv[p] = inv;
+    const float l = j == p ? sd : h[p] * inv;  // lanes after p: L[j][p]
+    h[p] = l;
+#pragma unroll
+    for (int B = 0; B < 4; B++) {
+      const int dB = B == 0 ? 0 : 9 + 6 * (B - 1), nB = B == 0 ? 9 : 6;
+      const int lastpos = B == 0 ? 26 : 6 * B - 1;  // position of the block's last pivot
+      if (lastpos <= pi) continue;                    // block already eliminated (static)
+      if (B == bp || ((cpl >> (4 * bp + B)) & 1)) {
+#pragma unroll
+        for (int k = 0; k < nB; k++) {
+          const int i = dB + k;
+          const int qi = i < 9 ? i + 18 : i - 9;
+          if (qi > pi) h[i] = fmaf(-readlane_f(l, i), l, h[i]);
+        }
+      }
+    }
+    const bool last_of_block = pi == 5 || pi == 11 || pi == 17;
+    if (last_of_block) {  // fill-in among the blocks eliminated later (cubes after bp, then arm)
+#pragma unroll
+      for (int x = 0; x < 4; x++)
+#pragma unroll
+        for (int y = 0; y < 4; y++) {
+          const bool later_x = x == 0 || x > bp, later_y = y == 0 || y > bp;
+          if (x != y && later_x && later_y && x != bp && y != bp && ((cpl >> (4 * bp + x)) & 1) &&
+              ((cpl >> (4 * bp + y)) & 1))
+            cpl |= 1 << (4 * x + y);
+        }
+    }
+  }
+  float y = j < 27 ? v : 0.f;
+#pragma unroll
+  for (int pi = 0; pi < 27; pi++) {  // L y = v in elimination order
+    const int p = pi < 18 ? pi + 9 : pi - 18;
+    const float yk = readlane_f(y, p) * dinv[p];
+    y = j == p ? yk : (pj > pi ? fmaf(-h[p], yk, y) : y);
+  }
+  const int jc = min(j, 26);
+  if (j < 27) {
+#pragma unroll
+    for (int m = 0; m < 27; m++) E.Lrow[j][m] = h[m];
+  }
+  SYNC();
+  float c[27];
+#pragma unroll
+  for (int k = 0; k < 27; k++) c[k] = E.Lrow[k][jc];  // L[k][j]
+#pragma unroll
+  for (int pi = 26; pi >= 0; pi--) {  // L' z = y
+    const int p = pi < 18 ? pi + 9 : pi - 18;
+    const float zk = readlane_f(y, p) * dinv[p];
+    y = j == p ? zk : (pj < pi ? fmaf(-c[p], zk, y) : y);
+  }
+  SYNC();
+  return y;
+}
+
 DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
   float* stats = E.stats;
   CLK_DECL;
@@ -1238,6 +1317,10 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
     rr[q] = 0.f;
     jp[q] = 0.f;
   }
+  int cpl = 0;  // block pairs that share constraint rows (uniform)
+  for (int t = 0; t < NTYPE; t++)
+    if (kTB1[t] != BLK_NONE && E.tbase[t + 1] > E.tbase[t]) cpl |= (1 << (4 * kTB0[t] + kTB1[t])) | (1 << (4 * kTB1[t] + kTB0[t]));
+  cpl = __builtin_amdgcn_readfirstlane(cpl);
   SYNC();
   int it = 0;
   resid = 0.f;
@@ -1262,7 +1345,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
     resid = sqrtf(wave_sum(g * g)) / scale;
     PROBE(1, stats, STAT_T_AUX1);
     if (resid < tol) break;
-    const float pj = chol_solve_reg(E, hrow, -g);
+    const float pj = chol_solve_arrow(E, hrow, -g, cpl);
     if (LANE < 27) E.p[LANE] = pj;
     SYNC();
     PROBE(1, stats, STAT_T_AUX2);
