@@ -519,6 +519,7 @@ DEV float impedance(const float* si, float pos) {
   if (x <= 0.f) return dmin;
   float y;
   if (power == 1.f) y = x;
+  else if (power == 2.f) y = x <= mid ? x * x / mid : 1.f - (1.f - x) * (1.f - x) / (1.f - mid);  // MuJoCo default
   else if (x <= mid) y = powf(x, power) / powf(mid, power - 1.f);
   else y = 1.f - powf(1.f - x, power) / powf(1.f - mid, power - 1.f);
   return dmin + y * (dmax - dmin);

@@ -585,7 +585,9 @@ struct WaveSink {
   // pair constants, loaded once per pair (MuJoCo mixing: friction max, condim max)
   bool ro;
   float mu0, mu1, mu2, dim;
+  int bodies;  // geom bodies packed above the 16-bit order key: b1 << 16 | b2 << 24
   DEV WaveSink(EnvSh* e, int p, bool st, int g1, int g2) : E(e), key(p * 8), store(st) {
+    bodies = (MMX_geom_body[g1] << 16) | (MMX_geom_body[g2] << 24);
     const int c1 = MMX_geom_class[g1], c2 = MMX_geom_class[g2];
     ro = (c1 == 1 && c2 == 2) || (c1 == 2 && c2 == 1);
     mu0 = fmaxf(MMX_geom_friction[3 * g1], MMX_geom_friction[3 * g2]);
@@ -612,7 +614,7 @@ struct WaveSink {
     c[CON_DIM] = dim;
     c[CON_G1] = (float)g1;
     c[CON_G2] = (float)g2;
-    E->conkey[slot] = key++;
+    E->conkey[slot] = (key++) | bodies;
   }
 };
 
@@ -784,14 +786,16 @@ DEV void collide_wave(EnvSh& E, bool only_ro) {
   if (only_ro) return;
   const int n = min(E.ncon, MMX_MAXCON);
   float* tmp = scr + COL_WORK;
-  if (LANE < n) {
-    const int key = E.conkey[LANE];
-    int rank = 0;
-    for (int j = 0; j < n; j++) rank += E.conkey[j] < key;
+  int kb = 0, rank = 0;
+  if (LANE < n) {  // rank by the 16-bit order key; the packed bodies travel with the record
+    kb = E.conkey[LANE];
+    const int key = kb & 0xFFFF;
+    for (int j = 0; j < n; j++) rank += (E.conkey[j] & 0xFFFF) < key;
 #pragma unroll
     for (int f = 0; f < CON_F; f++) tmp[rank * CON_F + f] = E.con[LANE][f];
   }
   SYNC();
+  if (LANE < n) E.conkey[rank] = kb;
   for (int k = LANE; k < n * CON_F; k += WG) (&E.con[0][0])[k] = tmp[k];
   if (LANE == 0) E.ncon = n;
   SYNC();
@@ -834,7 +838,7 @@ DEV void contact_row(EnvSh& E, int row, int c, int rr) {
   const V3 p = V3{cc[CON_POS], cc[CON_POS + 1], cc[CON_POS + 2]};
   const V3 n = V3{cc[CON_N], cc[CON_N + 1], cc[CON_N + 2]};
   const int dim = (int)cc[CON_DIM];
-  const int b1 = MMX_geom_body[(int)cc[CON_G1]], b2 = MMX_geom_body[(int)cc[CON_G2]];
+  const int b1 = (E.conkey[c] >> 16) & 255, b2 = (E.conkey[c] >> 24) & 255;
   const V3 t1 = V3{cgv[CG_T1], cgv[CG_T1 + 1], cgv[CG_T1 + 2]};
   V3 u = n, w = V3{0.f, 0.f, 0.f};
   float diag = cgv[CG_TRAN];
@@ -925,8 +929,8 @@ DEV void make_constraints_wave(EnvSh& E) {
   if (LANE < ncon) {
     dim = (int)E.con[LANE][CON_DIM];
     ncr = dim == 1 ? 1 : 2 * (dim - 1);
-    const int k1 = body_block(MMX_geom_body[(int)E.con[LANE][CON_G1]]);
-    const int k2 = body_block(MMX_geom_body[(int)E.con[LANE][CON_G2]]);
+    const int kb = E.conkey[LANE];
+    const int k1 = body_block((kb >> 16) & 255), k2 = body_block((kb >> 24) & 255);
     int rb0 = k1 >= 0 ? k1 : k2, rb1 = (k1 >= 0 && k2 >= 0 && k2 != k1) ? k2 : BLK_NONE;
     if (rb1 != BLK_NONE && rb1 < rb0) {
       const int t = rb0;
@@ -1006,7 +1010,7 @@ DEV void make_constraints_wave(EnvSh& E) {
     const float* c = E.con[LANE];
     const V3 n = V3{c[CON_N], c[CON_N + 1], c[CON_N + 2]};
     const int g1 = (int)c[CON_G1], g2 = (int)c[CON_G2];
-    const int b1 = MMX_geom_body[g1], b2 = MMX_geom_body[g2];
+    const int b1 = (E.conkey[LANE] >> 16) & 255, b2 = (E.conkey[LANE] >> 24) & 255;
     const V3 y = (n.y < 0.5f && n.y > -0.5f) ? V3{0.f, 1.f, 0.f} : V3{0.f, 0.f, 1.f};  // mju_makeFrame
     const V3 t1 = normalize(y - n * dot(n, y));
     float solref[2], solimp[5];
@@ -1031,6 +1035,7 @@ DEV void make_constraints_wave(EnvSh& E) {
     for (int rr = 0; rr < ncr && brow + rr < MMX_MAXEFC; rr++) rowmap[brow + rr] = LANE | (rr << 8);
   }
   SYNC();
+  PROBE(3, stats, STAT_T_AUX3);
   for (int r = LANE; r < nefc; r += WG) {
     const int m = rowmap[r];
     if (m >= 0) contact_row(E, r, m & 255, m >> 8);
