@@ -1079,11 +1079,15 @@ DEV float row_dot16(const EnvSh& E, int i, const float* x) {
   return s;
 }
 
-// cost at two candidate points (warm start, qacc_smooth) in one pass
-DEV void cost2_wave(const EnvSh& E, const float* xa, const float* xb, float& ca, float& cb) {
+// cost at two candidate points (warm start, qacc_smooth) in one pass; also returns, per lane,
+// the row residuals J x - aref of the rows it owns and (M (x - xs))_lane for both candidates, so
+// the Newton loop starts from them and then only updates them (r += a J p, M dx += a M p)
+DEV void cost2_wave(const EnvSh& E, const float* xa, const float* xb, float& ca, float& cb, float* va, float* vb,
+                    float& ma, float& mb) {
   float c0 = 0.f, c1 = 0.f;
+  ma = 0.f;
+  mb = 0.f;
   if (LANE < 27) {
-    float ma = 0.f, mb = 0.f;
 #pragma unroll
     for (int b = 0; b < 27; b++) {
       const float m = E.M[LANE][b];
@@ -1096,11 +1100,14 @@ DEV void cost2_wave(const EnvSh& E, const float* xa, const float* xb, float& ca,
 #pragma unroll
   for (int q = 0; q < RPL; q++) {
     const int i = LANE + WG * q;
+    va[q] = 0.f;
+    vb[q] = 0.f;
     if (i < E.nefc) {
       const bool eq = (E.hdr[i] >> 8) != 0;
-      const float va = row_dot16(E, i, xa) - E.aref[i], vb = row_dot16(E, i, xb) - E.aref[i];
-      if (eq || va < 0.f) c0 += 0.5f * E.D[i] * va * va;
-      if (eq || vb < 0.f) c1 += 0.5f * E.D[i] * vb * vb;
+      va[q] = row_dot16(E, i, xa) - E.aref[i];
+      vb[q] = row_dot16(E, i, xb) - E.aref[i];
+      if (eq || va[q] < 0.f) c0 += 0.5f * E.D[i] * va[q] * va[q];
+      if (eq || vb[q] < 0.f) c1 += 0.5f * E.D[i] * vb[q] * vb[q];
     }
   }
   ca = wave_sum(c0);
@@ -1116,7 +1123,7 @@ DEV void cost2_wave(const EnvSh& E, const float* xa, const float* xb, float& ca,
 // dof lanes into their Hessian row (static columns) and gradient.  Returns, in lane j < 27,
 // row j of H = M + J'WJ in hrow[0..27) and g_j = (M (x - xs) + J'W r)_j.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow) {
+DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
   float* stats = E.stats;
   CLK_DECL;
   float* G = &E.Lrow[0][0];  // 16 x 16 staging tile (Lrow is free until the Cholesky)
@@ -1179,9 +1186,6 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow) {
     SYNC();
     PROBE(6, stats, STAT_T_AUX1);
   }
-  float mdx = 0.f;
-#pragma unroll
-  for (int b = 0; b < 27; b++) mdx = fmaf(E.M[d][b], E.x[b] - E.qacc_s[b], mdx);
   PROBE(6, stats, STAT_T_AUX2);
   return LANE < 27 ? gacc + mdx : 0.f;
 }
@@ -1307,9 +1311,11 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
   CLK_DECL;
   const int nefc = E.nefc;
   // start from the cheaper of the warm start and qacc_smooth (as MuJoCo does)
-  float c_ws, c_s;
-  cost2_wave(E, E.ws, E.qacc_s, c_ws, c_s);
-  if (LANE < 27) E.x[LANE] = c_ws < c_s ? E.ws[LANE] : E.qacc_s[LANE];
+  float c_ws, c_s, ra[RPL], rs[RPL], mws, ms;
+  cost2_wave(E, E.ws, E.qacc_s, c_ws, c_s, ra, rs, mws, ms);
+  const bool from_ws = c_ws < c_s;
+  if (LANE < 27) E.x[LANE] = from_ws ? E.ws[LANE] : E.qacc_s[LANE];
+  float mdx = from_ws ? mws : ms;  // (M (x - xs))_lane, kept current through the iterations
   float scale = LANE < 27 ? E.qfrc[LANE] * E.qfrc[LANE] : 0.f;
   scale = sqrtf(wave_sum(scale)) + 1.f;
   float rr[RPL], jp[RPL], dd[RPL];
@@ -1319,7 +1325,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
     const int i = LANE + WG * q;
     dd[q] = i < nefc ? E.D[i] : 0.f;
     eq[q] = i < nefc && (E.hdr[i] >> 8) != 0;
-    rr[q] = 0.f;
+    rr[q] = from_ws ? ra[q] : rs[q];
     jp[q] = 0.f;
   }
   int cpl = 0;  // block pairs that share constraint rows (uniform)
@@ -1331,14 +1337,13 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
   resid = 0.f;
   PROBE(1, stats, STAT_T_AUX3);
   for (; it < max_iter; it++) {
-    // residuals r = J x - aref and active weights s (LDS copies feed the MFMA pass)
+    // active weights s and w r of the current residuals (LDS copies feed the MFMA pass)
 #pragma unroll
     for (int q = 0; q < RPL; q++) {
       const int i = LANE + WG * q;
       if (i < nefc) {
-        const float v = row_dot16(E, i, E.x) - E.aref[i];
+        const float v = rr[q];
         const float w = (eq[q] || v < 0.f) ? dd[q] : 0.f;
-        rr[q] = v;
         E.r[i] = w * v;  // w r for the gradient
         E.s[i] = w;
       }
@@ -1346,7 +1351,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
     SYNC();
     PROBE(1, stats, STAT_T_AUX0);
     float hrow[32];
-    const float g = hess_grad_mfma(E, nefc, hrow);
+    const float g = hess_grad_mfma(E, nefc, hrow, mdx);
     resid = sqrtf(wave_sum(g * g)) / scale;
     PROBE(1, stats, STAT_T_AUX1);
     if (resid < tol) break;
@@ -1360,9 +1365,8 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
       const int i = LANE + WG * q;
       jp[q] = i < nefc ? row_dot16(E, i, E.p) : 0.f;
     }
-    float c0 = 0.f, c1 = 0.f;
+    float c0 = 0.f, c1 = 0.f, mp = 0.f;
     if (LANE < 27) {
-      float mp = 0.f;
 #pragma unroll
       for (int b = 0; b < 27; b++) mp = fmaf(E.M[LANE][b], E.p[b], mp);
       c0 = mp * (E.x[LANE] - E.qacc_s[LANE]);
@@ -1398,6 +1402,9 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
       E.x[LANE] += alpha * pj;
       stepn = alpha * alpha * pj * pj;
     }
+    mdx = fmaf(alpha, mp, mdx);
+#pragma unroll
+    for (int q = 0; q < RPL; q++) rr[q] = fmaf(alpha, jp[q], rr[q]);
     SYNC();
     stepn = sqrtf(wave_sum(stepn));
     if (stepn < 1e-9f) {
