@@ -8,6 +8,8 @@
 #ifndef MMX_GEOM_H
 #define MMX_GEOM_H
 #include "mmx_device.h"
+#include "mmx_state.h"
+#include "mmx_clock.h"
 
 enum { GT_PLANE = 0, GT_CYL = 5, GT_BOX = 6, GT_MESH = 7 };
 
@@ -125,6 +127,7 @@ DEV float self3(float a0, float a1, float a2, int k) { return k == 0 ? a0 : (k =
 // poly, tmp: 8 V3 each of per-lane LDS scratch (a quad clipped by 4 half-planes has <= 8 corners)
 template <class Sink>
 DEV void box_box(Sink& cs, const Geom& G1, const Geom& G2, V3* poly, V3* tmp) {
+  CLK_DECL;
   const float* h1 = &MMX_geom_size[3 * G1.g];
   const float* h2 = &MMX_geom_size[3 * G2.g];
   const V3 A[3] = {col(G1.R, 0), col(G1.R, 1), col(G1.R, 2)};
@@ -164,6 +167,7 @@ DEV void box_box(Sink& cs, const Geom& G1, const Geom& G2, V3* poly, V3* tmp) {
         eL = L;
       }
     }
+  PROBEF(8, cs.E->stats, STAT_T_AUX0);
   if (ei >= 0 && best_edge < 0.95f * best_face - 1e-9f) {
     const V3 L = dot(eL, d) < 0.f ? -eL : eL;
     V3 ca = G1.x, cb = G2.x;
@@ -207,20 +211,42 @@ DEV void box_box(Sink& cs, const Geom& G1, const Geom& G2, V3* poly, V3* tmp) {
   const int u = bj == 2 ? 0 : bj + 1, v = bj == 0 ? 2 : bj - 1;
   const V3 Ru = sel3(Ri0, Ri1, Ri2, u) * self3(hi0, hi1, hi2, u);
   const V3 Rv = sel3(Ri0, Ri1, Ri2, v) * self3(hi0, hi1, hi2, v);
-  int np = 4;
-  poly[0] = ci + Ru + Rv;
-  poly[1] = ci - Ru + Rv;
-  poly[2] = ci - Ru - Rv;
-  poly[3] = ci + Ru - Rv;
+  const V3 q0 = ci + Ru + Rv, q1 = ci - Ru + Rv, q2 = ci - Ru - Rv, q3 = ci + Ru - Rv;
   const V3 cr = pr + nref * self3(hr0, hr1, hr2, k);
   const int ru = k == 2 ? 0 : k + 1, rv = k == 0 ? 2 : k - 1;
   const V3 ax0 = sel3(Rr0, Rr1, Rr2, ru), ax1 = sel3(Rr0, Rr1, Rr2, rv);
   const float hru = self3(hr0, hr1, hr2, ru), hrv = self3(hr0, hr1, hr2, rv);
+  const V3 nout = ref1 ? nref : -nref;
+  {  // incident face entirely inside the reference face (a cube resting on a larger box): the
+     // clip below would return the 4 corners unchanged, in order
+    const float b0 = dot(ax0, cr) + hru, b1 = dot(-ax0, cr) + hru, b2 = dot(ax1, cr) + hrv, b3 = dot(-ax1, cr) + hrv;
+    const V3 qs[4] = {q0, q1, q2, q3};
+    bool inside = true;
+#pragma unroll
+    for (int c = 0; c < 4; c++)
+      inside = inside && dot(qs[c], ax0) - b0 <= 0.f && dot(qs[c], -ax0) - b1 <= 0.f && dot(qs[c], ax1) - b2 <= 0.f &&
+               dot(qs[c], -ax1) - b3 <= 0.f;
+    PROBEF(8, cs.E->stats, STAT_T_AUX1);
+    if (inside) {
+#pragma unroll
+      for (int c = 0; c < 4; c++) {
+        const float depth = -dot(qs[c] - cr, nref);
+        if (depth >= 0.f) cs.add(G1.g, G2.g, -depth, qs[c] + nref * (0.5f * depth), nout);
+      }
+      PROBEF(8, cs.E->stats, STAT_T_AUX2);
+      return;
+    }
+  }
+  int np = 4;
+  poly[0] = q0;
+  poly[1] = q1;
+  poly[2] = q2;
+  poly[3] = q3;
   np = clip_poly(poly, np, tmp, ax0, dot(ax0, cr) + hru);
   np = clip_poly(tmp, np, poly, -ax0, dot(-ax0, cr) + hru);
   np = clip_poly(poly, np, tmp, ax1, dot(ax1, cr) + hrv);
   np = clip_poly(tmp, np, poly, -ax1, dot(-ax1, cr) + hrv);
-  const V3 nout = ref1 ? nref : -nref;
+  PROBEF(8, cs.E->stats, STAT_T_AUX3);
   for (int c = 0; c < np; c++) {
     const float depth = -dot(poly[c] - cr, nref);
     if (depth >= 0.f) cs.add(G1.g, G2.g, -depth, poly[c] + nref * (0.5f * depth), nout);

@@ -21,6 +21,7 @@
 #define MMX_MODEL_QUAL static __constant__
 #include "mmx_model_gen.h"
 #include "mmx_device.h"
+#include "mmx_clock.h"
 #include "mmx_geom.h"
 #include "mmx_state.h"
 
@@ -102,41 +103,6 @@ DEV M3 body_R(const EnvSh& E, int b) {
   return R;
 }
 DEV SV load_S(const EnvSh& E, int d) { return SV{V3{E.S[d][0], E.S[d][1], E.S[d][2]}, V3{E.S[d][3], E.S[d][4], E.S[d][5]}}; }
-
-// ---------------------------------------------------------------- phase clock (diagnostic build)
-// Built with -DMMX_PHASE_CLOCK (libmmx_prof.so) the kernels add the shader-clock cycles
-// (s_memtime) of each phase into stats[STAT_T_*]; the product build compiles them away.
-#ifdef MMX_PHASE_CLOCK
-// volatile asm: the compiler may not move a stamp across the code it brackets
-__device__ __forceinline__ unsigned long long clk_now() {
-  unsigned long long t;
-  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  return t;
-}
-#define CLK_DECL unsigned long long clk_t0_ = clk_now()
-#define CLK(st, k)                                                           \
-  do {                                                                       \
-    const unsigned long long clk_t1_ = clk_now();                            \
-    if (LANE == 0 && clk_t1_ > clk_t0_) (st)[k] += (float)(clk_t1_ - clk_t0_); \
-    clk_t0_ = clk_t1_;                                                       \
-  } while (0)
-#else
-#define CLK_DECL \
-  do {           \
-  } while (0)
-#define CLK(st, k) \
-  do {             \
-  } while (0)
-#endif
-// sub-phase probes into STAT_T_AUX0..3: MMX_PROBE selects the phase they instrument
-// (1 solver, 2 collision, 3 constraints)
-#ifndef MMX_PROBE
-#define MMX_PROBE 1
-#endif
-#define PROBE(set, st, k)            \
-  do {                               \
-    if (MMX_PROBE == (set)) CLK(st, k); \
-  } while (0)
 
 // ---------------------------------------------------------------- wave primitives
 // wave64 sum: DPP butterflies inside each row of 16 lanes, then the four row sums in a fixed
