@@ -1205,6 +1205,8 @@ DEV float chol_solve_reg(EnvSh& E, const float* hrow, float v) {
 // Uncoupled cubes cost a 6 x 6 factorisation each instead of touching all 27 rows; a grasped cube
 // adds its 6 x 9 coupling to the arm.  Same layout as chol_solve_reg: lane j = dof j.
 DEV float chol_solve_arrow(EnvSh& E, const float* hrow, float v, int cpl) {
+  float* stats = E.stats;
+  CLK_DECL;
   const int j = LANE;
   const int pj = j < 9 ? j + 18 : (j < 27 ? j - 9 : 1000);  // elimination position of dof j
   float h[27], dinv[27];
@@ -1215,7 +1217,7 @@ DEV float chol_solve_arrow(EnvSh& E, const float* hrow, float v, int cpl) {
     const int p = pi < 18 ? pi + 9 : pi - 18;
     const int bp = p < 9 ? 0 : 1 + (p - 9) / 6;
     const float d = fmaxf(readlane_f(h[p], p), 1e-20f);
-    const float sd = __builtin_amdgcn_sqrtf(d), inv = __builtin_amdgcn_rcpf(sd);
+    const float inv = __builtin_amdgcn_rsqf(d), sd = d * inv;  // one transcendental per pivot
     dinv[p] = inv;
     const float l = j == p ? sd : h[p] * inv;  // lanes after p: L[j][p]
     h[p] = l;
@@ -1246,6 +1248,7 @@ DEV float chol_solve_arrow(EnvSh& E, const float* hrow, float v, int cpl) {
         }
     }
   }
+  PROBE(9, stats, STAT_T_AUX0);
   float y = j < 27 ? v : 0.f;
 #pragma unroll
   for (int pi = 0; pi < 27; pi++) {  // L y = v in elimination order
@@ -1253,6 +1256,7 @@ DEV float chol_solve_arrow(EnvSh& E, const float* hrow, float v, int cpl) {
     const float yk = readlane_f(y, p) * dinv[p];
     y = j == p ? yk : (pj > pi ? fmaf(-h[p], yk, y) : y);
   }
+  PROBE(9, stats, STAT_T_AUX1);
   const int jc = min(j, 26);
   if (j < 27) {
 #pragma unroll
@@ -1262,6 +1266,7 @@ DEV float chol_solve_arrow(EnvSh& E, const float* hrow, float v, int cpl) {
   float c[27];
 #pragma unroll
   for (int k = 0; k < 27; k++) c[k] = E.Lrow[k][jc];  // L[k][j]
+  PROBE(9, stats, STAT_T_AUX2);
 #pragma unroll
   for (int pi = 26; pi >= 0; pi--) {  // L' z = y
     const int p = pi < 18 ? pi + 9 : pi - 18;
@@ -1269,6 +1274,7 @@ DEV float chol_solve_arrow(EnvSh& E, const float* hrow, float v, int cpl) {
     y = j == p ? zk : (pj < pi ? fmaf(-c[p], zk, y) : y);
   }
   SYNC();
+  PROBE(9, stats, STAT_T_AUX3);
   return y;
 }
 
@@ -1331,6 +1337,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
       const int i = LANE + WG * q;
       jp[q] = i < nefc ? row_dot16(E, i, E.p) : 0.f;
     }
+    PROBE(10, stats, STAT_T_AUX0);
     float c0 = 0.f, c1 = 0.f, mp = 0.f;
     if (LANE < 27) {
 #pragma unroll
@@ -1340,8 +1347,10 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
     }
     c0 = wave_sum(c0);
     c1 = wave_sum(c1);
+    PROBE(10, stats, STAT_T_AUX1);
     float alpha = 1.f, lo = 0.f, hi = 3e38f;
     for (int ls = 0; ls < 24; ls++) {
+      if (MMX_PROBE == 10 && LANE == 0) stats[STAT_T_AUX3] += 1.f;  // line-search steps
       float d1 = 0.f, d2 = 0.f;
 #pragma unroll
       for (int q = 0; q < RPL; q++) {
@@ -1363,6 +1372,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
       alpha = na;
     }
     PROBE(1, stats, STAT_T_AUX3);
+    PROBE(10, stats, STAT_T_AUX2);
     float stepn = 0.f;
     if (LANE < 27) {
       E.x[LANE] += alpha * pj;
