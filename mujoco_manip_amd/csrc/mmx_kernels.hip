@@ -425,8 +425,8 @@ DEV float chol_solve_small(const float* arow, float v, float eps) {
   }
 #pragma unroll
   for (int k = 0; k < N; k++) {
-    const float sd = sqrtf(fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(h[k]), k)), eps));
-    const float inv = 1.f / sd;
+    const float d = fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(h[k]), k)), eps);
+    const float inv = __builtin_amdgcn_rsqf(d), sd = d * inv;
     dinv[k] = inv;
     const float l = j == k ? sd : h[k] * inv;
     h[k] = l;
@@ -454,7 +454,10 @@ DEV float chol_solve_small(const float* arow, float v, float eps) {
 
 // whole wave: mass matrix (CRBA entries in parallel), smooth forces, qacc_smooth
 DEV void dynamics_wave(EnvSh& E) {
+  float* stats = E.stats;
+  CLK_DECL;
   rne_wave(E);
+  PROBE(11, stats, STAT_T_AUX0);
   for (int idx = LANE; idx < 27 * LD; idx += WG) (&E.M[0][0])[idx] = 0.f;
   SYNC();
   if (LANE < 45) {
@@ -473,6 +476,7 @@ DEV void dynamics_wave(EnvSh& E) {
     E.M[9 + k][9 + k] = rr < 3 ? MMX_body_mass[b] : MMX_body_inertia[9 * b + 4 * (rr - 3)];
   }
   SYNC();
+  PROBE(11, stats, STAT_T_AUX1);
   // smooth force: passive damping - bias + actuation (arm; one lane per actuator, then per dof),
   // gravity + gyroscopic (cubes, one lane each); arm qacc_smooth = M_arm^{-1} qfrc by a register
   // Cholesky (rows in lanes 0..8)
@@ -515,9 +519,11 @@ DEV void dynamics_wave(EnvSh& E) {
   const int jr = min(LANE, 8);
 #pragma unroll
   for (int e = 0; e < 9; e++) arow[e] = E.M[jr][e];
+  PROBE(11, stats, STAT_T_AUX2);
   const float xs = chol_solve_small<9>(arow, qf, 1e-12f);
   if (LANE < 9) E.qacc_s[LANE] = xs;
   SYNC();
+  PROBE(11, stats, STAT_T_AUX3);
 }
 
 // ============================================================================ collision (wave)
@@ -1568,6 +1574,61 @@ DEV void ik_lane0(EnvSh& E) {
   }
 }
 
+// Wave form of ik_lane0: J columns one lane per arm joint, the 6 x 6 DLS system one lane per row
+// (register Cholesky), dq = b + J' A^{-1} (e - J b) with b the null-space pull toward home
+// (= J' A^{-1} e + (I - J' A^{-1} J) b of controller.py:111-124).  Scratch: E.Lrow (free here).
+DEV void ik_wave(EnvSh& E) {
+  float* W = &E.Lrow[0][0];  // J [6][8] at 0, b [8] at 48, e [8] at 56, u [8] at 64
+  const V3 ee = V3{E.kin[KIN_HAND_POS], E.kin[KIN_HAND_POS + 1], E.kin[KIN_HAND_POS + 2]};
+  if (LANE < 7) {
+    const int d = LANE;
+    const V3 ax = V3{E.kin[KIN_AXIS + 3 * d], E.kin[KIN_AXIS + 3 * d + 1], E.kin[KIN_AXIS + 3 * d + 2]};
+    const V3 an = V3{E.kin[KIN_ANCHOR + 3 * d], E.kin[KIN_ANCHOR + 3 * d + 1], E.kin[KIN_ANCHOR + 3 * d + 2]};
+    const V3 jp = cross(ax, ee - an);
+    W[0 * 8 + d] = jp.x; W[1 * 8 + d] = jp.y; W[2 * 8 + d] = jp.z;
+    W[3 * 8 + d] = ax.x; W[4 * 8 + d] = ax.y; W[5 * 8 + d] = ax.z;
+    W[48 + d] = 0.5f * (kHome[d] - E.qpos[d]);
+  } else if (LANE == 7) {
+    M3 Rc;
+#pragma unroll
+    for (int k = 0; k < 9; k++) Rc.m[k] = E.kin[KIN_HAND_MAT + k];
+    V3 ori;
+    orientation_error(Rc, ori);
+    W[56] = E.target[0] - ee.x; W[57] = E.target[1] - ee.y; W[58] = E.target[2] - ee.z;
+    W[59] = ori.x; W[60] = ori.y; W[61] = ori.z;
+  }
+  SYNC();
+  const int r = min(LANE, 5);
+  float arow[6], rhs = W[56 + r];
+#pragma unroll
+  for (int c = 0; c < 6; c++) arow[c] = r == c ? 1e-3f : 0.f;
+#pragma unroll
+  for (int k = 0; k < 7; k++) {
+    const float jr = W[8 * r + k];
+#pragma unroll
+    for (int c = 0; c < 6; c++) arow[c] = fmaf(jr, W[8 * c + k], arow[c]);
+    rhs = fmaf(-jr, W[48 + k], rhs);
+  }
+  const float u = chol_solve_small<6>(arow, rhs, 1e-20f);
+  if (LANE < 6) W[64 + LANE] = u;
+  SYNC();
+  float dq = 0.f;
+  if (LANE < 7) {
+    dq = W[48 + LANE];
+#pragma unroll
+    for (int rr = 0; rr < 6; rr++) dq = fmaf(W[8 * rr + LANE], W[64 + rr], dq);
+  }
+  const float nrm = sqrtf(wave_sum(dq * dq));
+  const float scl = nrm > 5.0f ? 5.0f / nrm : 1.0f;
+  if (LANE < 7) {
+    float t = E.qpos[LANE] + dq * scl;
+    const float lo = MMX_jnt_range[2 * LANE], hi = MMX_jnt_range[2 * LANE + 1];
+    if (lo < hi) t = fminf(fmaxf(t, lo), hi);
+    E.ctrl[LANE] = t;
+  }
+  SYNC();
+}
+
 // ============================================================================ one mj_step
 DEV void mj_step_wave(int max_iter, float tol, EnvSh& E) {
   float* stats = E.stats;
@@ -2063,7 +2124,7 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_substep_kernel(MMXState S, 
   {
     float* stats = E.stats;
     CLK_DECL;
-    if ((mode & SS_IK) && LANE == 0) ik_lane0(E);  // IK on the kinematics of the previous position stage
+    if (mode & SS_IK) ik_wave(E);  // IK on the kinematics of the previous position stage
     SYNC();
     CLK(stats, STAT_T_IK);
   }
@@ -2094,8 +2155,7 @@ __device__ __attribute__((noinline)) void substep(int max_iter, float tol) {
   EnvSh& E = g_E;
   float* stats = E.stats;
   CLK_DECL;
-  if (LANE == 0) ik_lane0(E);  // IK on the kinematics left by the previous position stage
-  SYNC();
+  ik_wave(E);  // IK on the kinematics left by the previous position stage
   CLK(stats, STAT_T_IK);
   mj_step_wave(max_iter, tol, E);
 }
