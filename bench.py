@@ -104,6 +104,9 @@ def main():
     ap.add_argument("--envs-per-gpu", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    # rehearsal of the N > 1 path on a 1-GPU box: ranks share device 0 and talk over gloo
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"))
+    ap.add_argument("--share-device", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -114,20 +117,23 @@ def main():
     if not args.no_cpu_baseline and world == 1 and rank == 0:
         cpu = cpu_baseline(args.cpu_seconds)
     dist = None
+    dev_index = 0 if args.share_device else local_rank
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
-    dev = torch.device(f"cuda:{local_rank}")
+        torch.cuda.set_device(dev_index)
+        dist.init_process_group(args.dist_backend)
+    dev = torch.device(f"cuda:{dev_index}")
     torch.cuda.set_device(dev)
+    # collectives run on device tensors over RCCL, on host tensors over gloo
+    cdev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
     from mujoco_manip_amd import _lib
     from mujoco_manip_amd.vec_env import PickPlaceVecEnv
 
     N = args.envs_per_gpu
     env = PickPlaceVecEnv(N, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
-                          autoreset=True, device=local_rank)
+                          autoreset=True, device=dev_index)
     seeds = [_lib.episode_seed(42, rank * N + i) for i in range(N)]
     env.reset(seed=seeds)
 
@@ -152,7 +158,7 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps  # per launch
     if dist:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     solver = env.solver_stats()
@@ -165,7 +171,7 @@ def main():
 
     stats_all = None
     if dist:
-        loc = torch.tensor([solver["mean_nefc"], solver["mean_solver_iter"], value / world], device=dev)
+        loc = torch.tensor([solver["mean_nefc"], solver["mean_solver_iter"], value / world], device=cdev)
         gathered = [torch.zeros_like(loc) for _ in range(world)]
         dist.all_gather(gathered, loc)
         stats_all = [g.tolist() for g in gathered]
