@@ -141,8 +141,10 @@ def main():
     env.rollout_expert(args.warmup)
     torch.cuda.synchronize()
     env.clear_stats()
-    # the sim launches on torch's current stream: events there bracket exactly the K launches of
-    # the dominant (and only) kernel of a step, mmx_env_step_kernel (one launch per env step)
+    # the sim launches on torch's current stream and forks its `lanes` concurrent env ranges from
+    # it (each range: one mmx_env_step_kernel launch per env step on its own stream, joined back at
+    # the end): events on that stream bracket the K env steps of every range, so kern_ms is the
+    # per-step span over which the lanes' launches (N envs in total) ran side by side
     stream = torch.cuda.current_stream(dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if dist:
@@ -196,6 +198,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "mmx_env_step_kernel", "kernel_ms": kern_ms,
+                         "concurrent_launches": env.sim.rollout_lanes,
                          "algorithmic_bytes_per_launch": bytes_per_launch, "mean_nefc": solver["mean_nefc"],
                          "min_hbm_bytes_per_launch": min_bytes,
                          "min_hbm_GBs": min_bytes / (kern_ms * 1e-3) / 1e9},

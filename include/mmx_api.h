@@ -109,6 +109,11 @@ int mmx_expert_plan(mmx_sim* sim, int32_t n_steps, float* action_dev_out);
  * Requires action_mode == MMX_ACTION_ABS_POS. */
 int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps);
 
+/* Number of independent env ranges a multi-step rollout runs concurrently (one internal stream
+ * each, forked from and joined back to cfg.stream; env MMX_STREAMS overrides the default of one
+ * range per 1024 envs).  Single-step calls always run as one launch on cfg.stream. */
+int mmx_rollout_lanes(const mmx_sim* sim);
+
 /* Physics-level entry points (parity harnesses): n x mujoco.mj_step with the current ctrl
  * (env.py:119-121), optionally preceded by IKController.compute toward the decoded target
  * each substep; and the mj_forward position stage (kinematics + IK cache). */

@@ -51,7 +51,7 @@ class MMXBuffers(C.Structure):
 
 EXPORTED = ("mmx_config_default", "mmx_create", "mmx_destroy", "mmx_last_error", "mmx_reset", "mmx_step",
             "mmx_expert_plan", "mmx_rollout_expert", "mmx_physics_step", "mmx_forward", "mmx_get_buffers",
-            "mmx_synchronize", "mmx_get_state", "mmx_set_state", "mmx_episode_seed")
+            "mmx_synchronize", "mmx_get_state", "mmx_set_state", "mmx_episode_seed", "mmx_rollout_lanes")
 
 _lib = None
 
@@ -79,6 +79,8 @@ def load(build_if_missing: bool = True):
     L.mmx_expert_plan.argtypes = [vp, C.c_int32, vp]
     L.mmx_rollout_expert.argtypes = [vp, C.c_int32]
     L.mmx_physics_step.argtypes = [vp, C.c_int32, C.c_int32]
+    L.mmx_rollout_lanes.argtypes = [vp]
+    L.mmx_rollout_lanes.restype = C.c_int
     L.mmx_forward.argtypes = [vp]
     L.mmx_get_buffers.argtypes = [vp, C.POINTER(MMXBuffers)]
     L.mmx_synchronize.argtypes = [vp]
@@ -202,6 +204,10 @@ class Sim:
 
     def rollout_expert(self, n_env_steps: int):
         self._check(self.L.mmx_rollout_expert(self.ptr, n_env_steps), "mmx_rollout_expert")
+
+    @property
+    def rollout_lanes(self) -> int:
+        return int(self.L.mmx_rollout_lanes(self.ptr))
 
     def physics_step(self, n: int = 1, with_ik: bool = False):
         self._check(self.L.mmx_physics_step(self.ptr, n, int(with_ik)), "mmx_physics_step")

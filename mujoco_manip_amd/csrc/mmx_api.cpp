@@ -5,7 +5,9 @@
 // device PCG64 streams are bit-identical to the reference's np_random streams.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <random>
 #include <string>
@@ -16,7 +18,7 @@
 
 extern "C" hipError_t mmx_launch_reset(const MMXState* S, const unsigned char* mask, const int* task, hipStream_t st);
 extern "C" hipError_t mmx_launch_step(const MMXState* S, const float* action, int adim, int expert_autoreset,
-                                      hipStream_t st);
+                                      int base, int count, hipStream_t st);
 extern "C" hipError_t mmx_launch_expert(const MMXState* S, int n, float* action, hipStream_t st);
 extern "C" hipError_t mmx_launch_physics(const MMXState* S, int n, int with_ik, hipStream_t st);
 extern "C" hipError_t mmx_launch_forward(const MMXState* S, hipStream_t st);
@@ -30,6 +32,13 @@ struct mmx_sim {
   float* expert_action;  // [N][4]
   unsigned char* d_mask;
   int* d_task;
+  // Multi-step rollouts split the envs into `nlanes` independent ranges, each stepped on its own
+  // stream (lane 0 = the caller's stream): the ranges never wait for each other between steps,
+  // so one range's last-wave tail overlaps the next step of the others.
+  static constexpr int kMaxLanes = 8;
+  int nlanes = 1;
+  hipStream_t lane[kMaxLanes] = {};
+  hipEvent_t ev_fork = nullptr, ev_join[kMaxLanes] = {};
 };
 
 namespace {
@@ -113,7 +122,10 @@ template <typename T>
 T* dalloc(mmx_sim* sim, size_t count) {
   void* p = nullptr;
   if (hipMalloc(&p, count * sizeof(T)) != hipSuccess) return nullptr;
-  hipMemset(p, 0, count * sizeof(T));
+  if (hipMemset(p, 0, count * sizeof(T)) != hipSuccess) {
+    (void)hipFree(p);
+    return nullptr;
+  }
   sim->allocs.push_back(p);
   return static_cast<T*>(p);
 }
@@ -220,16 +232,38 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
     pcg64_seed((static_cast<uint64_t>(rd()) << 32) ^ rd(), st);
     for (int k = 0; k < 4; k++) rng[4 * i + k] = st[k];
   }
-  hipMemcpy(S.rng, rng.data(), rng.size() * sizeof(unsigned long long), hipMemcpyHostToDevice);
+  if (hipMemcpy(S.rng, rng.data(), rng.size() * sizeof(unsigned long long), hipMemcpyHostToDevice) != hipSuccess) {
+    mmx_destroy(sim);
+    return MMX_EDEVICE;
+  }
+  // rollout lanes: MMX_STREAMS overrides; by default one lane per 1024 envs (the chip holds
+  // 1024 resident step workgroups), at most kMaxLanes
+  int lanes = N / 1024;
+  if (const char* v = std::getenv("MMX_STREAMS")) lanes = std::atoi(v);
+  lanes = std::max(1, std::min(lanes, std::min(N, int(mmx_sim::kMaxLanes))));
+  if (hipEventCreateWithFlags(&sim->ev_fork, hipEventDisableTiming) != hipSuccess) lanes = 1;
+  for (int l = 1; l < lanes; l++)
+    if (hipStreamCreateWithFlags(&sim->lane[l], hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&sim->ev_join[l], hipEventDisableTiming) != hipSuccess) {
+      if (sim->lane[l]) (void)hipStreamDestroy(sim->lane[l]);
+      lanes = l;
+      break;
+    }
+  sim->nlanes = lanes;
   *out = sim;
   return hip_check(sim, hipDeviceSynchronize(), "mmx_create");
 }
 
 void mmx_destroy(mmx_sim* sim) {
   if (!sim) return;
-  hipDeviceSynchronize();
+  (void)hipDeviceSynchronize();
   for (void* p : sim->allocs)
-    if (p) hipFree(p);
+    if (p) (void)hipFree(p);
+  for (int l = 1; l < sim->nlanes; l++) {
+    (void)hipEventDestroy(sim->ev_join[l]);
+    (void)hipStreamDestroy(sim->lane[l]);
+  }
+  if (sim->ev_fork) (void)hipEventDestroy(sim->ev_fork);
   delete sim;
 }
 
@@ -243,10 +277,12 @@ int mmx_reset(mmx_sim* sim, const uint64_t* seeds, const uint8_t* seed_given, co
   if (seeds) {
     // re-seed selected envs: PCG64(SeedSequence(seed)); the 32-bit buffer is cleared
     std::vector<unsigned long long> rng(4 * n);
+    if (hipStreamSynchronize(sim->stream) != hipSuccess) return fail(sim, MMX_EDEVICE, "mmx_reset sync");
     if (hipMemcpy(rng.data(), S.rng, rng.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) != hipSuccess)
       return fail(sim, MMX_EDEVICE, "rng readback");
     std::vector<int> epi(EPI_N * n);
-    hipMemcpy(epi.data(), S.epi, epi.size() * sizeof(int), hipMemcpyDeviceToHost);
+    if (hipMemcpy(epi.data(), S.epi, epi.size() * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+      return fail(sim, MMX_EDEVICE, "epi readback");
     for (size_t i = 0; i < n; i++) {
       if (env_mask && !env_mask[i]) continue;
       if (seed_given && !seed_given[i]) continue;
@@ -255,13 +291,15 @@ int mmx_reset(mmx_sim* sim, const uint64_t* seeds, const uint8_t* seed_given, co
       for (int k = 0; k < 4; k++) rng[4 * i + k] = st[k];
       epi[EPI_N * i + EPI_RNG_HAS32] = 0;
     }
-    hipMemcpy(S.rng, rng.data(), rng.size() * sizeof(unsigned long long), hipMemcpyHostToDevice);
-    hipMemcpy(S.epi, epi.data(), epi.size() * sizeof(int), hipMemcpyHostToDevice);
+    if (hipMemcpy(S.rng, rng.data(), rng.size() * sizeof(unsigned long long), hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(S.epi, epi.data(), epi.size() * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)
+      return fail(sim, MMX_EDEVICE, "rng upload");
   }
   const unsigned char* dmask = nullptr;
   const int* dtask = nullptr;
   if (env_mask) {
-    hipMemcpyAsync(sim->d_mask, env_mask, n, hipMemcpyHostToDevice, sim->stream);
+    if (hipMemcpyAsync(sim->d_mask, env_mask, n, hipMemcpyHostToDevice, sim->stream) != hipSuccess)
+      return fail(sim, MMX_EDEVICE, "mask upload");
     dmask = sim->d_mask;
   }
   if (task_override) {
@@ -269,7 +307,8 @@ int mmx_reset(mmx_sim* sim, const uint64_t* seeds, const uint8_t* seed_given, co
       const int t = task_override[i];
       if (t >= 0 && ((t >> 4) > 2 || (t & 15) > 2)) return fail(sim, MMX_EINVAL, "task_override out of range");
     }
-    hipMemcpyAsync(sim->d_task, task_override, n * sizeof(int), hipMemcpyHostToDevice, sim->stream);
+    if (hipMemcpyAsync(sim->d_task, task_override, n * sizeof(int), hipMemcpyHostToDevice, sim->stream) != hipSuccess)
+      return fail(sim, MMX_EDEVICE, "task upload");
     dtask = sim->d_task;
   }
   int rc = hip_check(sim, mmx_launch_reset(&S, dmask, dtask, sim->stream), "mmx_reset");
@@ -281,7 +320,7 @@ int mmx_step(mmx_sim* sim, const float* action_dev, int32_t action_dim) {
   if (!sim || !action_dev) return MMX_EINVAL;
   static const int kDim[5] = {4, 8, 10, 8, 10};
   if (action_dim < kDim[sim->S.action_mode]) return fail(sim, MMX_EINVAL, "action_dim too small for action_mode");
-  return hip_check(sim, mmx_launch_step(&sim->S, action_dev, action_dim, 0, sim->stream), "mmx_step");
+  return hip_check(sim, mmx_launch_step(&sim->S, action_dev, action_dim, 0, 0, sim->S.N, sim->stream), "mmx_step");
 }
 
 int mmx_expert_plan(mmx_sim* sim, int32_t n_steps, float* action_dev_out) {
@@ -291,12 +330,29 @@ int mmx_expert_plan(mmx_sim* sim, int32_t n_steps, float* action_dev_out) {
 
 int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
   if (!sim || sim->S.action_mode != MMX_ACTION_ABS_POS) return MMX_EINVAL;
-  for (int k = 0; k < n_env_steps; k++) {  // the step kernel plans with the FSM itself (expert=1)
-    hipError_t e = mmx_launch_step(&sim->S, sim->expert_action, 4, 1, sim->stream);
-    if (e != hipSuccess) return hip_check(sim, e, "mmx_rollout_expert");
+  const int N = sim->S.N, L = n_env_steps > 1 ? sim->nlanes : 1;
+  hipError_t e = hipSuccess;
+  if (L > 1) {  // fork: every lane starts after the work already queued on the caller's stream
+    e = hipEventRecord(sim->ev_fork, sim->stream);
+    for (int l = 1; l < L && e == hipSuccess; l++) e = hipStreamWaitEvent(sim->lane[l], sim->ev_fork, 0);
   }
-  return MMX_OK;
+  // the step kernel plans with the FSM itself (expert=1); step k of range l only depends on step
+  // k-1 of range l
+  for (int k = 0; k < n_env_steps && e == hipSuccess; k++)
+    for (int l = 0; l < L && e == hipSuccess; l++) {
+      const int b0 = (int)((long)N * l / L), b1 = (int)((long)N * (l + 1) / L);
+      e = mmx_launch_step(&sim->S, sim->expert_action, 4, 1, b0, b1 - b0, l ? sim->lane[l] : sim->stream);
+    }
+  if (L > 1)  // join: the caller's stream sees the whole rollout, as with a single launch chain
+    for (int l = 1; l < L; l++) {
+      hipError_t j = hipEventRecord(sim->ev_join[l], sim->lane[l]);
+      if (j == hipSuccess) j = hipStreamWaitEvent(sim->stream, sim->ev_join[l], 0);
+      if (e == hipSuccess) e = j;
+    }
+  return hip_check(sim, e, "mmx_rollout_expert");
 }
+
+int mmx_rollout_lanes(const mmx_sim* sim) { return sim ? sim->nlanes : 0; }
 
 int mmx_physics_step(mmx_sim* sim, int32_t n, int32_t with_ik) {
   if (!sim || n < 0) return MMX_EINVAL;

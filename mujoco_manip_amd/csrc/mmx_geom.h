@@ -69,31 +69,56 @@ template <class Sink>
 DEV void plane_box(Sink& cs, const Geom& P, const Geom& B) {
   const V3 nz = col(P.R, 2);
   const float* h = &MMX_geom_size[3 * B.g];
-  float depth[8];
-  V3 pts[8];
+  // penetrating corners compacted in corner order, then a selection sort of the 4 deepest, as
+  // the oracle does it; every index is static (select chains), so nothing lands in scratch
+  float cd[8];
+  V3 cp[8];
   int cnt = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    cd[k] = 0.f;
+    cp[k] = V3{0.f, 0.f, 0.f};
+  }
 #pragma unroll
   for (int k = 0; k < 8; k++) {
     const V3 l = V3{(k & 1) ? h[0] : -h[0], (k & 2) ? h[1] : -h[1], (k & 4) ? h[2] : -h[2]};
     const V3 w = B.x + mul(B.R, l);
     const float d = dot(w - P.x, nz);
     if (d <= 0.f) {
-      depth[cnt] = d;
-      pts[cnt] = w - nz * (0.5f * d);
+      const V3 pw = w - nz * (0.5f * d);
+#pragma unroll
+      for (int q = 0; q <= k; q++)
+        if (q == cnt) {
+          cd[q] = d;
+          cp[q] = pw;
+        }
       cnt++;
     }
   }
-  for (int k = 0; k < cnt && k < 4; k++) {  // keep the 4 deepest corners
+#pragma unroll
+  for (int k = 0; k < 4; k++) {  // keep the 4 deepest corners
+    if (k >= cnt) break;
     int bi = k;
-    for (int m = k + 1; m < cnt; m++)
-      if (depth[m] < depth[bi]) bi = m;
-    const float td = depth[k];
-    depth[k] = depth[bi];
-    depth[bi] = td;
-    const V3 tp = pts[k];
-    pts[k] = pts[bi];
-    pts[bi] = tp;
-    cs.add(P.g, B.g, depth[k], pts[k], nz);
+    float bd = cd[k];
+    V3 bp = cp[k];
+#pragma unroll
+    for (int m = k + 1; m < 8; m++)
+      if (m < cnt && cd[m] < bd) {
+        bi = m;
+        bd = cd[m];
+        bp = cp[m];
+      }
+    const float td = cd[k];
+    const V3 tp = cp[k];
+    cd[k] = bd;
+    cp[k] = bp;
+#pragma unroll
+    for (int m = k + 1; m < 8; m++)
+      if (m == bi) {
+        cd[m] = td;
+        cp[m] = tp;
+      }
+    cs.add(P.g, B.g, cd[k], cp[k], nz);
   }
 }
 
@@ -319,8 +344,10 @@ DEV SVx mk_sv(const Geom& A, const Geom& B, V3 dir) {
   s.w = s.a - s.b;
   return s;
 }
-DEV bool gjk_line(SVx* S, int& n, V3& dir) {
-  const V3 ab = S[1].w - S[0].w, ao = -S[0].w;
+// GJK simplex in named registers (s0 = newest point): every case below is a fixed permutation,
+// so no simplex element is ever indexed at run time (that spilled the simplex to scratch).
+DEV bool gjk_line(const SVx& s0, const SVx& s1, int& n, V3& dir) {
+  const V3 ab = s1.w - s0.w, ao = -s0.w;
   if (dot(ab, ao) > 0.f) {
     dir = cross(cross(ab, ao), ab);
     n = 2;
@@ -330,70 +357,74 @@ DEV bool gjk_line(SVx* S, int& n, V3& dir) {
   dir = ao;
   return false;
 }
-DEV bool gjk_tri(SVx* S, int& n, V3& dir) {
-  const V3 ab = S[1].w - S[0].w, ac = S[2].w - S[0].w, ao = -S[0].w;
+DEV bool gjk_tri(const SVx& s0, SVx& s1, SVx& s2, int& n, V3& dir) {
+  const V3 ab = s1.w - s0.w, ac = s2.w - s0.w, ao = -s0.w;
   const V3 abc = cross(ab, ac);
   if (dot(cross(abc, ac), ao) > 0.f) {
     if (dot(ac, ao) > 0.f) {
-      S[1] = S[2];
+      s1 = s2;
       n = 2;
       dir = cross(cross(ac, ao), ac);
       return false;
     }
     n = 2;
-    return gjk_line(S, n, dir);
+    return gjk_line(s0, s1, n, dir);
   }
   if (dot(cross(ab, abc), ao) > 0.f) {
     n = 2;
-    return gjk_line(S, n, dir);
+    return gjk_line(s0, s1, n, dir);
   }
   const float dd = dot(abc, ao);
   n = 3;
   if (fabsf(dd) < 1e-12f * (1.f + dot(abc, abc))) return true;
   if (dd > 0.f) dir = abc;
   else {
-    const SVx t = S[1];
-    S[1] = S[2];
-    S[2] = t;
+    const SVx t = s1;
+    s1 = s2;
+    s2 = t;
     dir = -abc;
   }
   return false;
 }
-DEV bool gjk_tet(SVx* S, int& n, V3& dir) {
-  const V3 ao = -S[0].w;
-  const int F[3][3] = {{0, 1, 2}, {0, 2, 3}, {0, 3, 1}};
-  const int O[3] = {3, 1, 2};
-  for (int f = 0; f < 3; f++) {
-    V3 nn = cross(S[F[f][1]].w - S[0].w, S[F[f][2]].w - S[0].w);
-    if (dot(nn, S[O[f]].w - S[0].w) > 0.f) nn = -nn;
-    if (dot(nn, ao) > 0.f) {
-      const SVx t0 = S[F[f][0]], t1 = S[F[f][1]], t2 = S[F[f][2]];
-      S[0] = t0;
-      S[1] = t1;
-      S[2] = t2;
-      n = 3;
-      return gjk_tri(S, n, dir);
-    }
+// face (s0, b, c) with the fourth vertex o opposite: does the origin lie beyond it?
+DEV bool gjk_face_out(const SVx& s0, const SVx& b, const SVx& c, const SVx& o) {
+  V3 nn = cross(b.w - s0.w, c.w - s0.w);
+  if (dot(nn, o.w - s0.w) > 0.f) nn = -nn;
+  return dot(nn, -s0.w) > 0.f;
+}
+DEV bool gjk_tet(const SVx& s0, SVx& s1, SVx& s2, SVx& s3, int& n, V3& dir) {
+  n = 3;
+  if (gjk_face_out(s0, s1, s2, s3)) return gjk_tri(s0, s1, s2, n, dir);  // face (0,1,2)
+  if (gjk_face_out(s0, s2, s3, s1)) {                                     // face (0,2,3)
+    s1 = s2;
+    s2 = s3;
+    return gjk_tri(s0, s1, s2, n, dir);
+  }
+  if (gjk_face_out(s0, s3, s1, s2)) {  // face (0,3,1)
+    s2 = s1;
+    s1 = s3;
+    return gjk_tri(s0, s1, s2, n, dir);
   }
   n = 4;
   return true;
 }
-DEV bool gjk(const Geom& A, const Geom& B, SVx* S, int& n) {
+DEV bool gjk(const Geom& A, const Geom& B, SVx& s0, SVx& s1, SVx& s2, SVx& s3, int& n) {
   V3 dir = A.x - B.x;
   if (norm(dir) < 1e-9f) dir = V3{1.f, 0.f, 0.f};
-  S[0] = mk_sv(A, B, dir);
+  s0 = mk_sv(A, B, dir);
   n = 1;
-  dir = -S[0].w;
+  dir = -s0.w;
   for (int it = 0; it < 48; it++) {
     if (norm(dir) < 1e-12f) return true;
     const SVx P = mk_sv(A, B, dir);
     if (dot(P.w, dir) < 0.f) return false;
-#pragma unroll
-    for (int k = 3; k > 0; k--)  // static indices keep the simplex in registers
-      if (k <= n) S[k] = S[k - 1];
-    S[0] = P;
+    s3 = s2;  // push P; entries beyond n are dead
+    s2 = s1;
+    s1 = s0;
+    s0 = P;
     n++;
-    const bool hit = n == 2 ? gjk_line(S, n, dir) : (n == 3 ? gjk_tri(S, n, dir) : gjk_tet(S, n, dir));
+    const bool hit = n == 2 ? gjk_line(s0, s1, n, dir)
+                            : (n == 3 ? gjk_tri(s0, s1, s2, n, dir) : gjk_tet(s0, s1, s2, s3, n, dir));
     if (hit) return true;
   }
   return norm(dir) < 1e-12f;
@@ -421,11 +452,10 @@ DEV bool epa_face(const SVx* V, EFace& f, int a, int b, int c) {
 DEV bool epa(const Geom& A, const Geom& B, SVx* V, int nv, V3& nrm, float& depth, V3& pa, V3& pb, EFace* F,
              int (*edges)[2]) {
   int nf = 0;
-  const V3 dirs[6] = {V3{1.f, 0.f, 0.f}, V3{-1.f, 0.f, 0.f}, V3{0.f, 1.f, 0.f},
-                      V3{0.f, -1.f, 0.f}, V3{0.f, 0.f, 1.f}, V3{0.f, 0.f, -1.f}};
   if (nv == 1) {
-    for (int k = 0; k < 6 && nv < 2; k++) {
-      V[nv] = mk_sv(A, B, dirs[k]);
+    for (int k = 0; k < 6 && nv < 2; k++) {  // +x, -x, +y, -y, +z, -z
+      const float sg = (k & 1) ? -1.f : 1.f;
+      V[nv] = mk_sv(A, B, V3{k < 2 ? sg : 0.f, (k >> 1) == 1 ? sg : 0.f, k >= 4 ? sg : 0.f});
       if (norm(V[nv].w - V[0].w) > 1e-7f) nv++;
     }
   }
@@ -518,15 +548,16 @@ DEV bool epa(const Geom& A, const Geom& B, SVx* V, int nv, V3& nrm, float& depth
 // scr: EPA_SCRATCH_FLOATS of LDS; emits at most one contact (lane 0)
 template <class Sink>
 DEV void convex_convex(Sink& cs, const Geom& A, const Geom& B, float* scr) {
-  SVx S[4];
+  SVx s0, s1, s2, s3;
   int n = 0;
-  if (!gjk(A, B, S, n)) return;
+  if (!gjk(A, B, s0, s1, s2, s3, n)) return;
   SVx* V = reinterpret_cast<SVx*>(scr);
   EFace* F = reinterpret_cast<EFace*>(scr + 9 * EPA_MAXV);
   int(*edges)[2] = reinterpret_cast<int(*)[2]>(scr + 9 * EPA_MAXV + 7 * EPA_MAXF);
-#pragma unroll
-  for (int k = 0; k < 4; k++)
-    if (k < n) V[k] = S[k];
+  V[0] = s0;
+  if (n > 1) V[1] = s1;
+  if (n > 2) V[2] = s2;
+  if (n > 3) V[3] = s3;
   V3 nrm, pa, pb;
   float depth;
   if (!epa(A, B, V, n, nrm, depth, pa, pb, F, edges)) return;

@@ -2163,10 +2163,11 @@ __device__ __attribute__((noinline)) void substep(int max_iter, float tol) {
 // The whole PickPlaceGymEnv.step in ONE launch per env step (product path): the 16 substeps
 // loop inside the workgroup, so per-env cost variation averages out over the step instead of
 // stretching 16 separate launch tails (measured: one launch per substep ran 40 % slower).
-extern "C" __global__ void __launch_bounds__(WG) mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert) {
+extern "C" __global__ void __launch_bounds__(WG) mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert,
+                                                                     int base) {
   EnvSh& E = g_E;
   __shared__ float act[12];
-  const int i = blockIdx.x;
+  const int i = base + blockIdx.x;
   if (i >= S.N) return;
   load_env(S, i, E);
   if (LANE == 0) {
@@ -2230,8 +2231,11 @@ extern "C" hipError_t mmx_launch_reset(const MMXState* S, const unsigned char* m
   hipLaunchKernelGGL(mmx_reset_kernel, dim3(S->N), dim3(WG), 0, st, *S, mask, task);
   return hipGetLastError();
 }
-extern "C" hipError_t mmx_launch_step(const MMXState* S, const float* action, int adim, int expert, hipStream_t st) {
-  hipLaunchKernelGGL(mmx_env_step_kernel, dim3(S->N), dim3(WG), 0, st, *S, action, adim, expert);
+// envs [base, base+count): independent env ranges may run on separate streams
+extern "C" hipError_t mmx_launch_step(const MMXState* S, const float* action, int adim, int expert, int base,
+                                      int count, hipStream_t st) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mmx_env_step_kernel, dim3(count), dim3(WG), 0, st, *S, action, adim, expert, base);
   return hipGetLastError();
 }
 extern "C" hipError_t mmx_launch_expert(const MMXState* S, int n, float* action, hipStream_t st) {

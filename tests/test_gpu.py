@@ -246,6 +246,32 @@ def test_determinism_and_shard_independence():
     np.testing.assert_array_equal(outs[0][4:], outs[2])  # result independent of batch composition
 
 
+def test_rollout_lanes_bit_identical(monkeypatch):
+    """Concurrent env ranges on separate streams (mmx_rollout_lanes) change nothing but timing."""
+    import oracle_py as O
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    seeds = [O.episode_seed(3, i) for i in range(10)]
+    outs = []
+    for lanes in ("1", "3"):  # 3 lanes over 10 envs: ragged ranges 3/3/4
+        monkeypatch.setenv("MMX_STREAMS", lanes)
+        env = PickPlaceVecEnv(10, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
+                              autoreset=True)
+        assert env.sim.rollout_lanes == int(lanes)
+        env.reset(seed=seeds)
+        env.rollout_expert(40)
+        torch.cuda.synchronize()
+        q, v, _, _ = env.sim.get_state()
+        outs.append(np.concatenate([q, v, env.sim.view("episode_i", _lib_epi_n(), "<i4").cpu().numpy()], 1))
+    np.testing.assert_array_equal(outs[0], outs[1])
+
+
+def _lib_epi_n():
+    from mujoco_manip_amd import _lib
+
+    return _lib.EPI_N
+
+
 def test_autoreset_and_truncation():
     from mujoco_manip_amd.vec_env import PickPlaceVecEnv
 
