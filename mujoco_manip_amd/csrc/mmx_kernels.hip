@@ -1336,6 +1336,9 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
     const float pj = chol_solve_arrow(E, hrow, -g, cpl);
     if (LANE < 27) E.p[LANE] = pj;
     SYNC();
+    float hp = 0.f;  // (H p)_lane: the gradient's change per unit step while no row changes state
+#pragma unroll
+    for (int m = 0; m < 27; m++) hp = fmaf(hrow[m], E.p[m], hp);
     PROBE(1, stats, STAT_T_AUX2);
     // exact line search on phi(a) = cost(x + a p): phi' is piecewise linear and increasing
 #pragma unroll
@@ -1385,13 +1388,29 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
       stepn = alpha * alpha * pj * pj;
     }
     mdx = fmaf(alpha, mp, mdx);
+    bool flip = false;  // a row changed active state over the step
 #pragma unroll
-    for (int q = 0; q < RPL; q++) rr[q] = fmaf(alpha, jp[q], rr[q]);
+    for (int q = 0; q < RPL; q++) {
+      const float v = fmaf(alpha, jp[q], rr[q]);
+      flip |= !eq[q] && ((v < 0.f) != (rr[q] < 0.f));
+      rr[q] = v;
+    }
     SYNC();
     stepn = sqrtf(wave_sum(stepn));
     if (stepn < 1e-9f) {
       it++;
       break;
+    }
+    if (__ballot(flip) == 0ull) {
+      // same active set: H is unchanged, so g(x + a p) = g + a H p exactly; when that already
+      // meets the tolerance the confirming Hessian pass is skipped
+      const float gn = LANE < 27 ? fmaf(alpha, hp, g) : 0.f;
+      const float rn = sqrtf(wave_sum(gn * gn)) / scale;
+      if (rn < tol) {
+        resid = rn;
+        it++;
+        break;
+      }
     }
   }
   SYNC();
