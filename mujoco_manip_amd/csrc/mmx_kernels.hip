@@ -1962,41 +1962,57 @@ DEV float reward_lane0(const MMXState& S, int i, const EnvSh& E, bool robot_obst
 
 // FSM expert plan(n) (pick_and_place.py:167-277) -> abs_pos action (generate_dataset.py:142-148).
 // ee / object positions come from the last position stage (consistent after mj_forward).
+// PickAndPlaceTask.plan(n) (pick_and_place.py:167-277) in branch-free form: every transition
+// condition is evaluated, then each FSM field takes its new value through selects.  (Two
+// switch-statement forms of this function, called from one-lane-per-env divergent code, were
+// miscompiled: the LOWER_TO_BIN target's z and then the emitted action's z came out wrong.)
 DEV void expert_plan(const MMXState& S, int i, V3 o, V3 ee, int n, float* act4) {
-  int st = EPI(EPI_FSM_STATE), ti = EPI(EPI_FSM_TASKIDX), settle = EPI(EPI_FSM_SETTLE);
-  int grip = EPI(EPI_FSM_GRIP), has = EPI(EPI_FSM_HASTGT);
-  V3 t = V3{EPF(EPF_FSM_TARGET), EPF(EPF_FSM_TARGET + 1), EPF(EPF_FSM_TARGET + 2)};
-  V3 te = V3{EPF(EPF_FSM_TRANSIT), EPF(EPF_FSM_TRANSIT + 1), EPF(EPF_FSM_TRANSIT + 2)};
+  const int s = EPI(EPI_FSM_STATE), ti = EPI(EPI_FSM_TASKIDX), settle = EPI(EPI_FSM_SETTLE);
+  const int grip = EPI(EPI_FSM_GRIP), has = EPI(EPI_FSM_HASTGT);
+  const V3 t = V3{EPF(EPF_FSM_TARGET), EPF(EPF_FSM_TARGET + 1), EPF(EPF_FSM_TARGET + 2)};
+  const V3 te = V3{EPF(EPF_FSM_TRANSIT), EPF(EPF_FSM_TRANSIT + 1), EPF(EPF_FSM_TRANSIT + 2)};
   const V3 b = bin_pos(EPI(EPI_BIN));
-  auto reached = [&](V3 p) { return norm(ee - p) < 0.02f; };  // controller.py:139-145
-  switch (st) {
-    case 0:
-      if (ti >= 1) { st = 10; break; }
-      grip = 1; t = V3{o.x, o.y, 0.44f}; has = 1; st = 1; break;
-    case 1: if (reached(t)) { t = V3{o.x, o.y, 0.36f}; st = 2; } break;
-    case 2: if (reached(t)) { grip = 0; settle = 150; st = 3; } break;
-    case 3: settle -= n; if (settle <= 0) { t = V3{o.x, o.y, 0.55f}; st = 4; } break;
-    case 4: if (reached(t)) { te = V3{b.x, b.y, 0.55f}; st = 5; } break;
-    case 5: {
-      const V3 diff = te - t;
-      const float dist = norm(diff), step = 0.001f * n;
-      if (dist > step) t = t + diff * (step / dist);
-      else t = te;
-      if (dist <= 0.02f) { settle = 100; st = 6; }
-      break;
-    }
-    case 6: settle -= n; if (settle <= 0) { t = V3{b.x, b.y, 0.45f}; st = 7; } break;
-    case 7: if (reached(t)) { grip = 1; settle = 150; st = 8; } break;
-    case 8: settle -= n; if (settle <= 0) { t = V3{0.f, 0.3f, 0.55f}; st = 9; } break;
-    case 9: if (reached(t)) { ti += 1; st = 0; } break;
-    default: break;
+  const bool r = norm(ee - t) < 0.02f;  // controller.reached (controller.py:139-145)
+  const int sn = settle - n;
+  const bool idle_done = s == 0 && ti >= 1;  // single-task FSM: one pick and place, then DONE
+  const bool go1 = s == 0 && ti < 1;          // IDLE -> PRE_GRASP
+  const bool go2 = s == 1 && r;               // PRE_GRASP -> GRASP
+  const bool go3 = s == 2 && r;               // GRASP -> CLOSE_GRIPPER
+  const bool go4 = s == 3 && sn <= 0;         // CLOSE_GRIPPER -> LIFT
+  const bool go5 = s == 4 && r;               // LIFT -> MOVE_TO_BIN
+  const V3 diff = te - t;                     // MOVE_TO_BIN: advance 0.001 n toward the transit end
+  const float dist = norm(diff), step = 0.001f * n;
+  const V3 tmove = dist > step ? t + diff * (step / dist) : te;
+  const bool go6 = s == 5 && dist <= 0.02f;   // (pre-move distance) -> SETTLE_AT_BIN
+  const bool go7 = s == 6 && sn <= 0;         // SETTLE_AT_BIN -> LOWER_TO_BIN
+  const bool go8 = s == 7 && r;               // LOWER_TO_BIN -> RELEASE
+  const bool go9 = s == 8 && sn <= 0;         // RELEASE -> RETREAT
+  const bool go0 = s == 9 && r;               // RETREAT -> IDLE (next task)
+  float tx = t.x, ty = t.y, tz = t.z;
+  tx = go1 || go2 || go4 ? o.x : tx;
+  ty = go1 || go2 || go4 ? o.y : ty;
+  tz = go1 ? 0.44f : (go2 ? 0.36f : (go4 ? 0.55f : tz));
+  tx = s == 5 ? tmove.x : tx;
+  ty = s == 5 ? tmove.y : ty;
+  tz = s == 5 ? tmove.z : tz;
+  tx = go7 ? b.x : (go9 ? 0.f : tx);
+  ty = go7 ? b.y : (go9 ? 0.3f : ty);
+  tz = go7 ? 0.45f : (go9 ? 0.55f : tz);
+  const int ns = idle_done ? 10 : go1 ? 1 : go2 ? 2 : go3 ? 3 : go4 ? 4 : go5 ? 5 : go6 ? 6 : go7 ? 7
+               : go8 ? 8 : go9 ? 9 : go0 ? 0 : s;
+  int nset = (s == 3 || s == 6 || s == 8) ? sn : settle;
+  nset = go3 || go8 ? 150 : (go6 ? 100 : nset);
+  const int ng = go1 || go8 ? 1 : (go3 ? 0 : grip);
+  const int nhas = go1 ? 1 : has;
+  EPI(EPI_FSM_STATE) = ns; EPI(EPI_FSM_TASKIDX) = go0 ? ti + 1 : ti; EPI(EPI_FSM_SETTLE) = nset;
+  EPI(EPI_FSM_GRIP) = ng; EPI(EPI_FSM_HASTGT) = nhas;
+  EPF(EPF_FSM_TARGET) = tx; EPF(EPF_FSM_TARGET + 1) = ty; EPF(EPF_FSM_TARGET + 2) = tz;
+  if (go5) {
+    EPF(EPF_FSM_TRANSIT) = b.x; EPF(EPF_FSM_TRANSIT + 1) = b.y; EPF(EPF_FSM_TRANSIT + 2) = 0.55f;
   }
-  EPI(EPI_FSM_STATE) = st; EPI(EPI_FSM_TASKIDX) = ti; EPI(EPI_FSM_SETTLE) = settle;
-  EPI(EPI_FSM_GRIP) = grip; EPI(EPI_FSM_HASTGT) = has;
-  EPF(EPF_FSM_TARGET) = t.x; EPF(EPF_FSM_TARGET + 1) = t.y; EPF(EPF_FSM_TARGET + 2) = t.z;
-  EPF(EPF_FSM_TRANSIT) = te.x; EPF(EPF_FSM_TRANSIT + 1) = te.y; EPF(EPF_FSM_TRANSIT + 2) = te.z;
-  const V3 tgt = has ? t : ee;  // before the first plan the reference has no target
-  act4[0] = tgt.x; act4[1] = tgt.y; act4[2] = tgt.z; act4[3] = grip ? 1.f : 0.f;
+  // before the first plan the reference has no target and commands the current EE position
+  act4[0] = nhas ? tx : ee.x; act4[1] = nhas ? ty : ee.y; act4[2] = nhas ? tz : ee.z;
+  act4[3] = ng ? 1.f : 0.f;
 }
 
 // decode_action (gym_env.py:252-281) + gripper command (gym_env.py:550-553)

@@ -1,0 +1,504 @@
+"""Batched expert-demonstration dataset emission.
+
+Mirrors `scripts/generate_dataset.py` of the reference (run_episode :83-198, main :201-333,
+feature schema `mujoco_manip/features.py:10-106`), with the episodes run side by side on the
+MI355X instead of one after another:
+
+* every slot of a `PickPlaceVecEnv` runs one episode: `plan(ACTION_REPEAT)` on device, the frame
+  is built from the PRE-step observation plus the FSM's commanded target in four SE(3)
+  encodings, then `step(abs_pos action)`; the staged reward components of the step land in
+  `next.reward` (reference :140-196);
+* an episode ends when its FSM reaches DONE (terminated / truncated are ignored, as in the
+  reference loop); the slot is then re-reset with the next episode's seed and task
+  (episode e: task `task_list[e % len(task_list)]`, seed `SeedSequence(seed).spawn(E)[e]`
+  when `randomize_objects`, reference :267-277);
+* frames are gathered on device, copied to the host once, and written in the LeRobot v3.0
+  on-disk layout (parquet data files, `meta/info.json`, `meta/tasks.parquet`,
+  `meta/episodes/...parquet`, `meta/stats.json`) plus the reference's `metadata.json`
+  (generation config + `episode_seeds`, :306-319).
+
+Camera images need the batched renderer, which this build does not have yet:
+the two image features are rejected with a ValueError rather than silently dropped.
+LeRobot itself is not importable here, so the on-disk layout follows LeRobot v3.0's documented
+format without a round-trip check against the library ("format unpinned"); the frame VALUES are
+pinned against the oracle running the reference loop (tests/test_dataset.py).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from .constants import ACTION_REPEAT, BINS, CONTROL_FPS, OBJECTS, OBS_SLICES, TASK_SETS
+
+# features.py:10-106 (IMAGE_SIZE = 224)
+FEATURES = {
+    "observation.images.overhead": {"dtype": "image", "shape": (224, 224, 3), "names": ["height", "width", "channels"]},
+    "observation.images.wrist": {"dtype": "image", "shape": (224, 224, 3), "names": ["height", "width", "channels"]},
+    "observation.state": {"dtype": "float32", "shape": (11,), "names": None},
+    "observation.state.ee.pos_quat_g": {"dtype": "float32", "shape": (8,), "names": None},
+    "observation.state.ee.pos_rot6d_g": {"dtype": "float32", "shape": (10,), "names": None},
+    "observation.state.ee.pos_quat_g_rel": {"dtype": "float32", "shape": (8,), "names": None},
+    "observation.state.ee.pos_rot6d_g_rel": {"dtype": "float32", "shape": (10,), "names": None},
+    "action.ee.pos_quat_g": {"dtype": "float32", "shape": (8,), "names": None},
+    "action.ee.pos_rot6d_g": {"dtype": "float32", "shape": (10,), "names": None},
+    "action.ee.pos_quat_g_rel": {"dtype": "float32", "shape": (8,), "names": None},
+    "action.ee.pos_rot6d_g_rel": {"dtype": "float32", "shape": (10,), "names": None},
+    "observation.target_bin_onehot": {"dtype": "float32", "shape": (3,), "names": None},
+    "observation.target_obj_onehot": {"dtype": "float32", "shape": (3,), "names": None},
+    "observation.keypoints_overhead": {"dtype": "float32", "shape": (14,), "names": None},
+    "observation.keypoints_wrist": {"dtype": "float32", "shape": (14,), "names": None},
+    "observation.target_obj_keypoints_overhead": {"dtype": "float32", "shape": (2,), "names": None},
+    "observation.target_bin_keypoints_overhead": {"dtype": "float32", "shape": (2,), "names": None},
+    "observation.phase_description": {"dtype": "string", "shape": (1,), "names": None},
+    "next.reward": {"dtype": "float32", "shape": (6,), "names": None},
+}
+
+# generate_dataset.py:26-38 (+ the flattened keypoints :158-168)
+OBS_TO_FEATURE = {
+    "state": "observation.state",
+    "state.ee.pos_quat_g": "observation.state.ee.pos_quat_g",
+    "state.ee.pos_rot6d_g": "observation.state.ee.pos_rot6d_g",
+    "state.ee.pos_quat_g_rel": "observation.state.ee.pos_quat_g_rel",
+    "state.ee.pos_rot6d_g_rel": "observation.state.ee.pos_rot6d_g_rel",
+    "target_bin_onehot": "observation.target_bin_onehot",
+    "target_obj_onehot": "observation.target_obj_onehot",
+    "target_obj_keypoints_overhead": "observation.target_obj_keypoints_overhead",
+    "target_bin_keypoints_overhead": "observation.target_bin_keypoints_overhead",
+    "keypoints_overhead": "observation.keypoints_overhead",
+    "keypoints_wrist": "observation.keypoints_wrist",
+}
+ACTION_KEYS = ("action.ee.pos_quat_g", "action.ee.pos_rot6d_g", "action.ee.pos_quat_g_rel", "action.ee.pos_rot6d_g_rel")
+IMAGE_KEYS = ("observation.images.overhead", "observation.images.wrist")
+
+# pick_and_place.py:12-49 (State order = device FSM codes 0..10) and :128-149
+_STATE_PHASE = ["idle", "approaching", "grasping", "grasping", "lifting", "transporting", "transporting",
+                "placing", "placing", "retreating", "done"]
+FSM_DONE = 10
+
+# controller.py TARGET_ORI: the FSM's commanded hand orientation
+TARGET_ORI = np.array([[0.0, 1.0, 0.0], [1.0, 0.0, 0.0], [0.0, 0.0, -1.0]])
+
+
+def make_task_string(obj_name: str, bin_name: str) -> str:
+    """generate_dataset.py:41-54."""
+    return f"Pick {obj_name.replace('obj_', '')} object and place in {bin_name.replace('bin_', '')} bin"
+
+
+def phase_description(state: int, obj_name: str, bin_name: str) -> str:
+    """PickAndPlaceTask.phase_description (pick_and_place.py:128-149) for a device FSM code."""
+    phase = _STATE_PHASE[int(state)]
+    if phase in ("idle", "done"):
+        return "idle"
+    if phase == "retreating":
+        return "retreating to neutral position"
+    o, b = obj_name.replace("obj_", ""), bin_name.replace("bin_", "")
+    return {"approaching": f"approaching the {o} cube", "grasping": f"grasping the {o} cube",
+            "lifting": f"lifting the {o} cube", "transporting": f"transporting the {o} cube to the {b} bin",
+            "placing": f"placing the {o} cube in the {b} bin"}[phase]
+
+
+# ----------------------------------------------------------------------------- action encodings
+def _quat_xyzw_t(R):
+    """rotmat_to_quat_xyzw (pose_utils.py:48-82) on a batch [n, 3, 3], branch for branch."""
+    import torch
+
+    r00, r11, r22 = R[:, 0, 0], R[:, 1, 1], R[:, 2, 2]
+    tr = r00 + r11 + r22
+    one = torch.ones_like(tr)
+
+    def safe_s(v):
+        return 2.0 * torch.sqrt(torch.clamp(v, min=0.0) + 0.0) + (v <= 0).to(v.dtype) * 1.0  # never 0 in unused lanes
+
+    s0 = safe_s(tr + 1.0)
+    q0 = torch.stack([(R[:, 2, 1] - R[:, 1, 2]) / s0, (R[:, 0, 2] - R[:, 2, 0]) / s0, (R[:, 1, 0] - R[:, 0, 1]) / s0,
+                      0.25 * s0], 1)
+    s1 = safe_s(one + r00 - r11 - r22)
+    q1 = torch.stack([0.25 * s1, (R[:, 0, 1] + R[:, 1, 0]) / s1, (R[:, 0, 2] + R[:, 2, 0]) / s1,
+                      (R[:, 2, 1] - R[:, 1, 2]) / s1], 1)
+    s2 = safe_s(one + r11 - r00 - r22)
+    q2 = torch.stack([(R[:, 0, 1] + R[:, 1, 0]) / s2, 0.25 * s2, (R[:, 1, 2] + R[:, 2, 1]) / s2,
+                      (R[:, 0, 2] - R[:, 2, 0]) / s2], 1)
+    s3 = safe_s(one + r22 - r00 - r11)
+    q3 = torch.stack([(R[:, 0, 2] + R[:, 2, 0]) / s3, (R[:, 1, 2] + R[:, 2, 1]) / s3, 0.25 * s3,
+                      (R[:, 1, 0] - R[:, 0, 1]) / s3], 1)
+    b0 = (tr > 0)[:, None]
+    b1 = ((r00 > r11) & (r00 > r22))[:, None]
+    b2 = (r11 > r22)[:, None]
+    return torch.where(b0, q0, torch.where(b1, q1, torch.where(b2, q2, q3)))
+
+
+def encode_actions(target, gripper, T_init):
+    """get_actions (generate_dataset.py:57-80) batched on device.
+
+    target [n, 3], gripper [n], T_init [n, 4, 4] -> the four float32 encodings of the commanded
+    SE(3) (absolute and relative to T_init), computed in float64 like the reference's numpy.
+    """
+    import torch
+
+    dev = target.device
+    n = target.shape[0]
+    t = target.to(torch.float64)
+    g = gripper.to(torch.float64)[:, None]
+    Ti = T_init.to(torch.float64)
+    Rt = torch.as_tensor(TARGET_ORI, dtype=torch.float64, device=dev).expand(n, 3, 3)
+    # inv(T_init) @ T_target for a rigid transform: R' = Ri^T Rt, p' = Ri^T (t - pi)
+    RiT = Ti[:, :3, :3].transpose(1, 2)
+    Rr = RiT @ Rt
+    pr = (RiT @ (t - Ti[:, :3, 3])[:, :, None])[:, :, 0]
+    qa = _quat_xyzw_t(Rt)
+    qr = _quat_xyzw_t(Rr)
+    out = {
+        "action.ee.pos_quat_g": torch.cat([t, qa, g], 1),
+        "action.ee.pos_rot6d_g": torch.cat([t, Rt[:, :2, :].reshape(n, 6), g], 1),
+        "action.ee.pos_quat_g_rel": torch.cat([pr, qr, g], 1),
+        "action.ee.pos_rot6d_g_rel": torch.cat([pr, Rr[:, :2, :].reshape(n, 6), g], 1),
+    }
+    return {k: v.to(torch.float32) for k, v in out.items()}
+
+
+# ----------------------------------------------------------------------------- batched collection
+@dataclass
+class Episode:
+    index: int
+    obj: str
+    bin: str
+    seed: int | None
+    frames: dict = field(default_factory=dict)  # feature -> np.ndarray [T, ...] (strings: list)
+    length: int = 0
+
+
+def resolve_tasks(task=None, tasks="all"):
+    """generate_dataset.py:205-216 (same ValueErrors)."""
+    if task is not None:
+        pair = tuple(task)
+        if len(pair) != 2:
+            raise ValueError(f"task must be [obj, bin], got {pair}")
+        return [pair]
+    if tasks in TASK_SETS:
+        return TASK_SETS[tasks]
+    raise ValueError(f"Unknown task set '{tasks}'. Choose from: {list(TASK_SETS.keys())}")
+
+
+def resolve_features(features=None, reward_type="staged"):
+    """generate_dataset.py:218-230: subset selection, unknown keys -> ValueError,
+    next.reward only with the staged reward."""
+    feats = dict(FEATURES)
+    if features is not None:
+        requested = list(features)
+        unknown = [k for k in requested if k not in FEATURES]
+        if unknown:
+            raise ValueError(f"Unknown feature keys: {unknown}. Valid keys: {list(FEATURES.keys())}")
+        feats = {k: FEATURES[k] for k in requested}
+    if reward_type != "staged":
+        feats.pop("next.reward", None)
+    imgs = [k for k in feats if k in IMAGE_KEYS]
+    if imgs:
+        raise ValueError(f"image features {imgs} need the batched camera renderer (SURVEY §8 f1), "
+                         "which this build does not provide yet; request the numeric features only")
+    return feats
+
+
+def episode_seeds(seed: int, num_episodes: int) -> list[int]:
+    """generate_dataset.py:263-268: SeedSequence(seed).spawn(E)[e].generate_state(1)[0]."""
+    from . import _lib
+
+    return [_lib.episode_seed(seed, e) for e in range(num_episodes)]
+
+
+def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type="staged", randomize_objects=False,
+                     seed=0, spawn_x_range=(-0.20, 0.20), spawn_y_range=(0.30, 0.45), num_envs=1024, device=0,
+                     max_gym_steps=5000):
+    """Run `num_episodes` reference run_episode loops (generate_dataset.py:83-198) side by side.
+
+    Returns (episodes, seeds): a list of Episode with per-feature frame arrays in step order.
+    """
+    import torch
+
+    from .vec_env import PickPlaceVecEnv
+
+    E = int(num_episodes)
+    seeds = episode_seeds(seed, E) if randomize_objects else None
+    N = max(1, min(int(num_envs), E))
+    env = PickPlaceVecEnv(N, tasks=[tuple(t) for t in task_list], action_mode="abs_pos", reward_type=reward_type,
+                          randomize_objects=randomize_objects, spawn_x_range=tuple(spawn_x_range),
+                          spawn_y_range=tuple(spawn_y_range), autoreset=False, device=device)
+    dev = env.device
+    need_actions = bool(set(feature_keys) & set(ACTION_KEYS))
+    need_reward = "next.reward" in feature_keys and reward_type == "staged"
+    obs_feats = [(k, f) for k, f in OBS_TO_FEATURE.items() if f in feature_keys]
+
+    eps = [Episode(e, *task_list[e % len(task_list)], seeds[e] if seeds else None) for e in range(E)]
+    slot_ep = np.full(N, -1, np.int64)
+    next_ep = 0
+
+    def assign(slots):
+        nonlocal next_ep
+        mask = np.zeros(N, np.uint8)
+        sd = [None] * N
+        task = np.full(N, -1, np.int32)
+        for s in slots:
+            if next_ep >= E:
+                slot_ep[s] = -1
+                continue
+            ep = eps[next_ep]
+            slot_ep[s] = next_ep
+            next_ep += 1
+            mask[s] = 1
+            sd[s] = ep.seed
+            task[s] = (OBJECTS.index(ep.obj) << 4) | BINS.index(ep.bin)
+        if mask.any():
+            env.sim.reset(seeds=sd if seeds else None, task_override=task, env_mask=mask)
+
+    assign(range(N))
+    rec = []  # per step: (slots [k], ep ids [k], dict feature -> device tensor [k, ...], fsm [k])
+    steps = 0
+    fsm_view = env._epi[:, 4]
+    while (slot_ep >= 0).any():
+        if steps >= max_gym_steps:
+            raise RuntimeError(f"episodes {sorted(set(slot_ep[slot_ep >= 0].tolist()))} did not finish "
+                               f"within {max_gym_steps} gym steps")
+        done_before = (fsm_view == FSM_DONE).cpu().numpy()
+        finished = np.where((slot_ep >= 0) & done_before)[0]
+        if len(finished):
+            for s in finished:
+                slot_ep[s] = -1
+            assign(finished)
+            done_before = (fsm_view == FSM_DONE).cpu().numpy()
+        act_slots = np.where((slot_ep >= 0) & ~done_before)[0]
+        if len(act_slots) == 0:
+            continue
+        idx = torch.as_tensor(act_slots, device=dev)
+        obs_pre = env._obs.index_select(0, idx)  # PRE-step obs (from the reset or the previous step)
+        action = env.expert_plan(ACTION_REPEAT)  # fsm.plan(16) -> (target, gripper) for every slot
+        frame = {}
+        for k, f in obs_feats:
+            a, b, _ = OBS_SLICES[k]
+            frame[f] = obs_pre[:, a:b]
+        a_sel = action.index_select(0, idx)
+        if need_actions:
+            T = env.initial_ee_se3.index_select(0, idx)
+            enc = encode_actions(a_sel[:, :3], a_sel[:, 3], T)
+            for k in ACTION_KEYS:
+                if k in feature_keys:
+                    frame[k] = enc[k]
+        fsm_after = fsm_view.index_select(0, idx).clone()
+        env.step(action)
+        if need_reward:
+            frame["next.reward"] = env._rc.index_select(0, idx).clone()
+        rec.append((act_slots, slot_ep[act_slots].copy(), frame, fsm_after))
+        steps += 1
+    torch.cuda.synchronize(dev)
+
+    # host side: split the step records into per-episode frame arrays (step order is frame order)
+    per_ep_rows = [[] for _ in range(E)]
+    host = []
+    for r, (slots, ep_ids, frame, fsm) in enumerate(rec):
+        hf = {k: v.cpu().numpy() for k, v in frame.items()}
+        host.append((hf, fsm.cpu().numpy()))
+        for j, e in enumerate(ep_ids):
+            per_ep_rows[e].append((r, j))
+    for e, rows in enumerate(per_ep_rows):
+        ep = eps[e]
+        ep.length = len(rows)
+        for k in feature_keys:
+            if k == "observation.phase_description":
+                ep.frames[k] = [phase_description(host[r][1][j], ep.obj, ep.bin) for r, j in rows]
+            elif host and k in host[0][0]:
+                ep.frames[k] = np.stack([host[r][0][k][j] for r, j in rows]).astype(np.float32)
+    env.close()
+    return eps, seeds
+
+
+# ----------------------------------------------------------------------------- LeRobot v3.0 writer
+def _feature_stats(x: np.ndarray) -> dict:
+    x = x.reshape(len(x), -1).astype(np.float64)
+    return {"min": x.min(0).tolist(), "max": x.max(0).tolist(), "mean": x.mean(0).tolist(),
+            "std": x.std(0).tolist(), "count": [int(len(x))]}
+
+
+def write_lerobot_v3(root: str, repo_id: str, episodes, features: dict, *, fps=CONTROL_FPS,
+                     robot_type="franka_panda", chunks_size=1000, data_files_size_in_mb=100, extra_info=None):
+    """Write episodes in the LeRobot v3.0 layout (use_videos=False, no image features).
+
+    data/chunk-XXX/file-YYY.parquet  frames of consecutive episodes (features + timestamp,
+                                     frame_index, episode_index, index, task_index)
+    meta/info.json, meta/tasks.parquet, meta/episodes/chunk-000/file-000.parquet, meta/stats.json
+    """
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+
+    os.makedirs(root, exist_ok=True)
+    tasks = []
+    for ep in episodes:
+        t = make_task_string(ep.obj, ep.bin)
+        if t not in tasks:
+            tasks.append(t)
+    task_idx = {t: i for i, t in enumerate(tasks)}
+    num_keys = [k for k, f in features.items() if f["dtype"] == "float32"]
+    str_keys = [k for k, f in features.items() if f["dtype"] == "string"]
+
+    def ep_table(ep, start):
+        n = ep.length
+        cols, fields = {}, []
+        for k in num_keys:
+            dim = int(np.prod(features[k]["shape"]))
+            arr = np.asarray(ep.frames[k], np.float32).reshape(n, dim)
+            cols[k] = pa.FixedSizeListArray.from_arrays(pa.array(arr.ravel(), pa.float32()), dim)
+            fields.append(pa.field(k, pa.list_(pa.float32(), dim)))
+        for k in str_keys:
+            cols[k] = pa.array(list(ep.frames[k]), pa.string())
+            fields.append(pa.field(k, pa.string()))
+        fi = np.arange(n, dtype=np.int64)
+        extra = {"timestamp": pa.array((fi / fps).astype(np.float32)), "frame_index": pa.array(fi),
+                 "episode_index": pa.array(np.full(n, ep.index, np.int64)), "index": pa.array(start + fi),
+                 "task_index": pa.array(np.full(n, task_idx[make_task_string(ep.obj, ep.bin)], np.int64))}
+        for k, v in extra.items():
+            cols[k] = v
+            fields.append(pa.field(k, v.type))
+        return pa.Table.from_arrays([cols[f.name] for f in fields], schema=pa.schema(fields))
+
+    limit = data_files_size_in_mb * 1024 * 1024
+    ep_rows = []
+    chunk, fileno, cur, cur_bytes, start = 0, 0, [], 0, 0
+
+    def flush():
+        nonlocal chunk, fileno, cur, cur_bytes
+        if not cur:
+            return
+        d = os.path.join(root, "data", f"chunk-{chunk:03d}")
+        os.makedirs(d, exist_ok=True)
+        pq.write_table(pa.concat_tables(cur), os.path.join(d, f"file-{fileno:03d}.parquet"))
+        fileno += 1
+        if fileno >= chunks_size:
+            chunk, fileno = chunk + 1, 0
+        cur, cur_bytes = [], 0
+
+    for ep in sorted(episodes, key=lambda e: e.index):
+        tab = ep_table(ep, start)
+        if cur and cur_bytes + tab.nbytes > limit:
+            flush()
+        row = {"episode_index": ep.index, "tasks": [make_task_string(ep.obj, ep.bin)], "length": ep.length,
+               "data/chunk_index": chunk, "data/file_index": fileno, "dataset_from_index": start,
+               "dataset_to_index": start + ep.length, "meta/episodes/chunk_index": 0,
+               "meta/episodes/file_index": 0}
+        for k in num_keys:
+            for s, v in _feature_stats(np.asarray(ep.frames[k])).items():
+                row[f"stats/{k}/{s}"] = v
+        ep_rows.append(row)
+        cur.append(tab)
+        cur_bytes += tab.nbytes
+        start += ep.length
+    flush()
+
+    meta = os.path.join(root, "meta")
+    os.makedirs(os.path.join(meta, "episodes", "chunk-000"), exist_ok=True)
+    pq.write_table(pa.Table.from_pylist(ep_rows), os.path.join(meta, "episodes", "chunk-000", "file-000.parquet"))
+    pq.write_table(pa.table({"task_index": pa.array(np.arange(len(tasks), dtype=np.int64)),
+                             "task": pa.array(tasks, pa.string())}), os.path.join(meta, "tasks.parquet"))
+    stats = {}
+    for k in num_keys:
+        allf = np.concatenate([np.asarray(ep.frames[k], np.float32).reshape(ep.length, -1) for ep in episodes])
+        stats[k] = _feature_stats(allf)
+    with open(os.path.join(meta, "stats.json"), "w") as f:
+        json.dump(stats, f, indent=1)
+    feats = {k: {"dtype": v["dtype"], "shape": list(v["shape"]), "names": v["names"]} for k, v in features.items()}
+    for k, dt in (("timestamp", "float32"), ("frame_index", "int64"), ("episode_index", "int64"),
+                  ("index", "int64"), ("task_index", "int64")):
+        feats[k] = {"dtype": dt, "shape": [1], "names": None}
+    info = {"codebase_version": "v3.0", "robot_type": robot_type, "total_episodes": len(episodes),
+            "total_frames": int(start), "total_tasks": len(tasks), "chunks_size": chunks_size,
+            "data_files_size_in_mb": data_files_size_in_mb, "video_files_size_in_mb": 500, "fps": fps,
+            "splits": {"train": f"0:{len(episodes)}"},
+            "data_path": "data/chunk-{chunk_index:03d}/file-{file_index:03d}.parquet", "video_path": None,
+            "features": feats}
+    if extra_info:
+        info.update(extra_info)
+    with open(os.path.join(meta, "info.json"), "w") as f:
+        json.dump(info, f, indent=4)
+    return info
+
+
+def read_lerobot_v3(root: str):
+    """Load the frames written by write_lerobot_v3 -> (info, metadata or None, {episode: {feature: array}})."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+
+    info = json.load(open(os.path.join(root, "meta", "info.json")))
+    md_path = os.path.join(root, "metadata.json")
+    metadata = json.load(open(md_path)) if os.path.exists(md_path) else None
+    eps_tab = pq.read_table(os.path.join(root, "meta", "episodes", "chunk-000", "file-000.parquet")).to_pylist()
+    out = {}
+    files = {}
+    for row in eps_tab:
+        key = (row["data/chunk_index"], row["data/file_index"])
+        if key not in files:
+            p = info["data_path"].format(chunk_index=key[0], file_index=key[1])
+            files[key] = pq.read_table(os.path.join(root, p))
+        tab = files[key]
+        epi = tab.column("episode_index").to_numpy()
+        sel = np.where(epi == row["episode_index"])[0]
+        fr = {}
+        for name in tab.column_names:
+            col = tab.column(name).take(sel).combine_chunks()
+            if pa.types.is_fixed_size_list(col.type):
+                fr[name] = np.asarray(col.flatten(), np.float32).reshape(len(sel), col.type.list_size)
+            elif pa.types.is_string(col.type):
+                fr[name] = col.to_pylist()
+            else:
+                fr[name] = col.to_numpy()
+        out[row["episode_index"]] = fr
+    return info, metadata, out
+
+
+# ----------------------------------------------------------------------------- entry point
+def generate(repo_id, num_episodes=100, root="./datasets", task=None, tasks="all", reward_type="staged",
+             randomize_objects=False, seed=0, spawn_x_range=(-0.20, 0.20), spawn_y_range=(0.30, 0.45),
+             features=None, num_envs=1024, device=0):
+    """generate_dataset.main (generate_dataset.py:201-333) with the episodes batched on the GPU."""
+    if not repo_id:
+        raise ValueError("repo_id is required (e.g. repo_id=user/pick-place)")
+    task_list = resolve_tasks(task, tasks)
+    feats = resolve_features(features, reward_type)
+    eps, seeds = collect_episodes(num_episodes, task_list, set(feats), reward_type=reward_type,
+                                  randomize_objects=randomize_objects, seed=seed, spawn_x_range=spawn_x_range,
+                                  spawn_y_range=spawn_y_range, num_envs=num_envs, device=device)
+    path = os.path.join(root, repo_id)
+    cfg = {"repo_id": repo_id, "num_episodes": int(num_episodes), "root": root,
+           "task": list(task) if task is not None else None, "tasks": tasks, "reward_type": reward_type,
+           "randomize_objects": bool(randomize_objects), "seed": int(seed), "spawn_x_range": list(spawn_x_range),
+           "spawn_y_range": list(spawn_y_range), "push_to_hub": False, "private": True,
+           "features": list(features) if features is not None else None}
+    if seeds is not None:
+        cfg["episode_seeds"] = [int(s) for s in seeds]
+    info = write_lerobot_v3(path, repo_id, eps, feats, extra_info={"generation_config": cfg})
+    with open(os.path.join(path, "metadata.json"), "w") as f:
+        json.dump(cfg, f, indent=2)
+    return path, info
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description="Generate a LeRobot v3.0 dataset from batched expert FSM episodes")
+    ap.add_argument("--repo-id", required=True)
+    ap.add_argument("--num-episodes", type=int, default=100)
+    ap.add_argument("--root", default="./datasets")
+    ap.add_argument("--task", nargs=2, default=None, metavar=("OBJ", "BIN"))
+    ap.add_argument("--tasks", default="all")
+    ap.add_argument("--reward-type", default="staged")
+    ap.add_argument("--randomize-objects", action="store_true")
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--spawn-x-range", type=float, nargs=2, default=(-0.20, 0.20))
+    ap.add_argument("--spawn-y-range", type=float, nargs=2, default=(0.30, 0.45))
+    ap.add_argument("--features", nargs="*", default=None)
+    ap.add_argument("--num-envs", type=int, default=1024)
+    a = ap.parse_args(argv)
+    path, info = generate(a.repo_id, a.num_episodes, a.root, a.task, a.tasks, a.reward_type, a.randomize_objects,
+                          a.seed, a.spawn_x_range, a.spawn_y_range, a.features, a.num_envs)
+    print(f"Dataset saved to {path}: {info['total_episodes']} episodes, {info['total_frames']} frames")
+
+
+if __name__ == "__main__":
+    main()

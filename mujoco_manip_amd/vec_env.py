@@ -150,7 +150,7 @@ class PickPlaceVecEnv:
         sub = max(s[3], 1.0)
         out = {"mean_nefc": s[0] / sub, "mean_ncon": s[1] / sub, "mean_solver_iter": s[2] / sub,
                "max_resid": float(self.stats[:, 4].max().item())}
-        # per-phase shader-clock cycles per substep per env (s_memtime ticks, 100 MHz on gfx950)
+        # per-phase shader-clock cycles per substep per env (s_memtime ticks = shader cycles)
         for k, name in enumerate(_lib.STAT_FIELDS[5:], start=5):
             out[name + "_per_substep"] = s[k] / sub
         return out

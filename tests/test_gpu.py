@@ -171,6 +171,41 @@ def test_expert_rollout_parity_and_completion():  # L2 + L3 (test_pick_and_place
     assert (env.env_error.cpu().numpy() == 0).all()
 
 
+def test_fsm_golden_traces_on_device(golden):  # pick_and_place.py:167-277, golden traces (single task)
+    from mujoco_manip_amd import _lib
+    from mujoco_manip_amd.constants import BINS, OBJECTS
+
+    names = ["IDLE", "PRE_GRASP", "GRASP", "CLOSE_GRIPPER", "LIFT", "MOVE_TO_BIN", "SETTLE_AT_BIN",
+             "LOWER_TO_BIN", "RELEASE", "RETREAT", "DONE"]
+    traces = [tr for tr in golden["fsm"] if len(tr["tasks"]) == 1]  # the gym FSM runs one task per episode
+    assert traces
+    for tr in traces:
+        o, b = tr["tasks"][0]
+        sim = _lib.Sim(1, action_mode="abs_pos", reward_type="staged",
+                       fixed_task=(OBJECTS.index(o), BINS.index(b)))
+        sim.reset()
+        kin = sim.view("kin", _lib.KIN_N)
+        qpos = sim.view("qpos", _lib.NQ)
+        epi = sim.view("episode_i", _lib.EPI_N, "<i4")
+        epf = sim.view("episode_f", _lib.EPF_N)
+        act = torch.zeros(1, 4, device="cuda")
+        for k, st in enumerate(tr["trace"]):
+            kin[0, 0:3] = torch.tensor(st["ee"], dtype=torch.float32)
+            for j, nm in enumerate(OBJECTS):
+                qpos[0, 9 + 7 * j:12 + 7 * j] = torch.tensor(st["objs"][nm], dtype=torch.float32)
+            sim.expert_plan(tr["n_steps"], act.data_ptr())
+            torch.cuda.synchronize()
+            e = epi[0].cpu().numpy()
+            assert names[e[4]] == st["state"], f"step {k}"
+            assert e[6] == st["settle"], f"step {k}"
+            assert float(e[7]) == st["gripper"], f"step {k}"
+            if st["target"] is not None:
+                np.testing.assert_allclose(epf[0, 21:24].cpu().numpy(), st["target"], atol=2e-6, err_msg=f"step {k}")
+                np.testing.assert_allclose(act[0, :3].cpu().numpy(), st["target"], atol=2e-6, err_msg=f"step {k}")
+            assert act[0, 3].item() == st["gripper"]
+        sim.close()
+
+
 def test_ik_convergence_kat():  # tests/test_controller.py:84-139 on the GPU batch
     from mujoco_manip_amd.vec_env import PickPlaceVecEnv
 
