@@ -107,6 +107,8 @@ def main():
     # rehearsal of the N > 1 path on a 1-GPU box: ranks share device 0 and talk over gloo
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"))
     ap.add_argument("--share-device", action="store_true")
+    # 0 = the C3 workload (no images); 128 = C5's two 128 x 128 RGB cameras per env step
+    ap.add_argument("--image-size", type=int, default=0)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -133,6 +135,7 @@ def main():
 
     N = args.envs_per_gpu
     env = PickPlaceVecEnv(N, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
+                          image_size=args.image_size,
                           autoreset=True, device=dev_index)
     seeds = [_lib.episode_seed(42, rank * N + i) for i in range(N)]
     env.reset(seed=seeds)
@@ -191,9 +194,12 @@ def main():
             "value": value, "unit": "env steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic (seeded randomized scenes, FSM-expert actions)",
-            "config": {"workload": "C3: PickPlaceGymEnv.step x 4096 envs/GPU, tasks=all, randomize_objects, "
-                                   "seed=42 episode seeds, staged reward, FSM expert abs_pos, autoreset",
-                       "envs_per_gpu": N, "global_envs": N * world, "substeps": 16,
+            "config": {"workload": ("C3: PickPlaceGymEnv.step x 4096 envs/GPU, tasks=all, randomize_objects, "
+                                    "seed=42 episode seeds, staged reward, FSM expert abs_pos, autoreset"
+                                    if args.image_size == 0 else
+                                    f"C5-style: C3 settings plus overhead + wrist RGB {args.image_size}x"
+                                    f"{args.image_size} camera images rendered every env step"),
+                       "envs_per_gpu": N, "global_envs": N * world, "substeps": 16, "image_size": args.image_size,
                        "parallelism": f"env-batch dp{world}"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,

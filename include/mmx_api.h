@@ -52,7 +52,7 @@ typedef struct {
   int8_t task_bin[9];
   int32_t fixed_task_obj;       /* -1: sample from the pool (gym_env.py:511-517) */
   int32_t fixed_task_bin;
-  int32_t image_size;           /* keypoint normalisation only; no rendering in this build */
+  int32_t image_size;           /* camera image side (multiple of 4, <= 1024); 0 = no rendering */
   int32_t autoreset;            /* same-step autoreset on terminated/truncated/FSM done */
   int32_t solver_iterations;    /* Newton iteration cap (default 30) */
   float solver_tolerance;       /* relative gradient-norm tolerance (default 1e-6) */
@@ -80,6 +80,10 @@ typedef struct {
                                 collision, constraints, solver, integrate, step end (reward/obs/reset),
                                 4 sub-phase probes (cycle fields: diagnostic build only, else 0) */
   float* contacts;           /* [N][64][12] dist, pos3, normal3, mu3, dim, geom1, geom2 (last substep) */
+  uint8_t* images;           /* [N][2][S][S][3] RGB of the overhead and wrist cameras (S = image_size),
+                                rendered after every reset / step / forward; NULL when image_size = 0 */
+  uint8_t* seg;              /* [N][2][S][S] segment ids: 0 sky, 1 floor, 2 table, 3-5 bins (red, green,
+                                blue), 6-8 cubes (red, green, blue), 9 robot; NULL when image_size = 0 */
 } mmx_buffers;
 
 void mmx_config_default(mmx_config* cfg);

@@ -46,6 +46,7 @@ class MMXBuffers(C.Structure):
         ("qacc_warmstart", C.c_void_p), ("obs", C.c_void_p), ("reward", C.c_void_p), ("done", C.c_void_p),
         ("reward_components", C.c_void_p), ("episode_i", C.c_void_p), ("episode_f", C.c_void_p),
         ("kin", C.c_void_p), ("stats", C.c_void_p), ("contacts", C.c_void_p),
+        ("images", C.c_void_p), ("seg", C.c_void_p),
     ]
 
 
@@ -230,6 +231,18 @@ class Sim:
         self._check(self.L.mmx_set_state(self.ptr, *[_fptr(a) for a in arrs]), "mmx_set_state")
 
     # ---- zero-copy torch views of sim-owned buffers (env-major [N][F])
+    def image_views(self):
+        """(rgb [N, 2, S, S, 3] uint8, seg [N, 2, S, S] uint8) or None when image_size == 0."""
+        import torch
+
+        S = int(self.cfg.image_size)
+        if S <= 0 or not self.buffers.images:
+            return None
+        dev = f"cuda:{self.cfg.device}"
+        rgb = torch.as_tensor(_DevArray(self.buffers.images, (self.num_envs, 2, S, S, 3), "|u1", self), device=dev)
+        seg = torch.as_tensor(_DevArray(self.buffers.seg, (self.num_envs, 2, S, S), "|u1", self), device=dev)
+        return rgb, seg
+
     def view(self, name: str, nfield: int, dtype: str = "<f4"):
         import torch
 

@@ -22,6 +22,7 @@ extern "C" hipError_t mmx_launch_step(const MMXState* S, const float* action, in
 extern "C" hipError_t mmx_launch_expert(const MMXState* S, int n, float* action, hipStream_t st);
 extern "C" hipError_t mmx_launch_physics(const MMXState* S, int n, int with_ik, hipStream_t st);
 extern "C" hipError_t mmx_launch_forward(const MMXState* S, hipStream_t st);
+extern "C" hipError_t mmx_launch_render(const MMXState* S, int base, int count, hipStream_t st);
 
 struct mmx_sim {
   MMXState S;
@@ -159,6 +160,7 @@ void mmx_config_default(mmx_config* c) {
 int mmx_create(const mmx_config* cfg, mmx_sim** out) {
   if (!cfg || !out) return MMX_EINVAL;
   *out = nullptr;
+  if (cfg->image_size < 0 || cfg->image_size % 4 != 0 || cfg->image_size > 1024) return MMX_EINVAL;
   if (cfg->num_envs <= 0 || cfg->action_mode < 0 || cfg->action_mode > 4 || cfg->reward_type < 0 ||
       cfg->reward_type > 2 || cfg->n_tasks < 1 || cfg->n_tasks > 9)
     return MMX_EINVAL;
@@ -215,6 +217,12 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
   sim->expert_action = dalloc<float>(sim, 4 * n);
   sim->d_mask = dalloc<unsigned char>(sim, n);
   sim->d_task = dalloc<int>(sim, n);
+  if (cfg->image_size > 0) {  // camera renderer (mmx_render.hip): poses + RGB + segment ids
+    const size_t px = static_cast<size_t>(cfg->image_size) * cfg->image_size;
+    S.rpose = dalloc<float>(sim, 14 * 12 * n);
+    S.images = dalloc<unsigned char>(sim, 2 * px * 3 * n);
+    S.seg = dalloc<unsigned char>(sim, 2 * px * n);
+  }
   for (void* p : sim->allocs)
     if (!p) {
       mmx_destroy(sim);
@@ -313,6 +321,8 @@ int mmx_reset(mmx_sim* sim, const uint64_t* seeds, const uint8_t* seed_given, co
   }
   int rc = hip_check(sim, mmx_launch_reset(&S, dmask, dtask, sim->stream), "mmx_reset");
   if (rc) return rc;
+  rc = hip_check(sim, mmx_launch_render(&S, 0, S.N, sim->stream), "mmx_reset render");
+  if (rc) return rc;
   return hip_check(sim, hipStreamSynchronize(sim->stream), "mmx_reset sync");
 }
 
@@ -320,7 +330,9 @@ int mmx_step(mmx_sim* sim, const float* action_dev, int32_t action_dim) {
   if (!sim || !action_dev) return MMX_EINVAL;
   static const int kDim[5] = {4, 8, 10, 8, 10};
   if (action_dim < kDim[sim->S.action_mode]) return fail(sim, MMX_EINVAL, "action_dim too small for action_mode");
-  return hip_check(sim, mmx_launch_step(&sim->S, action_dev, action_dim, 0, 0, sim->S.N, sim->stream), "mmx_step");
+  hipError_t e = mmx_launch_step(&sim->S, action_dev, action_dim, 0, 0, sim->S.N, sim->stream);
+  if (e == hipSuccess) e = mmx_launch_render(&sim->S, 0, sim->S.N, sim->stream);
+  return hip_check(sim, e, "mmx_step");
 }
 
 int mmx_expert_plan(mmx_sim* sim, int32_t n_steps, float* action_dev_out) {
@@ -341,7 +353,9 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
   for (int k = 0; k < n_env_steps && e == hipSuccess; k++)
     for (int l = 0; l < L && e == hipSuccess; l++) {
       const int b0 = (int)((long)N * l / L), b1 = (int)((long)N * (l + 1) / L);
-      e = mmx_launch_step(&sim->S, sim->expert_action, 4, 1, b0, b1 - b0, l ? sim->lane[l] : sim->stream);
+      hipStream_t st = l ? sim->lane[l] : sim->stream;
+      e = mmx_launch_step(&sim->S, sim->expert_action, 4, 1, b0, b1 - b0, st);
+      if (e == hipSuccess) e = mmx_launch_render(&sim->S, b0, b1 - b0, st);
     }
   if (L > 1)  // join: the caller's stream sees the whole rollout, as with a single launch chain
     for (int l = 1; l < L; l++) {
@@ -361,7 +375,9 @@ int mmx_physics_step(mmx_sim* sim, int32_t n, int32_t with_ik) {
 
 int mmx_forward(mmx_sim* sim) {
   if (!sim) return MMX_EINVAL;
-  return hip_check(sim, mmx_launch_forward(&sim->S, sim->stream), "mmx_forward");
+  hipError_t e = mmx_launch_forward(&sim->S, sim->stream);
+  if (e == hipSuccess) e = mmx_launch_render(&sim->S, 0, sim->S.N, sim->stream);
+  return hip_check(sim, e, "mmx_forward");
 }
 
 int mmx_get_buffers(mmx_sim* sim, mmx_buffers* b) {
@@ -381,6 +397,8 @@ int mmx_get_buffers(mmx_sim* sim, mmx_buffers* b) {
   b->kin = S.kin;
   b->stats = S.stats;
   b->contacts = S.con;
+  b->images = S.images;
+  b->seg = S.seg;
   return MMX_OK;
 }
 

@@ -2066,6 +2066,11 @@ DEV void store_env(const MMXState& S, int i, const EnvSh& E) {
   if (LANE < KIN_N) S.kin[(size_t)i * KIN_N + LANE] = E.kin[LANE];
   if (LANE < 4) S.target[(size_t)i * 4 + LANE] = E.target[LANE];
   if (LANE < STAT_N) S.stats[(size_t)i * STAT_N + LANE] = E.stats[LANE];
+  if (S.rpose)  // body poses for the camera renderer (mmx_render.hip)
+    for (int k = LANE; k < NSLOT * 12; k += WG) {
+      const int sl = k / 12, c = k % 12;
+      S.rpose[(size_t)i * NSLOT * 12 + k] = c < 9 ? E.bR[sl][c] : E.bx[sl][c - 9];
+    }
 }
 DEV void store_obs(const MMXState& S, int i, const EnvSh& E) {
   SYNC();

@@ -1,0 +1,283 @@
+// Batched camera renderer for gfx950: the overhead and wrist images of
+// PickPlaceGymEnv's observation (gym_env.py:295-339 via cameras.py:9-53, mujoco.Renderer).
+//
+// One workgroup (256 lanes) renders one horizontal band of one camera image of one env:
+//   1. body poses of the env (stored by the step / reset / forward kernels in S.rpose) and the
+//      camera pose (overhead: fixed; wrist: on the hand, env.py:52-65) -> LDS;
+//   2. all render vertices (tools/compile_render.py: floor grid, table / bins / cubes as boxes
+//      and prisms, each Panda body as the hull of its visual meshes) to camera space -> LDS;
+//   3. triangles, one lane each: near cull, projection (MuJoCo pinhole, fovy, row 0 at the top),
+//      back-face cull, bounding box clipped to the band.  Small boxes are scanned by the lane
+//      itself; large ones (floor tiles, table top) go to an LDS queue that the whole workgroup
+//      scans pixel-parallel.  Depth test = one 32-bit LDS atomicMax per covered pixel on
+//      (inverse depth quantised over the camera's depth range : 20 bits | triangle : 12 bits);
+//   4. shading, 4 pixels per lane: flat per-face light (computed once per triangle in pass 3), MuJoCo's
+//      headlight (ambient 0.3, diffuse 0.6) + the scene's directional (0.8) and point (0.4)
+//      lights (pick_and_place_scene.xml:6-9,33-36), the floor checker (0.1 m squares), sky
+//      gradient elsewhere; RGB u8 and the segment id written as packed dwords.
+// Not modelled (documented in DESIGN.md): shadows, specular, reflectance, bin transparency
+// (alpha 0.4 -> opaque), visual-mesh detail beyond each body's convex hull.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define MMX_MODEL_QUAL static __constant__
+#include "mmx_model_gen.h"
+#define MMR_QUAL static __constant__
+#include "mmx_render_gen.h"
+#include "mmx_device.h"
+#include "mmx_state.h"
+
+#define RWG 256
+#define RNSLOT 14
+static_assert(MMR_NTRI <= 4096, "triangle index must fit the 12-bit depth-key field");
+#ifndef MMR_BAND_PX
+#define MMR_BAND_PX 8192
+#endif
+#ifndef MMR_SMALL_AREA
+#define MMR_SMALL_AREA 64
+#endif
+static constexpr int kBandPx = MMR_BAND_PX;      // z-buffer pixels per band (32 KB of LDS)
+static constexpr int kSmallArea = MMR_SMALL_AREA; // bounding boxes up to this many pixels: one lane
+static constexpr int kMaxBig = 1024;
+
+DEV int rend_band_rows(int S) { return kBandPx / S < S ? kBandPx / S : S; }
+
+struct RTri {  // screen-space setup of one triangle
+  float x0, y0, x1, y1, x2, y2;  // pixel coordinates
+  float iz0, iz1, iz2;           // 1 / depth
+  int i0, i1, i2;                // vertex ids: shared edges are evaluated in one canonical order
+  int bx0, by0, bx1, by1;        // pixel bbox (inclusive), clipped to the band
+};
+
+// Edge function of a -> b at p, evaluated from the lower vertex id to the higher one and negated
+// when the triangle walks the edge the other way: the two triangles of a shared edge get exactly
+// opposite values, so no pixel centre on the edge is missed by both (no FMA contraction either).
+DEV float rend_edge(float xa, float ya, int ia, float xb, float yb, int ib, float px, float py) {
+#pragma clang fp contract(off)
+  const bool fwd = ia < ib;
+  const float x0 = fwd ? xa : xb, y0 = fwd ? ya : yb, x1 = fwd ? xb : xa, y1 = fwd ? yb : ya;
+  const float e = __fsub_rn(__fmul_rn(x0 - px, y1 - py), __fmul_rn(x1 - px, y0 - py));
+  return fwd ? e : -e;
+}
+
+// camera-space vertex -> screen; false if behind the near plane
+DEV bool rend_project(float4 c, float f, float half, float znear, float& sx, float& sy, float& iz) {
+  const float d = -c.z;
+  if (d < znear) return false;
+  iz = 1.f / d;
+  sx = half + f * c.x * iz;
+  sy = half - f * c.y * iz;
+  return true;
+}
+
+DEV bool rend_setup(const float4* vc, int t, float f, float half, float znear, int S, int row0, int row1,
+                    RTri& T) {
+  const int a = MMR_tri[3 * t], b = MMR_tri[3 * t + 1], c = MMR_tri[3 * t + 2];
+  T.i0 = a;
+  T.i1 = b;
+  T.i2 = c;
+  if (!rend_project(vc[a], f, half, znear, T.x0, T.y0, T.iz0)) return false;
+  if (!rend_project(vc[b], f, half, znear, T.x1, T.y1, T.iz1)) return false;
+  if (!rend_project(vc[c], f, half, znear, T.x2, T.y2, T.iz2)) return false;
+  // screen y points down: a counter-clockwise (outward) face has negative signed area
+  const float area = (T.x1 - T.x0) * (T.y2 - T.y0) - (T.x2 - T.x0) * (T.y1 - T.y0);
+  if (!(area < -1e-12f)) return false;
+  const float mnx = fminf(T.x0, fminf(T.x1, T.x2)), mxx = fmaxf(T.x0, fmaxf(T.x1, T.x2));
+  const float mny = fminf(T.y0, fminf(T.y1, T.y2)), mxy = fmaxf(T.y0, fmaxf(T.y1, T.y2));
+  // pixel (i, j) has its centre at (i + 0.5, j + 0.5)
+  T.bx0 = max(0, (int)ceilf(mnx - 0.5f));
+  T.bx1 = min(S - 1, (int)floorf(mxx - 0.5f));
+  T.by0 = max(row0, (int)ceilf(mny - 0.5f));
+  T.by1 = min(row1 - 1, (int)floorf(mxy - 0.5f));
+  return T.bx0 <= T.bx1 && T.by0 <= T.by1;
+}
+
+// coverage + depth key of pixel (px, py) for triangle t; 0 = not covered
+DEV uint32_t rend_cover(const RTri& T, int t, int px, int py, float iz_lo, float iz_scale) {
+  const float x = px + 0.5f, y = py + 0.5f;
+  // front faces have negative screen area: inside = every edge function <= 0
+  const float e0 = rend_edge(T.x1, T.y1, T.i1, T.x2, T.y2, T.i2, x, y);
+  const float e1 = rend_edge(T.x2, T.y2, T.i2, T.x0, T.y0, T.i0, x, y);
+  const float e2 = rend_edge(T.x0, T.y0, T.i0, T.x1, T.y1, T.i1, x, y);
+  if (e0 > 0.f || e1 > 0.f || e2 > 0.f) return 0u;
+  const float inv = 1.f / (e0 + e1 + e2);
+  const float iz = (e0 * T.iz0 + e1 * T.iz1 + e2 * T.iz2) * inv;
+  const float q = fminf(fmaxf((iz - iz_lo) * iz_scale, 0.f), 1.f);
+  const uint32_t d = 1u + (uint32_t)(q * 1048574.f);  // 1 .. 2^20 - 1 (0 = empty)
+  return (d << 12) | (uint32_t)t;
+}
+
+extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, int env_base) {
+  extern __shared__ __align__(16) unsigned char rsmem[];
+  float4* vc = reinterpret_cast<float4*>(rsmem);                                 // [MMR_NVERT]
+  float* bpose = reinterpret_cast<float*>(vc + MMR_NVERT);                        // [19][12]
+  uint32_t* zb = reinterpret_cast<uint32_t*>(bpose + 19 * 12);                    // [kBandPx]
+  unsigned short* bigq = reinterpret_cast<unsigned short*>(zb + kBandPx);         // [kMaxBig]
+  int* nbig = reinterpret_cast<int*>(bigq + kMaxBig);
+  float* cam = reinterpret_cast<float*>(nbig + 4);                                // R (9), p (3)
+  uint32_t* tinfo = reinterpret_cast<uint32_t*>(cam + 12);                        // [MMR_NTRI]
+  float* mrgb = reinterpret_cast<float*>(tinfo + MMR_NTRI);                       // [MMR_NMAT][8]
+
+  const int tid = threadIdx.x;
+  const int Sz = S.image_size;
+  const int rows = rend_band_rows(Sz);
+  const int row0 = blockIdx.x * rows, row1 = min(Sz, row0 + rows);
+  const int ci = blockIdx.y;  // 0 overhead, 1 wrist
+  const int i = env_base + blockIdx.z;
+  if (i >= S.N || row0 >= Sz) return;
+  const float* rp = S.rpose + (size_t)i * RNSLOT * 12;
+
+  // 1. body poses (world, static scene bodies, moving bodies) and the camera
+  if (tid < 19) {
+    float* o = bpose + 12 * tid;
+    const int b = tid;
+    const int slot = b >= 1 && b <= 11 ? b - 1 : (b >= 16 ? b - 5 : -1);
+    if (slot >= 0) {
+      for (int k = 0; k < 12; k++) o[k] = rp[12 * slot + k];
+    } else {  // world and the static table / bins: parent = world
+      const M3 R = qmat(Q4{MMX_body_quat[4 * b], MMX_body_quat[4 * b + 1], MMX_body_quat[4 * b + 2],
+                           MMX_body_quat[4 * b + 3]});
+      for (int k = 0; k < 9; k++) o[k] = b == 0 ? (k % 4 == 0 ? 1.f : 0.f) : R.m[k];
+      for (int k = 0; k < 3; k++) o[9 + k] = b == 0 ? 0.f : MMX_body_pos[3 * b + k];
+    }
+  }
+  if (tid == 32) {
+    nbig[0] = 0;
+    const int c = ci == 0 ? MMX_CAM_OVERHEAD : MMX_CAM_WRIST;
+    const M3 lq = qmat(Q4{MMX_cam_quat[4 * c], MMX_cam_quat[4 * c + 1], MMX_cam_quat[4 * c + 2], MMX_cam_quat[4 * c + 3]});
+    const V3 lp = V3{MMX_cam_pos[3 * c], MMX_cam_pos[3 * c + 1], MMX_cam_pos[3 * c + 2]};
+    M3 R = lq;
+    V3 p = lp;
+    if (MMX_cam_body[c] != 0) {
+      const int s = MMX_cam_body[c] - 1;  // the hand: an arm body slot
+      M3 hR;
+      for (int k = 0; k < 9; k++) hR.m[k] = rp[12 * s + k];
+      const V3 hx = V3{rp[12 * s + 9], rp[12 * s + 10], rp[12 * s + 11]};
+      R = mul(hR, lq);
+      p = hx + mul(hR, lp);
+    }
+    for (int k = 0; k < 9; k++) cam[k] = R.m[k];
+    cam[9] = p.x; cam[10] = p.y; cam[11] = p.z;
+  }
+  for (int k = tid; k < (row1 - row0) * Sz; k += RWG) zb[k] = 0u;
+  if (tid < MMR_NMAT * 8) {  // rgb1, rgb2, checker square, segment id
+    const int m = tid >> 3, k = tid & 7;
+    mrgb[tid] = k < 6 ? MMR_mat_rgb[6 * m + k] : (k == 6 ? MMR_mat_checker[m] : (float)MMR_mat_seg[m]);
+  }
+  __syncthreads();
+
+  // 2. vertices to camera space
+  M3 cR;
+  for (int k = 0; k < 9; k++) cR.m[k] = cam[k];
+  const V3 cx = V3{cam[9], cam[10], cam[11]};
+  for (int v = tid; v < MMR_NVERT; v += RWG) {
+    const float* o = bpose + 12 * MMR_vert_body[v];
+    M3 R;
+    for (int k = 0; k < 9; k++) R.m[k] = o[k];
+    const V3 w = V3{o[9], o[10], o[11]} + mul(R, V3{MMR_vert[3 * v], MMR_vert[3 * v + 1], MMR_vert[3 * v + 2]});
+    const V3 c = mulT(cR, w - cx);
+    vc[v] = make_float4(c.x, c.y, c.z, 0.f);
+  }
+  __syncthreads();
+
+  // 3. rasterise
+  const int c = ci == 0 ? MMX_CAM_OVERHEAD : MMX_CAM_WRIST;
+  const float half = 0.5f * Sz;
+  const float f = half / tanf(MMX_cam_fovy[c] * (3.14159265358979f / 360.f));
+  // depth range of the camera: overhead 2 m above the floor, wrist from 1 cm
+  const float znear = ci == 0 ? 0.5f : 0.01f, zfar = ci == 0 ? 2.5f : 4.0f;
+  const float iz_lo = 1.f / zfar, iz_scale = 1.f / (1.f / znear - 1.f / zfar);
+  const V3 l_top = mulT(cR, V3{0.f, 0.f, 1.f});  // toward the directional light (dir 0 0 -1)
+  const V3 lp_cam = mulT(cR, V3{0.5f, 0.5f, 1.5f} - cx);
+  for (int t = tid; t < MMR_NTRI; t += RWG) {
+    RTri T;
+    if (!rend_setup(vc, t, f, half, znear, Sz, row0, row1, T)) continue;
+    {  // flat shading of the face, once: headlight + directional + point light (at the centroid)
+      const float4 a = vc[T.i0], b = vc[T.i1], cc = vc[T.i2];
+      const V3 n = normalize(cross(V3{b.x - a.x, b.y - a.y, b.z - a.z}, V3{cc.x - a.x, cc.y - a.y, cc.z - a.z}));
+      const V3 pc = V3{(a.x + b.x + cc.x) * (1.f / 3.f), (a.y + b.y + cc.y) * (1.f / 3.f), (a.z + b.z + cc.z) * (1.f / 3.f)};
+      const float light = 0.3f + 0.6f * fmaxf(n.z, 0.f) + 0.8f * fmaxf(dot(n, l_top), 0.f) +
+                          0.4f * fmaxf(dot(n, normalize(lp_cam - pc)), 0.f);
+      tinfo[t] = ((uint32_t)(fminf(light, 3.99f) * 16384.f) << 16) | MMR_tri_mat[t];
+    }
+    const int area = (T.bx1 - T.bx0 + 1) * (T.by1 - T.by0 + 1);
+    if (area > kSmallArea) {
+      const int k = atomicAdd(nbig, 1);
+      if (k < kMaxBig) bigq[k] = (unsigned short)t;
+      continue;
+    }
+    for (int py = T.by0; py <= T.by1; py++)
+      for (int px = T.bx0; px <= T.bx1; px++) {
+        const uint32_t key = rend_cover(T, t, px, py, iz_lo, iz_scale);
+        if (key) atomicMax(&zb[(py - row0) * Sz + px], key);
+      }
+  }
+  __syncthreads();
+  const int nb = min(nbig[0], kMaxBig);
+  for (int q = 0; q < nb; q++) {  // large triangles: the workgroup scans the box pixel-parallel
+    const int t = bigq[q];
+    RTri T;
+    rend_setup(vc, t, f, half, znear, Sz, row0, row1, T);
+    const int w = T.bx1 - T.bx0 + 1, area = w * (T.by1 - T.by0 + 1);
+    for (int k = tid; k < area; k += RWG) {
+      const int px = T.bx0 + k % w, py = T.by0 + k / w;
+      const uint32_t key = rend_cover(T, t, px, py, iz_lo, iz_scale);
+      if (key) atomicMax(&zb[(py - row0) * Sz + px], key);
+    }
+  }
+  __syncthreads();
+
+  // 4. shade, 4 pixels per lane (S is a multiple of 4): everything from LDS
+  const int npx = (row1 - row0) * Sz;
+  unsigned char* img = S.images + ((size_t)i * 2 + ci) * Sz * Sz * 3 + (size_t)row0 * Sz * 3;
+  unsigned char* seg = S.seg + ((size_t)i * 2 + ci) * Sz * Sz + (size_t)row0 * Sz;
+  for (int g = tid; g < npx / 4; g += RWG) {
+    uint32_t rgbw[3] = {0u, 0u, 0u}, segw = 0u;
+    for (int u = 0; u < 4; u++) {
+      const int p = 4 * g + u;
+      const int px = p % Sz, py = row0 + p / Sz;
+      const uint32_t key = zb[p];
+      const V3 dw = mul(cR, V3{(px + 0.5f - half) / f, -(py + 0.5f - half) / f, -1.f});  // world ray
+      float col[3];
+      int sid = 0;
+      if (key == 0u) {  // skybox gradient (rgb1 top -> rgb2 bottom, scene.xml:17-18)
+        const float sky = 0.5f * (dw.z * rsqrtf(dot(dw, dw)) + 1.f);
+        col[0] = 0.3f * sky; col[1] = 0.5f * sky; col[2] = 0.7f * sky;
+      } else {
+        const uint32_t ti = tinfo[key & 4095];
+        const float* mt = mrgb + 8 * (ti & 255);
+        const float light = (float)(ti >> 16) * (1.f / 16384.f);
+        sid = (int)mt[7];
+        bool alt = false;
+        if (mt[6] > 0.f) {  // floor checker: the ray meets the plane z = 0
+          const float s0 = -cx.z / dw.z;
+          alt = ((int)floorf((cx.x + s0 * dw.x) / mt[6]) + (int)floorf((cx.y + s0 * dw.y) / mt[6])) & 1;
+        }
+        for (int k = 0; k < 3; k++) col[k] = fminf((alt ? mt[3 + k] : mt[k]) * light, 1.f);
+      }
+      for (int k = 0; k < 3; k++) {
+        const uint32_t v8 = (uint32_t)(col[k] * 255.f + 0.5f);
+        const int byte = 3 * u + k;
+        rgbw[byte >> 2] |= v8 << (8 * (byte & 3));
+      }
+      segw |= (uint32_t)sid << (8 * u);
+    }
+    uint32_t* o = reinterpret_cast<uint32_t*>(img + 12 * (size_t)g);
+    o[0] = rgbw[0]; o[1] = rgbw[1]; o[2] = rgbw[2];
+    reinterpret_cast<uint32_t*>(seg)[g] = segw;
+  }
+}
+
+extern "C" size_t mmx_render_lds_bytes() {
+  return sizeof(float4) * MMR_NVERT + sizeof(float) * 19 * 12 + sizeof(uint32_t) * kBandPx +
+         sizeof(unsigned short) * kMaxBig + 4 * sizeof(int) + 12 * sizeof(float) + sizeof(uint32_t) * MMR_NTRI +
+         sizeof(float) * 8 * MMR_NMAT;
+}
+
+extern "C" hipError_t mmx_launch_render(const MMXState* S, int base, int count, hipStream_t st) {
+  if (count <= 0 || S->image_size <= 0) return hipSuccess;
+  const int rows = S->image_size < kBandPx / S->image_size ? S->image_size : kBandPx / S->image_size;
+  const int bands = (S->image_size + rows - 1) / rows;
+  hipLaunchKernelGGL(mmx_render_kernel, dim3(bands, 2, count), dim3(RWG), mmx_render_lds_bytes(), st, *S, base);
+  return hipGetLastError();
+}

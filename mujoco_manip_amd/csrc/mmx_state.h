@@ -89,6 +89,10 @@ struct MMXState {
   // diagnostics
   float* con;    // [N][MAXCON][CON_F] contacts of the last substep
   float* stats;  // [N][STAT_N]
+  // camera images (image_size > 0 only, else null)
+  float* rpose;            // [N][14][12] body poses (R row-major, p) of the last position stage
+  unsigned char* images;   // [N][2][S][S][3] overhead, wrist RGB
+  unsigned char* seg;      // [N][2][S][S] segment ids (0 sky, 1 floor, 2 table, 3-5 bins, 6-8 cubes, 9 robot)
 };
 
 #endif

@@ -32,7 +32,7 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from .constants import ACTION_REPEAT, BINS, CONTROL_FPS, OBJECTS, OBS_SLICES, TASK_SETS
+from .constants import ACTION_REPEAT, BINS, CONTROL_FPS, IMAGE_SIZE, OBJECTS, OBS_SLICES, TASK_SETS
 
 # features.py:10-106 (IMAGE_SIZE = 224)
 FEATURES = {
@@ -225,7 +225,8 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
     N = max(1, min(int(num_envs), E))
     env = PickPlaceVecEnv(N, tasks=[tuple(t) for t in task_list], action_mode="abs_pos", reward_type=reward_type,
                           randomize_objects=randomize_objects, spawn_x_range=tuple(spawn_x_range),
-                          spawn_y_range=tuple(spawn_y_range), autoreset=False, device=device)
+                          spawn_y_range=tuple(spawn_y_range), autoreset=False, device=device,
+                          image_size=IMAGE_SIZE if set(feature_keys) & set(IMAGE_KEYS) else 0)
     dev = env.device
     need_actions = bool(set(feature_keys) & set(ACTION_KEYS))
     need_reward = "next.reward" in feature_keys and reward_type == "staged"

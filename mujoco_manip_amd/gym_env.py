@@ -1,7 +1,7 @@
 """PickPlaceGymEnv — single-env façade with the reference signature (gym_env.py:62-75).
 
 A drop-in for mujoco_manip.gym_env.PickPlaceGymEnv on the numeric path: reset/step return
-numpy observations (same keys minus the camera images), float rewards and bool flags.
+numpy observations (same keys; camera images from the HIP renderer when image_size > 0), float rewards and bool flags.
 Internally it is a PickPlaceVecEnv with num_envs=1 running on the MI355X.
 """
 from __future__ import annotations
@@ -101,7 +101,15 @@ class PickPlaceGymEnv(_Base):
         return self._vec.expert_plan(n_steps)[0].cpu().numpy()
 
     def render(self):
-        raise NotImplementedError("camera rendering (config 5) is not part of this build")
+        """gym_env.py:583-596: 'rgb_array' returns the overhead RGB image of the current state
+        (rendered on the GPU at image_size); 'human' (interactive viewer) is out of scope."""
+        if self.render_mode == "rgb_array":
+            if self._vec._images is None:
+                raise ValueError("render_mode='rgb_array' needs image_size > 0")
+            return self._vec._images[0, 0].cpu().numpy()
+        if self.render_mode == "human":
+            raise NotImplementedError("the interactive MuJoCo viewer is out of scope (no display on the GPU box)")
+        return None
 
     def close(self):
         self._vec.close()

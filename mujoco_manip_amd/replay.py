@@ -86,7 +86,7 @@ def replay(dataset_root: str, episodes=None, action_key: str = "action.ee.pos_qu
     sx, sy = setups[0][2], setups[0][3]
     n = len(ids)
     env = PickPlaceVecEnv(n, action_mode=mode, reward_type="staged", randomize_objects=randomize,
-                          spawn_x_range=sx, spawn_y_range=sy, autoreset=False, device=device)
+                          spawn_x_range=sx, spawn_y_range=sy, autoreset=False, image_size=0, device=device)
     task = None
     if all(s[1] is not None for s in setups):
         task = [s[1] for s in setups]

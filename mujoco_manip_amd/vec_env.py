@@ -3,8 +3,9 @@
 Mirrors PickPlaceGymEnv (mujoco_manip/gym_env.py:39-602) with a leading env dimension:
 same constructor keywords, same 5 action modes, same numeric observation keys and reward
 types.  Differences, all documented in DESIGN.md:
-  * observations are torch tensors on the GPU ([N, ...]); images are not rendered in this
-    build (config 5 renderer is a follow-up), so the image keys are absent;
+  * observations are torch tensors on the GPU ([N, ...]); with image_size > 0 the
+    `image_overhead` / `image_wrist` keys are uint8 [N, S, S, 3] from the batched HIP renderer
+    (mmx_render.hip: hull geometry, MuJoCo lights; DESIGN.md §10), image_size = 0 skips them;
   * reset(seed=s) seeds env i with s + i (gymnasium vector convention); a list gives one
     seed per env;
   * with autoreset=True an env that terminated/truncated is reset inside the same step
@@ -60,6 +61,8 @@ class PickPlaceVecEnv:
         self.ctrl = s.view("ctrl", _lib.NU)
         self.stats = s.view("stats", _lib.STAT_N)
         self._expert_action = torch.zeros(self.num_envs, 4, device=self.device, dtype=torch.float32)
+        iv = s.image_views()
+        self._images, self._seg = iv if iv is not None else (None, None)
 
     # ------------------------------------------------------------------ gym API
     def _obs_dict(self):
@@ -67,7 +70,15 @@ class PickPlaceVecEnv:
         out = {}
         for k, (a, b, shape) in OBS_SLICES.items():
             out[k] = flat[:, a:b].reshape(self.num_envs, *shape).clone()
+        if self._images is not None:  # gym_env.py:325-326
+            out["image_overhead"] = self._images[:, 0].clone()
+            out["image_wrist"] = self._images[:, 1].clone()
         return out
+
+    @property
+    def segmentation(self) -> torch.Tensor | None:
+        """Segment ids [N, 2, S, S] of the last rendered images (overhead, wrist), or None."""
+        return None if self._seg is None else self._seg.clone()
 
     def reset(self, *, seed=None, options: dict | None = None):
         """PickPlaceGymEnv.reset (gym_env.py:477-534), batched."""

@@ -88,8 +88,8 @@ def test_physics_parity_one_env_step():  # L1: 16 substeps; SURVEY bound qpos <=
     assert dv.max() < 2e-2, dv.max()
 
 
-def _flat(obs, n):
-    return torch.cat([obs[k].reshape(n, -1) for k in obs], 1).cpu().numpy()
+def _flat(obs, n):  # the 85 numeric observation values (camera images excluded)
+    return torch.cat([obs[k].reshape(n, -1) for k in obs if not k.startswith("image_")], 1).cpu().numpy()
 
 
 def test_reset_parity_randomized_seeds():  # L0: PCG64 stream, spawn, task draw, obs codecs

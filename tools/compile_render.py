@@ -1,0 +1,222 @@
+#!/usr/bin/env python3
+"""Offline render-model compiler: scene + Panda visual meshes -> a triangle model.
+
+Runs in the build container only (the MJCF and meshes live under the reference mount). Its
+outputs are committed DATA:
+
+  mujoco_manip_amd/csrc/mmx_render_gen.h       tables for the HIP rasterizer
+  mujoco_manip_amd/model/render_model.json     the same model for the CPU ray-cast checker
+
+Geometry (all vertices in their BODY frame, so the device only needs body poses):
+  * floor plane (pick_and_place_scene.xml:40) as an 8 x 8 grid of quads, checker material
+    `groundplane` (rgb1/rgb2, texrepeat 5 5, texuniform: 0.1 m squares);
+  * every box geom of the table, bins and cubes (:43-125) as 12 triangles, the table legs
+    (cylinders) as 16-gon prisms, each with its own material rgba;
+  * each Panda body as the convex hull of all its visual meshes (panda.xml:123-246, the
+    134 k-triangle visual set is far beyond what a batched per-env rasterizer should carry),
+    reduced to <= MAX_HULL_VERTS points by farthest-point sampling, coloured with the
+    material of the body's largest visual part.
+Segment ids (the mask-level parity channel): 0 sky, 1 floor, 2 table, 3/4/5 bins red/green/blue,
+6/7/8 cubes red/green/blue, 9 robot.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import xml.etree.ElementTree as ET
+
+import numpy as np
+from scipy.spatial import ConvexHull
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import compile_model as CM  # noqa: E402
+
+MAX_HULL_VERTS = 96
+FLOOR_GRID = 8
+CYL_SIDES = 16
+SEG = {"floor": 1, "table": 2, "bin_red": 3, "bin_green": 4, "bin_blue": 5, "obj_red": 6, "obj_green": 7,
+       "obj_blue": 8, "robot": 9}
+ROBOT = ["link0", "link1", "link2", "link3", "link4", "link5", "link6", "link7", "hand", "left_finger",
+         "right_finger"]
+
+
+def rgba(s):
+    return [float(x) for x in s.split()]
+
+
+def box_mesh(half):
+    hx, hy, hz = half
+    v = np.array([[sx * hx, sy * hy, sz * hz] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)])
+    h = ConvexHull(v)
+    return v, oriented_faces(v, h)
+
+
+def cylinder_mesh(r, hh, n=CYL_SIDES):
+    ang = 2 * np.pi * np.arange(n) / n
+    ring = np.stack([r * np.cos(ang), r * np.sin(ang)], 1)
+    v = np.concatenate([np.c_[ring, -hh * np.ones(n)], np.c_[ring, hh * np.ones(n)]])
+    h = ConvexHull(v)
+    return v, oriented_faces(v, h)
+
+
+def oriented_faces(v, h):
+    c = v.mean(0)
+    out = []
+    for s in h.simplices:
+        a, b, cc = v[s]
+        n = np.cross(b - a, cc - a)
+        out.append([int(s[0]), int(s[1]), int(s[2])] if np.dot(n, a - c) > 0 else [int(s[0]), int(s[2]), int(s[1])])
+    return out
+
+
+def fps_subsample(p, k):
+    """farthest-point sampling of k points (deterministic: start at the point farthest from the mean)."""
+    if len(p) <= k:
+        return p
+    idx = [int(np.argmax(np.linalg.norm(p - p.mean(0), axis=1)))]
+    d = np.linalg.norm(p - p[idx[0]], axis=1)
+    for _ in range(k - 1):
+        i = int(np.argmax(d))
+        idx.append(i)
+        d = np.minimum(d, np.linalg.norm(p - p[i], axis=1))
+    return p[idx]
+
+
+def hull_mesh(points, k=MAX_HULL_VERTS):
+    h = ConvexHull(points)
+    p = fps_subsample(points[h.vertices], k)
+    h2 = ConvexHull(p)
+    v = p[h2.vertices]
+    remap = {int(j): i for i, j in enumerate(h2.vertices)}
+    faces = [[remap[int(j)] for j in s] for s in h2.simplices]
+    return v, oriented_faces(v, type("H", (), {"simplices": np.array(faces)})), float(h.volume)
+
+
+def geom_to_body(v, pos, quat):
+    R = CM.quat2mat(quat)
+    return v @ R.T + np.asarray(pos, float)
+
+
+def build():
+    model = CM.compile_model()
+    bodies = model["bodies"]
+    bnames = [b["name"] for b in bodies]
+    scene = ET.parse(CM.SCENE).getroot()
+    panda = ET.parse(CM.PANDA).getroot()
+    mats = {}
+    for m in list(scene.find("asset").iter("material")) + list(panda.find("asset").iter("material")):
+        if m.get("rgba"):
+            mats[m.get("name")] = rgba(m.get("rgba"))
+    # checker floor colours (pick_and_place_scene.xml:19-22)
+    tex = {t.get("name"): t for t in scene.find("asset").iter("texture")}["groundplane"]
+    materials = [dict(name="groundplane", rgb=rgba(tex.get("rgb1")), rgb2=rgba(tex.get("rgb2")), checker=0.1,
+                      seg=SEG["floor"])]
+    mat_index = {}
+
+    def material(name, seg):
+        key = (name, seg)
+        if key not in mat_index:
+            mat_index[key] = len(materials)
+            materials.append(dict(name=name, rgb=mats[name][:3], rgb2=mats[name][:3], checker=0.0, seg=seg))
+        return mat_index[key]
+
+    parts = []  # (body id, verts [k,3] body frame, faces, material index)
+    # floor: grid over [-2, 2]^2 at z = 0 (body 0)
+    g = np.linspace(-2.0, 2.0, FLOOR_GRID + 1)
+    fv = np.array([[x, y, 0.0] for y in g for x in g])
+    ff = []
+    for j in range(FLOOR_GRID):
+        for i in range(FLOOR_GRID):
+            a = j * (FLOOR_GRID + 1) + i
+            b, c, d = a + 1, a + FLOOR_GRID + 1, a + FLOOR_GRID + 2
+            ff += [[a, b, d], [a, d, c]]  # counter-clockwise seen from +z
+    parts.append((0, fv, ff, 0))
+
+    def scene_body(belem, bid):
+        bname = belem.get("name")
+        seg = SEG["table"] if bname == "table" else SEG[bname]
+        for ge in belem.findall("geom"):
+            t = ge.get("type")
+            pos = CM.fl(ge.get("pos", "0 0 0"))
+            size = CM.fl(ge.get("size"))
+            if t == "box":
+                v, f = box_mesh(size)
+            elif t == "cylinder":
+                v, f = cylinder_mesh(size[0], size[1])
+            else:
+                raise ValueError(t)
+            parts.append((bid, geom_to_body(v, pos, [1, 0, 0, 0]), f, material(ge.get("material"), seg)))
+
+    for be in scene.find("worldbody").findall("body"):
+        scene_body(be, bnames.index(be.get("name")))
+
+    # robot bodies: hull of the visual meshes (file coordinates = body frame; no geom pos/quat)
+    meshfile = {}
+    for m in panda.find("asset").findall("mesh"):
+        fname = m.get("file")
+        meshfile[m.get("name", os.path.splitext(fname)[0])] = os.path.join(CM.REF_DATA, "franka_emika_panda",
+                                                                           "assets", fname)
+
+    def walk(be):
+        name = be.get("name")
+        if name in ROBOT:
+            pts, best, best_vol = [], None, -1.0
+            for ge in be.findall("geom"):
+                if ge.get("class") != "visual":
+                    continue
+                assert ge.get("pos") is None and ge.get("quat") is None
+                p = CM.load_obj(meshfile[ge.get("mesh")])
+                vol = ConvexHull(p).volume
+                if vol > best_vol:
+                    best, best_vol = ge.get("material"), vol
+                pts.append(p)
+            v, f, _ = hull_mesh(np.concatenate(pts))
+            parts.append((bnames.index(name), v, f, material(best, SEG["robot"])))
+        for c in be.findall("body"):
+            walk(c)
+
+    for be in panda.find("worldbody").findall("body"):
+        walk(be)
+
+    # flatten, vertices grouped by body
+    verts, vbody, tris, tmat = [], [], [], []
+    for bid, v, f, m in sorted(parts, key=lambda p: p[0]):
+        base = len(verts)
+        verts += [list(map(float, x)) for x in v]
+        vbody += [bid] * len(v)
+        tris += [[base + a, base + b, base + c] for a, b, c in f]
+        tmat += [m] * len(f)
+    return dict(verts=verts, vert_body=vbody, tris=tris, tri_mat=tmat, materials=materials,
+                cameras=model["cameras"], body_names=bnames,
+                static_body_pos={n: bodies[i]["pos"] for i, n in enumerate(bnames) if n in
+                                 ("table", "bin_red", "bin_green", "bin_blue")})
+
+
+def emit(rm, path):
+    L = ["/* generated by tools/compile_render.py -- do not edit */\n#ifndef MMX_RENDER_GEN_H\n"
+         "#define MMX_RENDER_GEN_H\n\n#ifndef MMR_QUAL\n#define MMR_QUAL static const\n#endif\n\n"]
+    nv, nt, nm = len(rm["verts"]), len(rm["tris"]), len(rm["materials"])
+    L.append(f"#define MMR_NVERT {nv}\n#define MMR_NTRI {nt}\n#define MMR_NMAT {nm}\n\n")
+    L.append(CM.c_array("MMR_vert", "float", rm["verts"], "{:.9g}"))
+    L.append(CM.c_array("MMR_vert_body", "unsigned char", rm["vert_body"], "{}"))
+    L.append(CM.c_array("MMR_tri", "unsigned short", rm["tris"], "{}"))
+    L.append(CM.c_array("MMR_tri_mat", "unsigned char", rm["tri_mat"], "{}"))
+    L.append(CM.c_array("MMR_mat_rgb", "float", [m["rgb"] + m["rgb2"] for m in rm["materials"]], "{:.9g}"))
+    L.append(CM.c_array("MMR_mat_checker", "float", [m["checker"] for m in rm["materials"]], "{:.9g}"))
+    L.append(CM.c_array("MMR_mat_seg", "unsigned char", [m["seg"] for m in rm["materials"]], "{}"))
+    L.append("\n#endif /* MMX_RENDER_GEN_H */\n")
+    with open(path, "w") as f:
+        f.write("".join(L).replace(CM.QUAL + " ", "MMR_QUAL "))
+
+
+def main():
+    rm = build()
+    emit(rm, os.path.join(CM.REPO, "mujoco_manip_amd", "csrc", "mmx_render_gen.h"))
+    with open(os.path.join(CM.REPO, "mujoco_manip_amd", "model", "render_model.json"), "w") as f:
+        json.dump(rm, f, separators=(",", ":"))
+    print(f"render model: {len(rm['verts'])} verts, {len(rm['tris'])} triangles, {len(rm['materials'])} materials")
+
+
+if __name__ == "__main__":
+    main()

@@ -113,7 +113,7 @@ def rollout_speed(N=4096, steps=100, warm=50):
     from mujoco_manip_amd.vec_env import PickPlaceVecEnv
 
     env = PickPlaceVecEnv(N, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
-                          autoreset=True)
+                          autoreset=True, image_size=int(os.environ.get("MMX_IMAGE_SIZE", "0")))
     env.reset(seed=[_lib.episode_seed(42, i) for i in range(N)])
     env.rollout_expert(warm)  # bench-like state mix (50 warm-up steps)
     torch.cuda.synchronize()
