@@ -170,9 +170,14 @@ def main():
     env_steps = args.steps * N * world
     value = env_steps / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
-    bytes_per_launch = algorithmic_bytes_per_env_step(solver["mean_nefc"]) * N
-    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
-    min_bytes = min_hbm_bytes_per_env_step() * N
+    # one env step of the batch = `lanes` concurrent mmx_env_step_kernel dispatches of N / lanes
+    # envs each; they run side by side for the whole span, so a dispatch lasts ~kern_ms (rocprof's
+    # per-dispatch average agrees) and the chip-level rate is lanes x one dispatch's bytes / kern_ms
+    lanes = env.sim.rollout_lanes
+    envs_per_launch = N / lanes
+    bytes_per_launch = algorithmic_bytes_per_env_step(solver["mean_nefc"]) * envs_per_launch
+    achieved = lanes * bytes_per_launch / (kern_ms * 1e-3) / 1e9
+    min_bytes = min_hbm_bytes_per_env_step() * envs_per_launch
 
     stats_all = None
     if dist:
@@ -204,10 +209,13 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "mmx_env_step_kernel", "kernel_ms": kern_ms,
-                         "concurrent_launches": env.sim.rollout_lanes,
+                         "concurrent_launches": lanes, "envs_per_launch": envs_per_launch,
+                         "algorithmic_bytes_per_env_step": algorithmic_bytes_per_env_step(solver["mean_nefc"]),
                          "algorithmic_bytes_per_launch": bytes_per_launch, "mean_nefc": solver["mean_nefc"],
+                         "traffic_note": "traffic = PMC FETCH_SIZE x2 + WRITE_SIZE per dispatch "
+                                         "(profiles/pmc_traffic.json), same dispatch size",
                          "min_hbm_bytes_per_launch": min_bytes,
-                         "min_hbm_GBs": min_bytes / (kern_ms * 1e-3) / 1e9},
+                         "min_hbm_GBs": lanes * min_bytes / (kern_ms * 1e-3) / 1e9},
             "cpu_baseline": cpu,
             "solver": solver,
         }

@@ -67,3 +67,25 @@ def build(force: bool = False, verbose: bool = False, profile: bool | None = Fal
 
 if __name__ == "__main__":
     print(build(force=True, verbose=True, profile=None))
+
+
+def build_variant(out: str, defines: list[str], profile: bool = True) -> str:
+    """Diagnostic / experiment build of the same sources with extra -D defines into `out`
+    (e.g. build/libmmx_prof5.so for probe set 5); loaded with MMX_LIB_PATH.  Not the product."""
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    tag = os.path.splitext(os.path.basename(out))[0]
+    os.makedirs(os.path.dirname(os.path.abspath(out)), exist_ok=True)
+
+    def one(src):
+        obj = os.path.join(os.path.dirname(os.path.abspath(out)), f"{tag}_{os.path.splitext(src)[0]}.o")
+        cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", os.path.join(CSRC, src), "-o", obj]
+        cmd[1:1] = FLAGS + [f"-D{d}" for d in defines] + (["-DMMX_PHASE_CLOCK=1"] if profile else [])
+        if src.endswith(".cpp"):
+            cmd.insert(1, "-xhip")
+        subprocess.check_call(cmd)
+        return obj
+
+    with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
+        objs = list(ex.map(one, SOURCES))
+    subprocess.check_call([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out] + objs)
+    return out

@@ -63,7 +63,8 @@ def load(build_if_missing: bool = True):
     if _lib is not None:
         return _lib
     profile = os.environ.get("MMX_PROFILE", "0") not in ("", "0")
-    path = _build.lib_path(profile)
+    # MMX_LIB_PATH: a prebuilt variant of the same sources (diagnostic probe builds, experiments)
+    path = os.environ.get("MMX_LIB_PATH") or _build.lib_path(profile)
     if not os.path.exists(path):
         if not build_if_missing:
             raise RuntimeError(f"{os.path.basename(path)} missing at {path}; run __graft_entry__.build()")
