@@ -109,7 +109,17 @@ def main():
     ap.add_argument("--share-device", action="store_true")
     # 0 = the C3 workload (no images); 128 = C5's two 128 x 128 RGB cameras per env step
     ap.add_argument("--image-size", type=int, default=0)
+    # BASELINE.json configs: c3 (default, the metric's config), c2 (1024 envs, fixed task
+    # (obj_red, bin_red), keyframe start, no randomisation), c5 (c3 settings + 2 x 128^2 RGB
+    # cameras per env step, 8192 envs per GPU as in the 65536-env / 8-GPU config)
+    ap.add_argument("--workload", default="c3", choices=("c2", "c3", "c5"))
     args = ap.parse_args()
+    if args.workload == "c5":
+        args.image_size = args.image_size or 128
+        if args.envs_per_gpu == 4096:
+            args.envs_per_gpu = 8192
+    if args.workload == "c2" and args.envs_per_gpu == 4096:
+        args.envs_per_gpu = 1024
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -134,8 +144,9 @@ def main():
     from mujoco_manip_amd.vec_env import PickPlaceVecEnv
 
     N = args.envs_per_gpu
-    env = PickPlaceVecEnv(N, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
-                          image_size=args.image_size,
+    c2 = args.workload == "c2"
+    env = PickPlaceVecEnv(N, task=("obj_red", "bin_red") if c2 else None, tasks="all", action_mode="abs_pos",
+                          reward_type="staged", randomize_objects=not c2, image_size=args.image_size,
                           autoreset=True, device=dev_index)
     seeds = [_lib.episode_seed(42, rank * N + i) for i in range(N)]
     env.reset(seed=seeds)
@@ -199,10 +210,13 @@ def main():
             "value": value, "unit": "env steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
             "dtype": "f32", "data": "synthetic (seeded randomized scenes, FSM-expert actions)",
-            "config": {"workload": ("C3: PickPlaceGymEnv.step x 4096 envs/GPU, tasks=all, randomize_objects, "
+            "config": {"workload": (f"C2: PickPlaceGymEnv.step x {N} envs/GPU, fixed task (obj_red, bin_red), "
+                                    "keyframe start (no randomisation), staged reward, FSM expert abs_pos, autoreset"
+                                    if c2 else
+                                    f"C3: PickPlaceGymEnv.step x {N} envs/GPU, tasks=all, randomize_objects, "
                                     "seed=42 episode seeds, staged reward, FSM expert abs_pos, autoreset"
                                     if args.image_size == 0 else
-                                    f"C5-style: C3 settings plus overhead + wrist RGB {args.image_size}x"
+                                    f"C5: C3 settings x {N} envs/GPU plus overhead + wrist RGB {args.image_size}x"
                                     f"{args.image_size} camera images rendered every env step"),
                        "envs_per_gpu": N, "global_envs": N * world, "substeps": 16, "image_size": args.image_size,
                        "parallelism": f"env-batch dp{world}"},

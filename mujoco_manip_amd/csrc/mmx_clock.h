@@ -17,7 +17,7 @@ __device__ __forceinline__ unsigned long long clk_now() {
 #define CLK(st, k)                                                           \
   do {                                                                       \
     const unsigned long long clk_t1_ = clk_now();                            \
-    if (threadIdx.x == 0 && clk_t1_ > clk_t0_) (st)[k] += (float)(clk_t1_ - clk_t0_); \
+    if ((threadIdx.x & 63) == 0 && clk_t1_ > clk_t0_) (st)[k] += (float)(clk_t1_ - clk_t0_); \
     clk_t0_ = clk_t1_;                                                       \
   } while (0)
 // variant for divergent code: the first active lane records
@@ -25,7 +25,7 @@ __device__ __forceinline__ unsigned long long clk_now() {
   do {                                                                                     \
     const unsigned long long clk_t1_ = clk_now();                                          \
     const unsigned long long act_ = __ballot(1);                                           \
-    if ((int)threadIdx.x == __ffsll((long long)act_) - 1 && clk_t1_ > clk_t0_)             \
+    if ((int)(threadIdx.x & 63) == __ffsll((long long)act_) - 1 && clk_t1_ > clk_t0_)             \
       (st)[k] += (float)(clk_t1_ - clk_t0_);                                               \
     clk_t0_ = clk_t1_;                                                                     \
   } while (0)

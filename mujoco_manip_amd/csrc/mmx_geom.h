@@ -321,7 +321,7 @@ DEV V3 support_wave(const Geom& G, V3 dir) {
   const int a = MMX_mesh_vertadr[m], nvert = MMX_mesh_vertnum[m];
   float best = -3.0e38f;
   int bi = 0x7fffffff;
-  for (int v = (int)threadIdx.x; v < nvert; v += 64) {
+  for (int v = (int)(threadIdx.x & 63); v < nvert; v += 64) {
     const int q = 3 * (a + v);
     const float s = MMX_mesh_vert[q] * dl.x + MMX_mesh_vert[q + 1] * dl.y + MMX_mesh_vert[q + 2] * dl.z;
     if (s > best) {
@@ -563,7 +563,7 @@ DEV void convex_convex(Sink& cs, const Geom& A, const Geom& B, float* scr) {
   if (!epa(A, B, V, n, nrm, depth, pa, pb, F, edges)) return;
   if (depth < 0.f) return;
   // Minkowski A-B face normal n: translating B by +depth n separates -> normal A->B is n
-  if (threadIdx.x == 0) cs.add(A.g, B.g, -depth, (pa + pb) * 0.5f, nrm);
+  if ((threadIdx.x & 63) == 0) cs.add(A.g, B.g, -depth, (pa + pb) * 0.5f, nrm);
 }
 
 // soft-constraint impedance d(pos) (MuJoCo solimp: dmin, dmax, width, midpoint, power)

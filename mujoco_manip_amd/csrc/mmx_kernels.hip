@@ -25,9 +25,20 @@
 #include "mmx_geom.h"
 #include "mmx_state.h"
 
-#define WG 64
-#define LANE ((int)threadIdx.x)
-#define SYNC() __syncthreads()
+#define WG 64  // lanes of the wave that runs a phase
+// lane within the wave; WAVE_ID: which of the env-step kernel's two waves (0 or 1)
+#define LANE ((int)(threadIdx.x & 63))
+#define WAVE_ID ((int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6))
+// SYNC: wave-local LDS ordering (a phase runs on ONE wave: its lanes exchange data through LDS,
+// whose operations a wave issues and completes in order, so no s_barrier / waitcnt is needed,
+// only a compiler fence).  XSYNC: both waves of the env-step workgroup (s_barrier).
+DEV void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+#define SYNC() wave_sync()
+#define XSYNC() __syncthreads()
 
 static constexpr float kDt = 0.002f;
 static constexpr float kHome[7] = {1.5708f, -0.2f, 0.0f, -2.1f, 0.0f, 1.8f, 0.785f};  // controller.py:8
@@ -1671,6 +1682,14 @@ DEV void mj_step_wave(int max_iter, float tol, EnvSh& E) {
     stats[STAT_SOLVER_ITER] += (float)it;
     stats[STAT_SUBSTEPS] += 1.f;
     stats[STAT_RESID] = fmaxf(stats[STAT_RESID], resid);
+#ifdef MMX_PHASE_CLOCK
+    if (MMX_PROBE == 12) {  // row / contact count distribution (sizes the LDS row capacity)
+      stats[STAT_T_AUX0] = fmaxf(stats[STAT_T_AUX0], (float)E.nefc);
+      stats[STAT_T_AUX1] = fmaxf(stats[STAT_T_AUX1], (float)E.ncon);
+      stats[STAT_T_AUX2] += E.nefc > 192 ? 1.f : 0.f;
+      stats[STAT_T_AUX3] += E.nefc > 224 ? 1.f : 0.f;
+    }
+#endif
   }
   SYNC();
 }
@@ -2187,39 +2206,93 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_substep_kernel(MMXState S, 
 // One substep = IK + mj_step, kept out of line: nothing is hoisted across the 16 iterations of
 // the env-step loop (hoisted invariants would pin registers for the whole kernel and serialise
 // the phases' LDS loads); the price is the callee-saved register spill / fill per call.
-#ifdef MMX_INLINE_SUBSTEP
-DEV void substep(int max_iter, float tol) {
+//
+// Two waves per env (STEP_WG = 128): after the position stage, wave 0 runs the smooth dynamics
+// (RNE, CRBA, actuation, qacc_smooth) while wave 1 runs collision detection; the two phases
+// touch disjoint LDS (M / Ic / bias / qfrc / qacc_s / Lrow scratch vs. contacts / J scratch).
+// Everything else runs on wave 0.  With 4 workgroups per CU (LDS-bound), the second wave is
+// what puts two waves on every SIMD.  MMX_ONE_WAVE builds the single-wave form (64 lanes).
+#ifdef MMX_ONE_WAVE
+#define STEP_WG 64
 #else
-__device__ __attribute__((noinline)) void substep(int max_iter, float tol) {
+#define STEP_WG 128
 #endif
+__device__ __attribute__((noinline)) void substep(int max_iter, float tol) {
   EnvSh& E = g_E;
   float* stats = E.stats;
+#ifdef MMX_ONE_WAVE
   CLK_DECL;
   ik_wave(E);  // IK on the kinematics left by the previous position stage
   CLK(stats, STAT_T_IK);
   mj_step_wave(max_iter, tol, E);
+#else
+  const int w = WAVE_ID;
+  if (w == 0) {
+    CLK_DECL;
+    ik_wave(E);  // IK on the kinematics left by the previous position stage
+    CLK(stats, STAT_T_IK);
+    kinematics_wave(E);
+    CLK(stats, STAT_T_KIN);
+  }
+  XSYNC();
+  if (w == 0) {
+    CLK_DECL;
+    dynamics_wave(E);
+    CLK(stats, STAT_T_DYN);
+  } else {
+    CLK_DECL;
+    collide_wave(E, false);
+    CLK(stats, STAT_T_COL);  // wave 1's lane 0 (its own stats slot)
+  }
+  XSYNC();
+  if (w == 0) {
+    CLK_DECL;
+    make_constraints_wave(E);
+    CLK(stats, STAT_T_CON);
+    float resid = 0.f;
+    const int it = newton_wave(E, max_iter, tol, resid);
+    CLK(stats, STAT_T_SOLVE);
+    integrate_wave(E);
+    CLK(stats, STAT_T_INT);
+    if (LANE == 0) {
+      stats[STAT_NEFC] += (float)E.nefc;
+      stats[STAT_NCON] += (float)E.ncon;
+      stats[STAT_SOLVER_ITER] += (float)it;
+      stats[STAT_SUBSTEPS] += 1.f;
+      stats[STAT_RESID] = fmaxf(stats[STAT_RESID], resid);
+    }
+  }
+  // no trailing barrier: wave 1's next phase (collision) waits at the XSYNC after the next
+  // position stage, which wave 0 reaches only after finishing this substep
+#endif
 }
 
 // The whole PickPlaceGymEnv.step in ONE launch per env step (product path): the 16 substeps
 // loop inside the workgroup, so per-env cost variation averages out over the step instead of
 // stretching 16 separate launch tails (measured: one launch per substep ran 40 % slower).
-extern "C" __global__ void __launch_bounds__(WG) mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert,
-                                                                     int base) {
+extern "C" __global__ void __launch_bounds__(STEP_WG) __attribute__((amdgpu_waves_per_eu(2, 2)))
+mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert, int base) {
   EnvSh& E = g_E;
   __shared__ float act[12];
   const int i = base + blockIdx.x;
   if (i >= S.N) return;
-  load_env(S, i, E);
-  if (LANE == 0) {
-    if (expert) expert_plan(S, i, obj_pos(E, EPI(EPI_OBJ)), hand_pos(E), MMX_NSUBSTEP, act);
-    else
-      for (int k = 0; k < adim && k < 12; k++) act[k] = action[(size_t)i * adim + k];
-    decode_lane0(S, i, E, act);
+  const bool w0 = STEP_WG == 64 || WAVE_ID == 0;
+  if (w0) {
+    load_env(S, i, E);
+    if (LANE == 0) {
+      if (expert) expert_plan(S, i, obj_pos(E, EPI(EPI_OBJ)), hand_pos(E), MMX_NSUBSTEP, act);
+      else
+        for (int k = 0; k < adim && k < 12; k++) act[k] = action[(size_t)i * adim + k];
+      decode_lane0(S, i, E, act);
+    }
+    SYNC();
   }
-  SYNC();
+  XSYNC();
   for (int sub = 0; sub < MMX_NSUBSTEP; sub++) substep(S.solver_max_iter, S.solver_tol);
-  step_end(S, i, E, expert != 0);
-  store_env(S, i, E);
+  if (w0) {
+    step_end(S, i, E, expert != 0);
+    store_env(S, i, E);
+  }
 }
 
 // mj_forward position stage only (kinematics -> IK cache) + observation refresh
@@ -2275,7 +2348,7 @@ extern "C" hipError_t mmx_launch_reset(const MMXState* S, const unsigned char* m
 extern "C" hipError_t mmx_launch_step(const MMXState* S, const float* action, int adim, int expert, int base,
                                       int count, hipStream_t st) {
   if (count <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mmx_env_step_kernel, dim3(count), dim3(WG), 0, st, *S, action, adim, expert, base);
+  hipLaunchKernelGGL(mmx_env_step_kernel, dim3(count), dim3(STEP_WG), 0, st, *S, action, adim, expert, base);
   return hipGetLastError();
 }
 extern "C" hipError_t mmx_launch_expert(const MMXState* S, int n, float* action, hipStream_t st) {

@@ -125,10 +125,31 @@ def rollout_speed(N=4096, steps=100, warm=50):
     return {"env_steps_per_s": N * steps / dt, "ms_per_step": 1000 * dt / steps, "solver": env.solver_stats()}
 
 
+def nefc_dist(N=4096, steps=400):
+    """Probe set 12 build: max nefc / ncon per env over a C3 rollout, substeps with nefc > 192 / 224."""
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    env = PickPlaceVecEnv(N, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
+                          autoreset=True)
+    env.reset(seed=[_lib.episode_seed(42, i) for i in range(N)])
+    env.clear_stats()
+    env.rollout_expert(steps)
+    torch.cuda.synchronize()
+    st = env.sim.view("stats", _lib.STAT_N).double().cpu().numpy()
+    sub = st[:, 3].sum()
+    mx = st[:, 13]
+    return {"substeps": float(sub), "max_nefc": float(mx.max()), "p999_env_max_nefc": float(np.quantile(mx, 0.999)),
+            "p99_env_max_nefc": float(np.quantile(mx, 0.99)), "max_ncon": float(st[:, 14].max()),
+            "frac_nefc_gt192": float(st[:, 15].sum() / sub), "frac_nefc_gt224": float(st[:, 16].sum() / sub),
+            "mean_nefc": float(st[:, 0].sum() / sub),
+            "efc_overflow_envs": int(((env.env_error & 2) != 0).sum()) if hasattr(env, "env_error") else -1}
+
+
 if __name__ == "__main__":
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     for name, fn in [("phys1", lambda: physics_parity(1)), ("phys16", lambda: physics_parity(16)),
-                     ("gym", gym_parity), ("expert", expert_success), ("speed", rollout_speed)]:
+                     ("gym", gym_parity), ("expert", expert_success), ("speed", rollout_speed),
+                     ("nefc", nefc_dist)]:
         if len(sys.argv) > 1 and name not in sys.argv[1:]:
             continue
         t = time.time()
