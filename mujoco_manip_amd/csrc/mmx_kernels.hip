@@ -49,38 +49,87 @@ static constexpr int kBinBody[3] = {MMX_BODY_BIN_RED, MMX_BODY_BIN_GREEN, MMX_BO
 
 // ============================================================================ per-env LDS
 struct EnvSh {
-  float qpos[32], qvel[28], ctrl[8], ws[28];
-  float kin[KIN_N + 2];
+  float qpos[30], qvel[28], ctrl[8], ws[28];
   float target[4];
   float bx[NSLOT][3], bR[NSLOT][9];
   float S[9][6];
-  float Ic[12][10];  // composite inertias (m, h, J) of arm bodies
-  float M[27][LD];
-  float qfrc[LD], qacc_s[LD], x[LD], g[LD], p[LD];
-  float bias[9];
+  // mass matrix: the arm's 9 x 9 block (the 3 free cubes are separate trees whose 6 x 6 blocks are
+  // diagonal: mass x3, principal inertia x3, centre of mass at the joint)
+  float M9[9][9];
+  float Mc[18];
+  float qfrc[LD], qacc_s[LD], x[LD], p[LD];
   float con[MMX_MAXCON][CON_F];
   int conkey[MMX_MAXCON];
   // constraint rows in block format: a row touches at most two dof blocks (arm = 9 dofs,
   // cube k = 6 dofs); J[i][0..n0) holds block b0's columns, J[i][n0..n0+n1) block b1's;
   // J doubles as the contact-sort scratch in collide_wave (rows are built after it)
-  alignas(16) float J[MMX_MAXEFC][16];  // slot 15 (and any slot past the row's width) = 0
-  // (+8 pad: the MFMA pass reads whole 4-row groups past nefc)
-  alignas(16) int hdr[MMX_MAXEFC + 8];  // b0 | b1 << 4 | eq << 8 (block 15 = none)
-  alignas(16) float r[MMX_MAXEFC + 8], s[MMX_MAXEFC + 8];
-  float aref[MMX_MAXEFC], D[MMX_MAXEFC];
-  float Lrow[27][27];  // Newton Cholesky factor, row-major (read back as columns)
-  float obs[MMX_NOBS + 3];
-  int ncon, nefc, flags, iters;
+  alignas(16) float J[MMX_MAXEFC][16];  // slots past the row's width = 0; slot 15 = the row's aref
+  unsigned char hdr[MMX_MAXEFC];  // b0 | b1 << 4 (block 15 = none); row 0 is the equality
+  // D: the row's 1 / R while the rows are built (doubling as the row -> contact map before) and in
+  // the solver's setup; then the Newton iterations' active weights s
+  float D[MMX_MAXEFC];
+  int ncon, nefc, flags;
+  int ncls[3];    // collision candidates per narrowphase class (plane, box-box, GJK)
   int tbase[11];  // rows are grouped by block-pair type: type t owns rows [tbase[t], tbase[t+1])
-  int act_unclamped[8];
+  int act_free;  // bit a: actuator a's force is inside its forcerange (its kv enters qDeriv)
   float stats[STAT_N];  // lane 0 accumulates; loaded / stored with the env record
 };
 // The workgroup's env lives in one file-scope LDS object: the non-inlined substep function below
 // reaches it by symbol (LDS address space), not through a generic pointer.
 static __shared__ EnvSh g_E;
+
+// E.J is the phases' scratch outside the constraint build + Newton solve (rows are rebuilt every
+// substep): the collision layout below, the position stage's chain scan, the IK system, the RNE /
+// composite-inertia / actuator scratch of the dynamics (at COL_WORK: the two-wave step runs the
+// dynamics beside the collision prune, which only touches [0, COL_WORK)) and the observation of
+// the step end.  The Newton Hessian staging tile and Cholesky transpose live in E.con instead
+// (contacts are dead once the rows exist; the last substep stores them to HBM first).
+#define COL_GX 0      // [NGEOM][16] world pose (x3, R9), rbound, type
+#define COL_CAND 768  // [COL_LIST] candidate pairs after the sphere test, then grouped by class
+#define COL_LIST 784
+#define COL_WORK (COL_CAND + COL_LIST)  // narrowphase work space: box-box polygons and (beside
+#define COL_POLY 48                     // them) the EPA polytope, then the contact sort
+#define COL_PLANES 32                   // lanes that clip box-box polygons at a time
+#define COL_EPA (COL_WORK + COL_PLANES * COL_POLY)
+static_assert(COL_EPA + EPA_SCRATCH_FLOATS <= MMX_MAXEFC * 16, "box-box polygons + EPA scratch exceed E.J");
+static_assert(COL_WORK + MMX_MAXCON * CON_F <= MMX_MAXEFC * 16, "contact sort exceeds E.J");
+static_assert(MMX_NGEOM * 16 <= COL_CAND && MMX_NPAIR <= COL_LIST && MMX_NPAIR < 4096, "collision scratch layout");
+
+#define SCR_DYN COL_WORK           // RNE frc + inertia [12][16], subtree force [12][6] (264), then:
+#define SCR_IC (SCR_DYN + 272)     // composite inertias [12][10]
+#define SCR_AF (SCR_IC + 120)      // actuator forces [8]
+#define SCR_BIAS (SCR_AF + 8)      // RNE bias force of the arm dofs [9]
+#define SCR_OBS 4496               // observation (step end, reset, forward)
+#define SCR_ACT 4592               // raw action of the step (lane 0, before the substeps)
+static_assert(SCR_BIAS + 9 <= 4096 && SCR_OBS + MMX_NOBS <= SCR_ACT && SCR_ACT + 12 <= MMX_MAXEFC * 16,
+              "E.J scratch layout");
+static_assert(27 * 27 <= MMX_MAXCON * CON_F, "Newton Cholesky transpose exceeds E.con");
+DEV float* scr_of(EnvSh& E) { return &E.J[0][0]; }
+DEV float* obs_of(EnvSh& E) { return &E.J[0][0] + SCR_OBS; }
+DEV const float* obs_of(const EnvSh& E) { return &E.J[0][0] + SCR_OBS; }
+DEV float* lrow_of(EnvSh& E) { return &E.con[0][0]; }  // [27][27] Newton factor / staging tile
+// the last substep's contacts (diagnostic copy, mmx_buffers.contacts), stored once the rows are
+// built: the solver then reuses E.con as scratch
+DEV void store_contacts(float* dst, const EnvSh& E) {
+  const int n = E.ncon;
+  for (int k = LANE; k < MMX_MAXCON * CON_F; k += WG) dst[k] = k < n * CON_F ? (&E.con[0][0])[k] : 0.f;
+}
+DEV float* contacts_dst(const MMXState& S, int i) { return S.con + (size_t)i * MMX_MAXCON * CON_F; }
 enum { SHF_ROBOT_OBST = 1, SHF_CON_OVF = 2, SHF_EFC_OVF = 4, SHF_NAN = 8 };
 
 DEV int body_slot(int b) { return b <= 11 ? b - 1 : b - 5; }
+// The IK's kinematics cache (KIN_*: hand pose, arm joint axes and anchors of the last position
+// stage, the HBM record's kin[]) is not a separate LDS array: its entries ARE the position
+// stage's outputs (hand slot of bx / bR, angular part of S, joint bodies' bx), which stay
+// untouched from one position stage to the next IK.  load_env scatters the record into them,
+// store_env gathers it back.
+DEV float& kin_ref(EnvSh& E, int k) {
+  if (k < KIN_HAND_MAT) return E.bx[body_slot(MMX_BODY_HAND)][k - KIN_HAND_POS];
+  if (k < KIN_AXIS) return E.bR[body_slot(MMX_BODY_HAND)][k - KIN_HAND_MAT];
+  if (k < KIN_ANCHOR) return E.S[(k - KIN_AXIS) / 3][(k - KIN_AXIS) % 3];
+  return E.bx[body_slot(MMX_jnt_body[(k - KIN_ANCHOR) / 3])][(k - KIN_ANCHOR) % 3];
+}
+DEV float kin_get(const EnvSh& E, int k) { return kin_ref(const_cast<EnvSh&>(E), k); }
 DEV int body_block(int b) { return (b >= 2 && b <= 11) ? 0 : (b >= 16 ? b - 15 : -1); }
 #define BLK_NONE 15
 DEV int blk_size(int b) { return b == 0 ? 9 : (b == BLK_NONE ? 0 : 6); }
@@ -177,10 +226,6 @@ DEV void kinematics_lane0(EnvSh& E) {
         const V3 lin = cross(pos, axw);
         E.S[j][0] = axw.x; E.S[j][1] = axw.y; E.S[j][2] = axw.z;
         E.S[j][3] = lin.x; E.S[j][4] = lin.y; E.S[j][5] = lin.z;
-        if (j < 7) {
-          E.kin[KIN_AXIS + 3 * j] = axw.x; E.kin[KIN_AXIS + 3 * j + 1] = axw.y; E.kin[KIN_AXIS + 3 * j + 2] = axw.z;
-          E.kin[KIN_ANCHOR + 3 * j] = pos.x; E.kin[KIN_ANCHOR + 3 * j + 1] = pos.y; E.kin[KIN_ANCHOR + 3 * j + 2] = pos.z;
-        }
       } else {  // slide
         E.S[j][0] = 0.f; E.S[j][1] = 0.f; E.S[j][2] = 0.f;
         E.S[j][3] = axw.x; E.S[j][4] = axw.y; E.S[j][5] = axw.z;
@@ -205,10 +250,6 @@ DEV void kinematics_lane0(EnvSh& E) {
 #pragma unroll
     for (int k = 0; k < 9; k++) E.bR[s][k] = R.m[k];
   }
-  const int hs = body_slot(MMX_BODY_HAND);
-  E.kin[KIN_HAND_POS] = E.bx[hs][0]; E.kin[KIN_HAND_POS + 1] = E.bx[hs][1]; E.kin[KIN_HAND_POS + 2] = E.bx[hs][2];
-#pragma unroll
-  for (int k = 0; k < 9; k++) E.kin[KIN_HAND_MAT + k] = E.bR[hs][k];
 }
 
 // Wave form of kinematics_lane0: one lane per body.  Each arm body first builds its local
@@ -216,7 +257,7 @@ DEV void kinematics_lane0(EnvSh& E) {
 // cover the 10-deep finger chain): T_b <- T_anc(b) o T_b, anc(b) <- anc(anc(b)).  Cubes read their
 // free joints directly.  Results equal kinematics_lane0 up to fp32 association order.
 DEV void kinematics_wave(EnvSh& E) {
-  float* T = &E.Lrow[0][0];  // [12][8] scan scratch: q (4), p (3), ancestor (Lrow is free here)
+  float* T = scr_of(E);  // [12][8] scan scratch: q (4), p (3), ancestor
   const int b = LANE + 1;    // lanes 0..10 -> arm bodies 1..11
   Q4 q = Q4{1.f, 0.f, 0.f, 0.f};
   V3 p = V3{0.f, 0.f, 0.f};
@@ -267,19 +308,10 @@ DEV void kinematics_wave(EnvSh& E) {
         const V3 lin = cross(p, axw);
         E.S[j][0] = axw.x; E.S[j][1] = axw.y; E.S[j][2] = axw.z;
         E.S[j][3] = lin.x; E.S[j][4] = lin.y; E.S[j][5] = lin.z;
-        if (j < 7) {
-          E.kin[KIN_AXIS + 3 * j] = axw.x; E.kin[KIN_AXIS + 3 * j + 1] = axw.y; E.kin[KIN_AXIS + 3 * j + 2] = axw.z;
-          E.kin[KIN_ANCHOR + 3 * j] = p.x; E.kin[KIN_ANCHOR + 3 * j + 1] = p.y; E.kin[KIN_ANCHOR + 3 * j + 2] = p.z;
-        }
       } else {
         E.S[j][0] = 0.f; E.S[j][1] = 0.f; E.S[j][2] = 0.f;
         E.S[j][3] = axw.x; E.S[j][4] = axw.y; E.S[j][5] = axw.z;
       }
-    }
-    if (b == MMX_BODY_HAND) {
-      E.kin[KIN_HAND_POS] = p.x; E.kin[KIN_HAND_POS + 1] = p.y; E.kin[KIN_HAND_POS + 2] = p.z;
-#pragma unroll
-      for (int k = 0; k < 9; k++) E.kin[KIN_HAND_MAT + k] = R.m[k];
     }
   } else if (LANE < 14) {  // cubes: free joints
     const int c = LANE - 11, qa = 9 + 7 * c;
@@ -335,46 +367,12 @@ DEV RI ri_load(const float* d) {
 
 #define LT(r, c) ((r) * ((r) + 1) / 2 + (c))
 
-// lane 0: RNE bias of the arm + composite inertias (for CRBA)
-DEV void rne_lane0(EnvSh& E) {
-  RI Ib[12];
-#pragma unroll
-  for (int b = 2; b <= 11; b++) Ib[b] = body_inertia(E, b);
-  SV vel[12], acc[12], frc[12];
-  vel[1] = SV{V3{0.f, 0.f, 0.f}, V3{0.f, 0.f, 0.f}};
-  acc[1] = SV{V3{0.f, 0.f, 0.f}, V3{0.f, 0.f, -MMX_GRAVITY_Z}};  // base acceleration = -gravity
-#pragma unroll
-  for (int b = 2; b <= 11; b++) {
-    const int p = MMX_body_parent[b];
-    const int j = MMX_body_jnt[b];
-    vel[b] = vel[p];
-    acc[b] = acc[p];
-    if (j >= 0) {
-      const SV vj = load_S(E, j) * E.qvel[j];
-      acc[b] = acc[b] + cross_motion(vel[p], vj);
-      vel[b] = vel[b] + vj;
-    }
-    frc[b] = rimul(Ib[b], acc[b]) + cross_force(vel[b], rimul(Ib[b], vel[b]));
-  }
-#pragma unroll
-  for (int b = 11; b >= 3; b--) {
-    const int p = MMX_body_parent[b];
-    frc[p] = frc[p] + frc[b];
-  }
-#pragma unroll
-  for (int d = 0; d < 9; d++) E.bias[d] = sdot(load_S(E, d), frc[MMX_jnt_body[d]]);
-#pragma unroll
-  for (int b = 11; b >= 3; b--) riadd(Ib[MMX_body_parent[b]], Ib[b]);
-#pragma unroll
-  for (int b = 2; b <= 11; b++) ri_store(E.Ic[b], Ib[b]);
-}
-
-// Wave form of rne_lane0: one lane per moving arm body (2..11).  A body's velocity and
+// RNE bias of the arm + composite inertias (for CRBA), one lane per moving arm body (2..11).  A body's velocity and
 // acceleration are running sums over the joints on its root path (arm_anc), its force is local;
 // subtree sums of force and inertia (the backward pass and the composite inertia) are gathers
-// over descendants.  Scratch in E.Lrow: per body frc (6) + inertia (10), then subtree force (6).
+// over descendants.  Scratch at SCR_DYN: per body frc (6) + inertia (10), then subtree force (6).
 DEV void rne_wave(EnvSh& E) {
-  float* F = &E.Lrow[0][0];
+  float* F = scr_of(E) + SCR_DYN;
   const int b = LANE + 2;
   if (LANE < 10) {
     const RI Ib = body_inertia(E, b);
@@ -408,7 +406,7 @@ DEV void rne_wave(EnvSh& E) {
       for (int m = 0; m < 10; m++) is[m] += in ? o[6 + m] : 0.f;
     }
 #pragma unroll
-    for (int m = 0; m < 10; m++) E.Ic[b][m] = is[m];
+    for (int m = 0; m < 10; m++) (scr_of(E) + SCR_IC)[10 * b + m] = is[m];
     float* o = F + 16 * 12 + 6 * b;
 #pragma unroll
     for (int m = 0; m < 6; m++) o[m] = fs[m];
@@ -416,7 +414,7 @@ DEV void rne_wave(EnvSh& E) {
   SYNC();
   if (LANE < 9) {
     const float* o = F + 16 * 12 + 6 * MMX_jnt_body[LANE];
-    E.bias[LANE] = sdot(load_S(E, LANE), SV{V3{o[0], o[1], o[2]}, V3{o[3], o[4], o[5]}});
+    (scr_of(E) + SCR_BIAS)[LANE] = sdot(load_S(E, LANE), SV{V3{o[0], o[1], o[2]}, V3{o[3], o[4], o[5]}});
   }
   SYNC();
 }
@@ -469,29 +467,28 @@ DEV void dynamics_wave(EnvSh& E) {
   CLK_DECL;
   rne_wave(E);
   PROBE(11, stats, STAT_T_AUX0);
-  for (int idx = LANE; idx < 27 * LD; idx += WG) (&E.M[0][0])[idx] = 0.f;
-  SYNC();
   if (LANE < 45) {
     int d, e;
     tri_index(LANE, d, e);
     float v = 0.f;
     if (e == d || (e <= 6 && !(d == 8 && e == 7))) {  // fingers 7, 8 are siblings
-      const RI Ic = ri_load(E.Ic[MMX_jnt_body[d]]);
+      const RI Ic = ri_load(scr_of(E) + SCR_IC + 10 * MMX_jnt_body[d]);
       v = sdot(load_S(E, e), rimul(Ic, load_S(E, d)));
     }
     if (d == e) v += MMX_dof_armature[d];
-    E.M[d][e] = v;
-    E.M[e][d] = v;
+    E.M9[d][e] = v;
+    E.M9[e][d] = v;
   } else if (LANE < 45 + 18) {
     const int k = LANE - 45, c = k / 6, rr = k % 6, b = 16 + c;
-    E.M[9 + k][9 + k] = rr < 3 ? MMX_body_mass[b] : MMX_body_inertia[9 * b + 4 * (rr - 3)];
+    E.Mc[k] = rr < 3 ? MMX_body_mass[b] : MMX_body_inertia[9 * b + 4 * (rr - 3)];
   }
   SYNC();
   PROBE(11, stats, STAT_T_AUX1);
   // smooth force: passive damping - bias + actuation (arm; one lane per actuator, then per dof),
   // gravity + gyroscopic (cubes, one lane each); arm qacc_smooth = M_arm^{-1} qfrc by a register
   // Cholesky (rows in lanes 0..8)
-  float* af = &E.Lrow[0][0];  // actuator forces (Lrow is free after the RNE)
+  float* af = scr_of(E) + SCR_AF;  // actuator forces
+  bool unclamped = false;
   if (LANE < 8) {
     const int a = LANE;
     const float c = fminf(fmaxf(E.ctrl[a], MMX_act_ctrlrange[2 * a]), MMX_act_ctrlrange[2 * a + 1]);
@@ -500,14 +497,16 @@ DEV void dynamics_wave(EnvSh& E) {
     const float tvel = MMX_tendon_coef[0] * E.qvel[7] + MMX_tendon_coef[1] * E.qvel[8];
     const float len = j >= 0 ? E.qpos[j] : tlen, vel = j >= 0 ? E.qvel[j] : tvel;
     float f = MMX_act_gain[a] * c + MMX_act_bias[3 * a] + MMX_act_bias[3 * a + 1] * len + MMX_act_bias[3 * a + 2] * vel;
-    E.act_unclamped[a] = f > MMX_act_forcerange[2 * a] && f < MMX_act_forcerange[2 * a + 1];
+    unclamped = f > MMX_act_forcerange[2 * a] && f < MMX_act_forcerange[2 * a + 1];
     af[a] = fminf(fmaxf(f, MMX_act_forcerange[2 * a]), MMX_act_forcerange[2 * a + 1]);
   }
+  const unsigned free_mask = (unsigned)__ballot(unclamped);
+  if (LANE == 0) E.act_free = (int)free_mask;
   SYNC();
   float qf = 0.f;
   if (LANE < 9) {
     const int d = LANE;
-    qf = -MMX_dof_damping[d] * E.qvel[d] - E.bias[d];
+    qf = -MMX_dof_damping[d] * E.qvel[d] - (scr_of(E) + SCR_BIAS)[d];
 #pragma unroll
     for (int a = 0; a < 8; a++) {  // actuator order as the serial accumulation
       const int j = MMX_act_trn_joint[a];
@@ -529,7 +528,7 @@ DEV void dynamics_wave(EnvSh& E) {
   float arow[9];
   const int jr = min(LANE, 8);
 #pragma unroll
-  for (int e = 0; e < 9; e++) arow[e] = E.M[jr][e];
+  for (int e = 0; e < 9; e++) arow[e] = E.M9[jr][e];
   PROBE(11, stats, STAT_T_AUX2);
   const float xs = chol_solve_small<9>(arow, qf, 1e-12f);
   if (LANE < 9) E.qacc_s[LANE] = xs;
@@ -601,17 +600,6 @@ struct WaveSink {
   }
 };
 
-// LDS scratch layout of the collision phase (inside E.J, which is rebuilt after collision)
-#define COL_GX 0      // [NGEOM][16] world pose (x3, R9), rbound, type
-#define COL_CAND 768  // [COL_LIST] candidate pairs (pair | class << 12) after the sphere test
-#define COL_LIST 784
-#define COL_WORK (COL_CAND + COL_LIST)  // narrowphase work space: box-box polygons, EPA polytope,
-#define COL_POLY 48                     // then the contact sort (each used after the previous)
-static_assert(COL_WORK + WG * COL_POLY <= MMX_MAXEFC * 16, "box-box polygons exceed E.J");
-static_assert(COL_WORK + EPA_SCRATCH_FLOATS <= MMX_MAXEFC * 16, "EPA scratch exceeds E.J");
-static_assert(COL_WORK + MMX_MAXCON * CON_F <= MMX_MAXEFC * 16, "contact sort exceeds E.J");
-static_assert(MMX_NGEOM * 16 <= COL_CAND && MMX_NPAIR <= COL_LIST && MMX_NPAIR < 4096, "collision scratch layout");
-
 DEV Geom geom_lds(const float* gx, int g) {
   const float* o = gx + 16 * g;
   Geom G;
@@ -642,11 +630,14 @@ DEV int wave_compact(bool keep, int* list, int base, int val) {
 }
 
 // Collision in coherent stages: (1) world poses of all geoms into LDS, one lane per geom;
-// (2) bounding-sphere / plane-distance prune of all pairs, compacted with ballots; (3) OBB prune
-// and split by narrowphase class; (4) one pass per class (plane-convex/box, box-box, GJK/EPA), so
-// lanes of a pass run the same code; (5) deterministic rank sort of the contacts by pair key.
-// Every prune is conservative, so the contact set equals the all-pairs narrowphase.
-DEV void collide_wave(EnvSh& E, bool only_ro) {
+// (2) bounding-sphere / plane-distance prune of all pairs, compacted with ballots; (3) OBB prune,
+// split by narrowphase class into per-class lists (E.ncls); (4) one pass per class (plane-convex
+// / box lane per pair, box-box lane per pair, GJK/EPA one pair per wave), so lanes of a pass run
+// the same code; (5) deterministic rank sort of the contacts by pair key.  Every prune is
+// conservative, so the contact set equals the all-pairs narrowphase.  (1)-(3), (4) and (5) are
+// separate functions: the two-wave env step runs (4)'s lane-per-pair classes on one wave and the
+// GJK pairs on the other (their contacts meet through the LDS atomic slot counter).
+DEV void collide_prune(EnvSh& E, bool only_ro) {
   float* stats = E.stats;
   CLK_DECL;
   if (LANE == 0) {
@@ -698,22 +689,43 @@ DEV void collide_wave(EnvSh& E, bool only_ro) {
   }
   SYNC();
   PROBE(2, stats, STAT_T_AUX1);
-  // (3) OBB prune; the class (0 plane, 1 box-box, 2 GJK, 3 pruned) is stored with the pair
+  // (3) OBB prune and class (0 plane, 1 box-box, 2 GJK, 3 pruned); then the candidates are
+  // regrouped in place as [plane | box-box | GJK], each group in candidate (pair) order
+  constexpr int NCP = (COL_LIST + WG - 1) / WG;
+  int ce[NCP];
   int ncls[3] = {0, 0, 0};
-  for (int base = 0; base < nc; base += WG) {
-    const int k = base + LANE;
-    int c = 3;
-    if (k < nc) {
-      const int p = cand[k];
-      int g1, g2;
-      pair_geoms(gx, p, g1, g2);
-      const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
-      if (A.type == GT_PLANE) c = 0;
-      else if (obb_overlap(A, B)) c = (A.type == GT_BOX && B.type == GT_BOX) ? 1 : 2;
-      cand[k] = p | (c << 12);
-    }
 #pragma unroll
-    for (int q = 0; q < 3; q++) ncls[q] += __popcll(__ballot(c == q));
+  for (int q = 0; q < NCP; q++) {
+    const int k = q * WG + LANE;
+    int c = 3, p = 0;
+    if (q * WG < nc) {
+      if (k < nc) {
+        p = cand[k];
+        int g1, g2;
+        pair_geoms(gx, p, g1, g2);
+        const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
+        if (A.type == GT_PLANE) c = 0;
+        else if (obb_overlap(A, B)) c = (A.type == GT_BOX && B.type == GT_BOX) ? 1 : 2;
+      }
+#pragma unroll
+      for (int t = 0; t < 3; t++) ncls[t] += __popcll(__ballot(c == t));
+    }
+    ce[q] = p | (c << 12);
+  }
+  SYNC();
+  int base[3] = {0, ncls[0], ncls[0] + ncls[1]};
+#pragma unroll
+  for (int q = 0; q < NCP; q++) {
+    if (q * WG < nc) {
+      const int c = ce[q] >> 12;
+#pragma unroll
+      for (int t = 0; t < 3; t++) base[t] = wave_compact(c == t, cand, base[t], ce[q] & 4095);
+    }
+  }
+  if (LANE == 0) {
+    E.ncls[0] = ncls[0];
+    E.ncls[1] = ncls[1];
+    E.ncls[2] = ncls[2];
   }
   SYNC();
   if (MMX_PROBE == 4 && LANE == 0) {
@@ -724,49 +736,64 @@ DEV void collide_wave(EnvSh& E, bool only_ro) {
   }
   PROBE(2, stats, STAT_T_AUX2);
   PROBE(5, stats, STAT_T_AUX3);
-  // (4) narrowphase, one pass per class over the candidate list: lanes of a class run together
-  V3* poly = reinterpret_cast<V3*>(scr + COL_WORK + COL_POLY * LANE);
-#pragma unroll
-  for (int q = 0; q < 2; q++) {  // lane per pair
-    if (ncls[q] == 0) continue;
-    for (int base = 0; base < nc; base += WG) {
-      const int k = base + LANE;
-      const int e = k < nc ? cand[k] : (3 << 12);
-      if ((e >> 12) == q) {
-        const int p = e & 4095;
-        int g1, g2;
-        pair_geoms(gx, p, g1, g2);
-        const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
-        WaveSink cs(&E, p, !only_ro, g1, g2);
-        if (q == 0) {
-          if (B.type == GT_BOX) plane_box(cs, A, B);
-          else if (B.type == GT_MESH) plane_convex(cs, A, B);
-        } else {
-          box_box(cs, A, B, poly, poly + 8);
-        }
-      }
-    }
-    SYNC();
-    if (q == 0) PROBE(5, stats, STAT_T_AUX0);
-    else PROBE(5, stats, STAT_T_AUX1);
-  }
-  // GJK / EPA pairs: the whole wave on one pair at a time (EPA polytope in the work space)
-  if (ncls[2] > 0) {
-    for (int k = 0; k < nc; k++) {
-      const int e = cand[k];
-      if ((e >> 12) != 2) continue;
-      const int p = e & 4095;
+}
+
+// (4) narrowphase over the class lists of collide_prune: which & 1 = plane pairs and box-box
+// pairs (lane per pair), which & 2 = GJK/EPA pairs (the whole wave on one pair at a time, EPA
+// polytope in LDS beside the box-box polygons)
+DEV void collide_pairs(EnvSh& E, bool only_ro, int which) {
+  float* stats = E.stats;
+  CLK_DECL;
+  float* scr = &E.J[0][0];
+  const float* gx = scr + COL_GX;
+  const int* cand = reinterpret_cast<const int*>(scr + COL_CAND);
+  const int n0 = E.ncls[0], n1 = E.ncls[1], n2 = E.ncls[2];
+  if (which & 1) {
+    for (int k = LANE; k < n0; k += WG) {  // plane-box / plane-convex
+      const int p = cand[k];
       int g1, g2;
       pair_geoms(gx, p, g1, g2);
       const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
       WaveSink cs(&E, p, !only_ro, g1, g2);
-      convex_convex(cs, A, B, scr + COL_WORK);
+      if (B.type == GT_BOX) plane_box(cs, A, B);
+      else if (B.type == GT_MESH) plane_convex(cs, A, B);
     }
+    SYNC();
+    PROBE(5, stats, STAT_T_AUX0);
+    V3* poly = reinterpret_cast<V3*>(scr + COL_WORK + COL_POLY * min(LANE, COL_PLANES - 1));
+    for (int k0 = 0; k0 < n1; k0 += COL_PLANES) {  // box-box
+      const int k = k0 + LANE;
+      if (LANE < COL_PLANES && k < n1) {
+        const int p = cand[n0 + k];
+        int g1, g2;
+        pair_geoms(gx, p, g1, g2);
+        const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
+        WaveSink cs(&E, p, !only_ro, g1, g2);
+        box_box(cs, A, B, poly, poly + 8);
+      }
+    }
+    SYNC();
+    PROBE(5, stats, STAT_T_AUX1);
   }
-  SYNC();
-  PROBE(2, stats, STAT_T_AUX3);
-  PROBE(5, stats, STAT_T_AUX2);
-  if (only_ro) return;
+  if (which & 2) {
+    for (int k = 0; k < n2; k++) {  // GJK / EPA
+      const int p = cand[n0 + n1 + k];
+      int g1, g2;
+      pair_geoms(gx, p, g1, g2);
+      const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
+      WaveSink cs(&E, p, !only_ro, g1, g2);
+      convex_convex(cs, A, B, scr + COL_EPA);
+    }
+    SYNC();
+    PROBE(5, stats, STAT_T_AUX2);
+  }
+}
+
+// (5) deterministic order: rank sort of the contacts by their 16-bit pair/order key
+DEV void collide_sort(EnvSh& E) {
+  float* stats = E.stats;
+  CLK_DECL;
+  float* scr = &E.J[0][0];
   const int n = min(E.ncon, MMX_MAXCON);
   float* tmp = scr + COL_WORK;
   int kb = 0, rank = 0;
@@ -785,6 +812,12 @@ DEV void collide_wave(EnvSh& E, bool only_ro) {
   PROBE(5, stats, STAT_T_AUX3);
 }
 
+DEV void collide_wave(EnvSh& E, bool only_ro) {
+  collide_prune(E, only_ro);
+  collide_pairs(E, only_ro, 3);
+  if (!only_ro) collide_sort(E);
+}
+
 // ============================================================================ constraints (wave)
 // Soft-constraint reference terms of a row: K, B from solref, impedance from solimp (MuJoCo
 // mj_makeImpedance); D = 1 / R with R = (1 - imp) / imp * diag.
@@ -801,38 +834,41 @@ DEV void store_row(EnvSh& E, int row, const float* jv, int hdr, float vel, float
                    float diag) {
   float4* Jr = reinterpret_cast<float4*>(E.J[row]);
 #pragma unroll
-  for (int q = 0; q < 4; q++) Jr[q] = make_float4(jv[4 * q], jv[4 * q + 1], jv[4 * q + 2], jv[4 * q + 3]);
-  E.hdr[row] = hdr;
-  E.aref[row] = -B * vel - kid;
+  for (int q = 0; q < 3; q++) Jr[q] = make_float4(jv[4 * q], jv[4 * q + 1], jv[4 * q + 2], jv[4 * q + 3]);
+  Jr[3] = make_float4(jv[12], jv[13], jv[14], -B * vel - kid);  // slot 15: aref
+  E.hdr[row] = (unsigned char)hdr;
   E.D[row] = 1.f / fmaxf(imp_ratio * diag, 1e-15f);
 }
 
-// per-contact row generator, written by the contact's lane and read by its rows' lanes
-// (kept in E.r / E.s, which the solver overwrites later)
-enum { CG_T1 = 0, CG_IMPR = 3, CG_KID, CG_B, CG_TRAN, CG_ROT, CG_MU0, CG_MU1, CG_N };
+// per-contact row generator, written by the contact's lane into fields of its own contact record
+// that the rows no longer need (distance, torsional friction, geom ids) and read by its rows'
+// lanes: impedance ratio x translational / rotational invweight, K imp pos, B.  The contacts are
+// copied to HBM (last substep) before this overwrite.
+enum { CG_IT = CON_DIST, CG_IR = CON_MU2, CG_KID = CON_G1, CG_B = CON_G2 };
+DEV V3 contact_t1(V3 n) {  // mju_makeFrame's first tangent
+  const V3 y = (n.y < 0.5f && n.y > -0.5f) ? V3{0.f, 1.f, 0.f} : V3{0.f, 0.f, 1.f};
+  return normalize(y - n * dot(n, y));
+}
 
 // one pyramid row (rr) of contact c, built straight into block format: an arm block entry is
 // the motion subspace of dof d seen at the contact point, a cube block the free-body Jacobian
 DEV void contact_row(EnvSh& E, int row, int c, int rr) {
   const float* cc = E.con[c];
-  float cgv[CG_N];
-#pragma unroll
-  for (int k = 0; k < CG_N; k++) cgv[k] = k < 5 ? E.r[5 * c + k] : E.s[5 * c + k - 5];
   const V3 p = V3{cc[CON_POS], cc[CON_POS + 1], cc[CON_POS + 2]};
   const V3 n = V3{cc[CON_N], cc[CON_N + 1], cc[CON_N + 2]};
   const int dim = (int)cc[CON_DIM];
   const int b1 = (E.conkey[c] >> 16) & 255, b2 = (E.conkey[c] >> 24) & 255;
-  const V3 t1 = V3{cgv[CG_T1], cgv[CG_T1 + 1], cgv[CG_T1 + 2]};
+  const V3 t1 = contact_t1(n);
   V3 u = n, w = V3{0.f, 0.f, 0.f};
-  float diag = cgv[CG_TRAN];
+  float idiag = cc[CG_IT];  // impedance ratio x diagApprox
   if (dim > 1) {  // pyramid edge J_n +/- mu_k J_k
     const int k = rr >> 1;
-    const float mu = k < 2 ? cgv[CG_MU0] : cgv[CG_MU1];
+    const float mu = k < 2 ? cc[CON_MU0] : cc[CON_MU1];
     const float sg = (rr & 1) ? -mu : mu;
     if (k == 0) u = n + t1 * sg;
     else if (k == 1) u = n + cross(n, t1) * sg;
     else w = n * sg;
-    diag = cgv[CG_TRAN] + mu * mu * (k < 2 ? cgv[CG_TRAN] : cgv[CG_ROT]);
+    idiag = cc[CG_IT] + mu * mu * (k < 2 ? cc[CG_IT] : cc[CG_IR]);
   }
   const int k1 = body_block(b1), k2 = body_block(b2);
   int rb0 = k1 >= 0 ? k1 : k2, rb1 = (k1 >= 0 && k2 >= 0 && k2 != k1) ? k2 : BLK_NONE;
@@ -887,7 +923,7 @@ DEV void contact_row(EnvSh& E, int row, int c, int rr) {
     const float vc = j < 6 ? cubeA[j] : (j < 12 ? cubeB[j - 6] : 0.f);
     jv[j] = armrow ? va : vc;
   }
-  store_row(E, row, jv, rb0 | (rb1 << 4), vel, cgv[CG_IMPR], cgv[CG_KID], cgv[CG_B], diag);
+  store_row(E, row, jv, rb0 | (rb1 << 4), vel, 1.f, cc[CG_KID], cc[CG_B], idiag);
 }
 
 // Constraint rows in MuJoCo's order per lane scan: finger equality (lane 0), joint limits
@@ -899,8 +935,9 @@ DEV void make_constraints_wave(EnvSh& E) {
   const float def_ref[2] = {0.02f, 1.0f};
   const float def_imp[5] = {0.9f, 0.95f, 0.001f, 0.5f, 2.0f};
   const int ncon = E.ncon;
-  int* rowmap = reinterpret_cast<int*>(&E.Lrow[0][0]);  // Lrow is free until the solver
-  static_assert(27 * 27 >= MMX_MAXEFC, "rowmap scratch");
+  // row -> (contact, pyramid edge) map, -1 for the equality / limit rows; it lives in E.D, so the
+  // equality / limit rows (whose store_row writes D) are stored after the contact rows
+  int* rowmap = reinterpret_cast<int*>(E.D);
   int nlim = 0, ncr = 0, dim = 0, tc = -1;
   bool lo_act = false, hi_act = false;
   if (LANE < 9) {
@@ -959,18 +996,50 @@ DEV void make_constraints_wave(EnvSh& E) {
   }
   int row = arow;
   PROBE(3, stats, STAT_T_AUX0);
+  if (LANE == 0 && row < MMX_MAXEFC) rowmap[row++] = -1;  // finger equality
+  if (LANE < 9) {
+#pragma unroll
+    for (int side = 0; side < 2; side++)
+      if ((side == 0 ? lo_act : hi_act) && row < MMX_MAXEFC) rowmap[row++] = -1;  // joint limits
+  }
+  PROBE(3, stats, STAT_T_AUX1);
+  if (LANE < ncon) {  // contact generator: mixed parameters, reference terms
+    float* c = E.con[LANE];
+    const int g1 = (int)c[CON_G1], g2 = (int)c[CON_G2];
+    const int b1 = (E.conkey[LANE] >> 16) & 255, b2 = (E.conkey[LANE] >> 24) & 255;
+    float solref[2], solimp[5];
+#pragma unroll
+    for (int k = 0; k < 2; k++) solref[k] = 0.5f * (MMX_geom_solref[2 * g1 + k] + MMX_geom_solref[2 * g2 + k]);
+#pragma unroll
+    for (int k = 0; k < 5; k++) solimp[k] = 0.5f * (MMX_geom_solimp[5 * g1 + k] + MMX_geom_solimp[5 * g2 + k]);
+    float impr, kid, B;
+    row_ref(solref, solimp, c[CON_DIST], impr, kid, B);
+    const float tran = MMX_body_invweight0[2 * b1] + MMX_body_invweight0[2 * b2];
+    const float rot = MMX_body_invweight0[2 * b1 + 1] + MMX_body_invweight0[2 * b2 + 1];
+    c[CG_IT] = impr * tran;
+    c[CG_IR] = impr * rot;
+    c[CG_KID] = kid;
+    c[CG_B] = B;
+    for (int rr = 0; rr < ncr && brow + rr < MMX_MAXEFC; rr++) rowmap[brow + rr] = LANE | (rr << 8);
+  }
+  SYNC();
+  PROBE(3, stats, STAT_T_AUX3);
+  for (int r = LANE; r < nefc; r += WG) {
+    const int m = rowmap[r];
+    if (m >= 0) contact_row(E, r, m & 255, m >> 8);
+  }
+  row = arow;
   float jv[16];
   if (LANE == 0 && row < MMX_MAXEFC) {  // finger equality (panda.xml:261)
 #pragma unroll
     for (int j = 0; j < 16; j++) jv[j] = j == 7 ? 1.f : (j == 8 ? -1.f : 0.f);
     float ir, kid, B;
     row_ref(MMX_eq_solref, MMX_eq_solimp, E.qpos[7] - E.qpos[8], ir, kid, B);
-    store_row(E, row, jv, 0 | (BLK_NONE << 4) | (1 << 8), E.qvel[7] - E.qvel[8], ir, kid, B,
+    store_row(E, row, jv, 0 | (BLK_NONE << 4), E.qvel[7] - E.qvel[8], ir, kid, B,
               MMX_dof_invweight0[7] + MMX_dof_invweight0[8]);
-    rowmap[row] = -1;
     row++;
   }
-  if (LANE < 9) {
+  if (LANE < 9) {  // joint limits (MuJoCo default solref / solimp)
     const float q = E.qpos[LANE];
 #pragma unroll
     for (int side = 0; side < 2; side++) {
@@ -983,45 +1052,9 @@ DEV void make_constraints_wave(EnvSh& E) {
         float ir, kid, B;
         row_ref(def_ref, def_imp, dist, ir, kid, B);
         store_row(E, row, jv, 0 | (BLK_NONE << 4), sg * E.qvel[LANE], ir, kid, B, MMX_dof_invweight0[LANE]);
-        rowmap[row] = -1;
         row++;
       }
     }
-  }
-  PROBE(3, stats, STAT_T_AUX1);
-  if (LANE < ncon) {  // contact generator: frame, mixed parameters, reference terms
-    const float* c = E.con[LANE];
-    const V3 n = V3{c[CON_N], c[CON_N + 1], c[CON_N + 2]};
-    const int g1 = (int)c[CON_G1], g2 = (int)c[CON_G2];
-    const int b1 = (E.conkey[LANE] >> 16) & 255, b2 = (E.conkey[LANE] >> 24) & 255;
-    const V3 y = (n.y < 0.5f && n.y > -0.5f) ? V3{0.f, 1.f, 0.f} : V3{0.f, 0.f, 1.f};  // mju_makeFrame
-    const V3 t1 = normalize(y - n * dot(n, y));
-    float solref[2], solimp[5];
-#pragma unroll
-    for (int k = 0; k < 2; k++) solref[k] = 0.5f * (MMX_geom_solref[2 * g1 + k] + MMX_geom_solref[2 * g2 + k]);
-#pragma unroll
-    for (int k = 0; k < 5; k++) solimp[k] = 0.5f * (MMX_geom_solimp[5 * g1 + k] + MMX_geom_solimp[5 * g2 + k]);
-    float cgv[CG_N];
-    cgv[CG_T1] = t1.x;
-    cgv[CG_T1 + 1] = t1.y;
-    cgv[CG_T1 + 2] = t1.z;
-    row_ref(solref, solimp, c[CON_DIST], cgv[CG_IMPR], cgv[CG_KID], cgv[CG_B]);
-    cgv[CG_TRAN] = MMX_body_invweight0[2 * b1] + MMX_body_invweight0[2 * b2];
-    cgv[CG_ROT] = MMX_body_invweight0[2 * b1 + 1] + MMX_body_invweight0[2 * b2 + 1];
-    cgv[CG_MU0] = c[CON_MU0];
-    cgv[CG_MU1] = c[CON_MU1];
-#pragma unroll
-    for (int k = 0; k < CG_N; k++) {
-      if (k < 5) E.r[5 * LANE + k] = cgv[k];
-      else E.s[5 * LANE + k - 5] = cgv[k];
-    }
-    for (int rr = 0; rr < ncr && brow + rr < MMX_MAXEFC; rr++) rowmap[brow + rr] = LANE | (rr << 8);
-  }
-  SYNC();
-  PROBE(3, stats, STAT_T_AUX3);
-  for (int r = LANE; r < nefc; r += WG) {
-    const int m = rowmap[r];
-    if (m >= 0) contact_row(E, r, m & 255, m >> 8);
   }
   SYNC();
   PROBE(3, stats, STAT_T_AUX2);
@@ -1062,6 +1095,27 @@ DEV float row_dot16(const EnvSh& E, int i, const float* x) {
   return s;
 }
 
+// (M v)_lane for lane < 27 (arm rows: the 9 x 9 block; cube rows: the diagonal)
+DEV float mass_mul(const EnvSh& E, const float* v) {
+  if (LANE < 9) {
+    float m = 0.f;
+#pragma unroll
+    for (int b = 0; b < 9; b++) m = fmaf(E.M9[LANE][b], v[b], m);
+    return m;
+  }
+  return LANE < 27 ? E.Mc[LANE - 9] * v[LANE] : 0.f;
+}
+// (M (xa - xb))_lane, same layout
+DEV float mass_mul_diff(const EnvSh& E, const float* xa, const float* xb) {
+  if (LANE < 9) {
+    float m = 0.f;
+#pragma unroll
+    for (int b = 0; b < 9; b++) m = fmaf(E.M9[LANE][b], xa[b] - xb[b], m);
+    return m;
+  }
+  return LANE < 27 ? E.Mc[LANE - 9] * (xa[LANE] - xb[LANE]) : 0.f;
+}
+
 // cost at two candidate points (warm start, qacc_smooth) in one pass; also returns, per lane,
 // the row residuals J x - aref of the rows it owns and (M (x - xs))_lane for both candidates, so
 // the Newton loop starts from them and then only updates them (r += a J p, M dx += a M p)
@@ -1071,12 +1125,8 @@ DEV void cost2_wave(const EnvSh& E, const float* xa, const float* xb, float& ca,
   ma = 0.f;
   mb = 0.f;
   if (LANE < 27) {
-#pragma unroll
-    for (int b = 0; b < 27; b++) {
-      const float m = E.M[LANE][b];
-      ma = fmaf(m, xa[b] - E.qacc_s[b], ma);
-      mb = fmaf(m, xb[b] - E.qacc_s[b], mb);
-    }
+    ma = mass_mul_diff(E, xa, E.qacc_s);
+    mb = mass_mul_diff(E, xb, E.qacc_s);
     c0 = 0.5f * (xa[LANE] - E.qacc_s[LANE]) * ma;
     c1 = 0.5f * (xb[LANE] - E.qacc_s[LANE]) * mb;
   }
@@ -1086,9 +1136,10 @@ DEV void cost2_wave(const EnvSh& E, const float* xa, const float* xb, float& ca,
     va[q] = 0.f;
     vb[q] = 0.f;
     if (i < E.nefc) {
-      const bool eq = (E.hdr[i] >> 8) != 0;
-      va[q] = row_dot16(E, i, xa) - E.aref[i];
-      vb[q] = row_dot16(E, i, xb) - E.aref[i];
+      const bool eq = i == 0;  // row 0: the finger equality
+      const float aref = E.J[i][15];
+      va[q] = row_dot16(E, i, xa) - aref;
+      vb[q] = row_dot16(E, i, xb) - aref;
       if (eq || va[q] < 0.f) c0 += 0.5f * E.D[i] * va[q] * va[q];
       if (eq || vb[q] < 0.f) c1 += 0.5f * E.D[i] * vb[q] * vb[q];
     }
@@ -1109,12 +1160,12 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
   float* stats = E.stats;
   CLK_DECL;
-  float* G = &E.Lrow[0][0];  // 16 x 16 staging tile (Lrow is free until the Cholesky)
+  float* G = lrow_of(E);  // 16 x 16 staging tile (the factor's space is free until the Cholesky)
   const int col = LANE & 15, rk = LANE >> 4;
   const int d = min(LANE, 26);
   const int bd = dof_blk(d), od = d - blk_d0(bd);
 #pragma unroll
-  for (int i = 0; i < 27; i++) hrow[i] = E.M[d][i];
+  for (int i = 0; i < 27; i++) hrow[i] = d < 9 ? (i < 9 ? E.M9[d][i] : 0.f) : (i == d ? E.Mc[d - 9] : 0.f);
   float gacc = 0.f;
   PROBE(6, stats, STAT_T_AUX3);
   for (int t = 0; t < NTYPE; t++) {
@@ -1122,21 +1173,20 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
     if (r1 <= r0) continue;
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
     for (int s0 = r0; s0 < r1; s0 += 8) {  // 2 MFMA steps per trip, loads first
-      float jv[2], w[2], wr[2];
+      float jv[2], w[2];
       bool valid[2];
 #pragma unroll
       for (int u = 0; u < 2; u++) {
         const int r = s0 + 4 * u + rk;
         valid[u] = r < r1;
         const int rc = valid[u] ? r : r0;
-        jv[u] = E.J[rc][col];
-        w[u] = E.s[rc];
-        wr[u] = E.r[rc];
+        jv[u] = E.J[rc][col];  // slot 15 holds w r
+        w[u] = E.D[rc];        // active weight s
       }
 #pragma unroll
       for (int u = 0; u < 2; u++) {
-        const float a = valid[u] ? jv[u] : 0.f;
-        const float b = valid[u] ? (col == 15 ? wr[u] : w[u] * jv[u]) : 0.f;
+        const float a = valid[u] ? jv[u] : 0.f;  // (slot 15 only feeds G's unused row 15)
+        const float b = valid[u] ? (col == 15 ? jv[u] : w[u] * jv[u]) : 0.f;
         if (u) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc1, 0, 0, 0);
         else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc0, 0, 0, 0);
       }
@@ -1201,12 +1251,12 @@ DEV float chol_solve_reg(EnvSh& E, const float* hrow, float v) {
   const int jc = min(j, 26);
   if (j < 27) {
 #pragma unroll
-    for (int m = 0; m < 27; m++) E.Lrow[j][m] = h[m];
+    for (int m = 0; m < 27; m++) lrow_of(E)[27 * j + m] = h[m];
   }
   SYNC();
   float c[27];
 #pragma unroll
-  for (int k = 0; k < 27; k++) c[k] = E.Lrow[k][jc];  // L[k][j]
+  for (int k = 0; k < 27; k++) c[k] = lrow_of(E)[27 * k + jc];  // L[k][j]
 #pragma unroll
   for (int k = 26; k >= 0; k--) {  // L' z = y
     const float zk = readlane_f(y, k) * dinv[k];
@@ -1277,12 +1327,12 @@ DEV float chol_solve_arrow(EnvSh& E, const float* hrow, float v, int cpl) {
   const int jc = min(j, 26);
   if (j < 27) {
 #pragma unroll
-    for (int m = 0; m < 27; m++) E.Lrow[j][m] = h[m];
+    for (int m = 0; m < 27; m++) lrow_of(E)[27 * j + m] = h[m];
   }
   SYNC();
   float c[27];
 #pragma unroll
-  for (int k = 0; k < 27; k++) c[k] = E.Lrow[k][jc];  // L[k][j]
+  for (int k = 0; k < 27; k++) c[k] = lrow_of(E)[27 * k + jc];  // L[k][j]
   PROBE(9, stats, STAT_T_AUX2);
 #pragma unroll
   for (int pi = 26; pi >= 0; pi--) {  // L' z = y
@@ -1313,7 +1363,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
   for (int q = 0; q < RPL; q++) {
     const int i = LANE + WG * q;
     dd[q] = i < nefc ? E.D[i] : 0.f;
-    eq[q] = i < nefc && (E.hdr[i] >> 8) != 0;
+    eq[q] = i == 0;  // row 0: the finger equality (always present)
     rr[q] = from_ws ? ra[q] : rs[q];
     jp[q] = 0.f;
   }
@@ -1333,8 +1383,8 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
       if (i < nefc) {
         const float v = rr[q];
         const float w = (eq[q] || v < 0.f) ? dd[q] : 0.f;
-        E.r[i] = w * v;  // w r for the gradient
-        E.s[i] = w;
+        E.J[i][15] = w * v;  // w r for the gradient (the row's aref slot is dead after the setup)
+        E.D[i] = w;          // s (D itself is in registers since the setup)
       }
     }
     SYNC();
@@ -1360,8 +1410,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
     PROBE(10, stats, STAT_T_AUX0);
     float c0 = 0.f, c1 = 0.f, mp = 0.f;
     if (LANE < 27) {
-#pragma unroll
-      for (int b = 0; b < 27; b++) mp = fmaf(E.M[LANE][b], E.p[b], mp);
+      mp = mass_mul(E, E.p);
       c0 = mp * (E.x[LANE] - E.qacc_s[LANE]);
       c1 = mp * pj;
     }
@@ -1439,17 +1488,17 @@ DEV void integrate_wave(EnvSh& E) {
   float rhs = E.qfrc[d];
 #pragma unroll
   for (int c = 0; c < 9; c++) {
-    arow[c] = E.M[d][c];
-    rhs += E.M[d][c] * (E.x[c] - E.qacc_s[c]);
+    arow[c] = E.M9[d][c];
+    rhs += E.M9[d][c] * (E.x[c] - E.qacc_s[c]);
   }
 #pragma unroll
   for (int c = 0; c < 9; c++) {
     float a = arow[c];
     if (c == d) {
       a += kDt * MMX_dof_damping[d];
-      if (d < 7 && E.act_unclamped[d]) a -= kDt * MMX_act_bias[3 * d + 2];
+      if (d < 7 && ((E.act_free >> d) & 1)) a -= kDt * MMX_act_bias[3 * d + 2];
     }
-    if (E.act_unclamped[7] && d >= 7 && c >= 7) {  // tendon actuator kv on the finger pair
+    if (((E.act_free >> 7) & 1) && d >= 7 && c >= 7) {  // tendon actuator kv on the finger pair
       const float bv = MMX_act_bias[3 * 7 + 2];
       a -= kDt * bv * MMX_tendon_coef[d - 7] * MMX_tendon_coef[c - 7];
     }
@@ -1541,15 +1590,15 @@ DEV void chol6_solve(const float* A, float* x) {
 // DLS IK with nullspace bias on the stale kinematics cache -> ctrl[0:7]
 DEV void ik_lane0(EnvSh& E) {
   const V3 tgt = V3{E.target[0], E.target[1], E.target[2]};
-  const V3 ee = V3{E.kin[KIN_HAND_POS], E.kin[KIN_HAND_POS + 1], E.kin[KIN_HAND_POS + 2]};
+  const V3 ee = V3{kin_get(E, KIN_HAND_POS), kin_get(E, KIN_HAND_POS + 1), kin_get(E, KIN_HAND_POS + 2)};
   M3 Rc;
 #pragma unroll
-  for (int k = 0; k < 9; k++) Rc.m[k] = E.kin[KIN_HAND_MAT + k];
+  for (int k = 0; k < 9; k++) Rc.m[k] = kin_get(E, KIN_HAND_MAT + k);
   float J[6][7];
 #pragma unroll
   for (int d = 0; d < 7; d++) {
-    const V3 ax = V3{E.kin[KIN_AXIS + 3 * d], E.kin[KIN_AXIS + 3 * d + 1], E.kin[KIN_AXIS + 3 * d + 2]};
-    const V3 an = V3{E.kin[KIN_ANCHOR + 3 * d], E.kin[KIN_ANCHOR + 3 * d + 1], E.kin[KIN_ANCHOR + 3 * d + 2]};
+    const V3 ax = V3{kin_get(E, KIN_AXIS + 3 * d), kin_get(E, KIN_AXIS + 3 * d + 1), kin_get(E, KIN_AXIS + 3 * d + 2)};
+    const V3 an = V3{kin_get(E, KIN_ANCHOR + 3 * d), kin_get(E, KIN_ANCHOR + 3 * d + 1), kin_get(E, KIN_ANCHOR + 3 * d + 2)};
     const V3 jp = cross(ax, ee - an);
     J[0][d] = jp.x; J[1][d] = jp.y; J[2][d] = jp.z;
     J[3][d] = ax.x; J[4][d] = ax.y; J[5][d] = ax.z;
@@ -1606,14 +1655,14 @@ DEV void ik_lane0(EnvSh& E) {
 
 // Wave form of ik_lane0: J columns one lane per arm joint, the 6 x 6 DLS system one lane per row
 // (register Cholesky), dq = b + J' A^{-1} (e - J b) with b the null-space pull toward home
-// (= J' A^{-1} e + (I - J' A^{-1} J) b of controller.py:111-124).  Scratch: E.Lrow (free here).
+// (= J' A^{-1} e + (I - J' A^{-1} J) b of controller.py:111-124).  Scratch: E.J (free here).
 DEV void ik_wave(EnvSh& E) {
-  float* W = &E.Lrow[0][0];  // J [6][8] at 0, b [8] at 48, e [8] at 56, u [8] at 64
-  const V3 ee = V3{E.kin[KIN_HAND_POS], E.kin[KIN_HAND_POS + 1], E.kin[KIN_HAND_POS + 2]};
+  float* W = scr_of(E);  // J [6][8] at 0, b [8] at 48, e [8] at 56, u [8] at 64
+  const V3 ee = V3{kin_get(E, KIN_HAND_POS), kin_get(E, KIN_HAND_POS + 1), kin_get(E, KIN_HAND_POS + 2)};
   if (LANE < 7) {
     const int d = LANE;
-    const V3 ax = V3{E.kin[KIN_AXIS + 3 * d], E.kin[KIN_AXIS + 3 * d + 1], E.kin[KIN_AXIS + 3 * d + 2]};
-    const V3 an = V3{E.kin[KIN_ANCHOR + 3 * d], E.kin[KIN_ANCHOR + 3 * d + 1], E.kin[KIN_ANCHOR + 3 * d + 2]};
+    const V3 ax = V3{kin_get(E, KIN_AXIS + 3 * d), kin_get(E, KIN_AXIS + 3 * d + 1), kin_get(E, KIN_AXIS + 3 * d + 2)};
+    const V3 an = V3{kin_get(E, KIN_ANCHOR + 3 * d), kin_get(E, KIN_ANCHOR + 3 * d + 1), kin_get(E, KIN_ANCHOR + 3 * d + 2)};
     const V3 jp = cross(ax, ee - an);
     W[0 * 8 + d] = jp.x; W[1 * 8 + d] = jp.y; W[2 * 8 + d] = jp.z;
     W[3 * 8 + d] = ax.x; W[4 * 8 + d] = ax.y; W[5 * 8 + d] = ax.z;
@@ -1621,7 +1670,7 @@ DEV void ik_wave(EnvSh& E) {
   } else if (LANE == 7) {
     M3 Rc;
 #pragma unroll
-    for (int k = 0; k < 9; k++) Rc.m[k] = E.kin[KIN_HAND_MAT + k];
+    for (int k = 0; k < 9; k++) Rc.m[k] = kin_get(E, KIN_HAND_MAT + k);
     V3 ori;
     orientation_error(Rc, ori);
     W[56] = E.target[0] - ee.x; W[57] = E.target[1] - ee.y; W[58] = E.target[2] - ee.z;
@@ -1660,7 +1709,7 @@ DEV void ik_wave(EnvSh& E) {
 }
 
 // ============================================================================ one mj_step
-DEV void mj_step_wave(int max_iter, float tol, EnvSh& E) {
+DEV void mj_step_wave(int max_iter, float tol, EnvSh& E, float* con_dst) {
   float* stats = E.stats;
   CLK_DECL;
   kinematics_wave(E);
@@ -1669,6 +1718,7 @@ DEV void mj_step_wave(int max_iter, float tol, EnvSh& E) {
   CLK(stats, STAT_T_DYN);
   collide_wave(E, false);
   CLK(stats, STAT_T_COL);
+  if (con_dst) store_contacts(con_dst, E);  // before the row build reuses contact fields
   make_constraints_wave(E);
   CLK(stats, STAT_T_CON);
   float resid = 0.f;
@@ -1748,11 +1798,11 @@ DEV V3 bin_pos(int bn) {
   const int b = kBinBody[bn];  // static bins: body origin = constant body pos (parent = world)
   return V3{MMX_body_pos[3 * b], MMX_body_pos[3 * b + 1], MMX_body_pos[3 * b + 2]};
 }
-DEV V3 hand_pos(const EnvSh& E) { return V3{E.kin[KIN_HAND_POS], E.kin[KIN_HAND_POS + 1], E.kin[KIN_HAND_POS + 2]}; }
+DEV V3 hand_pos(const EnvSh& E) { return V3{kin_get(E, KIN_HAND_POS), kin_get(E, KIN_HAND_POS + 1), kin_get(E, KIN_HAND_POS + 2)}; }
 DEV M3 hand_R(const EnvSh& E) {
   M3 R;
 #pragma unroll
-  for (int k = 0; k < 9; k++) R.m[k] = E.kin[KIN_HAND_MAT + k];
+  for (int k = 0; k < 9; k++) R.m[k] = kin_get(E, KIN_HAND_MAT + k);
   return R;
 }
 
@@ -1799,7 +1849,7 @@ DEV void rotmat_to_quat_xyzw(const float* R, float* q) {  // pose_utils.py:48-82
 DEV void obs_lane0(const MMXState& S, int i, EnvSh& E) {
   const V3 hx = hand_pos(E);
   const M3 hR = hand_R(E);
-  float* o = E.obs;
+  float* o = obs_of(E);
   const float g = E.ctrl[7] / 255.f;
   o[0] = hx.x; o[1] = hx.y; o[2] = hx.z; o[3] = g;
 #pragma unroll
@@ -1886,7 +1936,7 @@ DEV void reset_lane0(const MMXState& S, int i, EnvSh& E, int task_override) {
   kinematics_lane0(E);
   const V3 hx = hand_pos(E);
 #pragma unroll
-  for (int k = 0; k < 9; k++) EPF(EPF_TINIT + k) = E.kin[KIN_HAND_MAT + k];
+  for (int k = 0; k < 9; k++) EPF(EPF_TINIT + k) = kin_get(E, KIN_HAND_MAT + k);
   EPF(EPF_TINIT + 9) = hx.x; EPF(EPF_TINIT + 10) = hx.y; EPF(EPF_TINIT + 11) = hx.z;
   EPI(EPI_STEP) = 0;
   EPI(EPI_FLAGS) = 0;
@@ -2064,7 +2114,7 @@ DEV void load_env(const MMXState& S, int i, EnvSh& E) {
     E.ws[LANE] = S.qacc_ws[(size_t)i * 27 + LANE];
   }
   if (LANE < 8) E.ctrl[LANE] = S.ctrl[(size_t)i * 8 + LANE];
-  if (LANE < KIN_N) E.kin[LANE] = S.kin[(size_t)i * KIN_N + LANE];
+  if (LANE < KIN_N) kin_ref(E, LANE) = S.kin[(size_t)i * KIN_N + LANE];
   if (LANE < 4) E.target[LANE] = S.target[(size_t)i * 4 + LANE];
   if (LANE < STAT_N) E.stats[LANE] = S.stats[(size_t)i * STAT_N + LANE];
   if (LANE == 0) {
@@ -2082,7 +2132,7 @@ DEV void store_env(const MMXState& S, int i, const EnvSh& E) {
     S.qacc_ws[(size_t)i * 27 + LANE] = E.ws[LANE];
   }
   if (LANE < 8) S.ctrl[(size_t)i * 8 + LANE] = E.ctrl[LANE];
-  if (LANE < KIN_N) S.kin[(size_t)i * KIN_N + LANE] = E.kin[LANE];
+  if (LANE < KIN_N) S.kin[(size_t)i * KIN_N + LANE] = kin_get(E, LANE);
   if (LANE < 4) S.target[(size_t)i * 4 + LANE] = E.target[LANE];
   if (LANE < STAT_N) S.stats[(size_t)i * STAT_N + LANE] = E.stats[LANE];
   if (S.rpose)  // body poses for the camera renderer (mmx_render.hip)
@@ -2093,12 +2143,7 @@ DEV void store_env(const MMXState& S, int i, const EnvSh& E) {
 }
 DEV void store_obs(const MMXState& S, int i, const EnvSh& E) {
   SYNC();
-  for (int k = LANE; k < MMX_NOBS; k += WG) S.obs[(size_t)i * MMX_NOBS + k] = E.obs[k];
-}
-DEV void store_contacts(const MMXState& S, int i, const EnvSh& E) {
-  const int n = E.ncon;
-  float* dst = S.con + (size_t)i * MMX_MAXCON * CON_F;
-  for (int k = LANE; k < MMX_MAXCON * CON_F; k += WG) dst[k] = k < n * CON_F ? (&E.con[0][0])[k] : 0.f;
+  for (int k = LANE; k < MMX_NOBS; k += WG) S.obs[(size_t)i * MMX_NOBS + k] = obs_of(E)[k];
 }
 
 // ============================================================================ kernels
@@ -2119,7 +2164,6 @@ DEV void fold_flags(const MMXState& S, int i, const EnvSh& E) {  // lane 0
 DEV void step_end(const MMXState& S, int i, EnvSh& E, bool expert) {
   float* stats = E.stats;
   CLK_DECL;
-  store_contacts(S, i, E);
   // mj_forward position stage (gym_env.py:560): kinematics + contacts for the staged penalty
   if (LANE == 0) {
     EPI(EPI_NCON) = E.ncon;
@@ -2169,7 +2213,7 @@ DEV void step_end(const MMXState& S, int i, EnvSh& E, bool expert) {
 
 extern "C" __global__ void __launch_bounds__(WG) mmx_substep_kernel(MMXState S, const float* action, int adim, int mode) {
   EnvSh& E = g_E;
-  __shared__ float act[12];
+  float* act = scr_of(E) + SCR_ACT;  // lane 0's decoded action (E.J is free before the substeps)
   const int i = blockIdx.x;
   if (i >= S.N) return;
   load_env(S, i, E);
@@ -2187,11 +2231,10 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_substep_kernel(MMXState S, 
     SYNC();
     CLK(stats, STAT_T_IK);
   }
-  mj_step_wave(S.solver_max_iter, S.solver_tol, E);
+  mj_step_wave(S.solver_max_iter, S.solver_tol, E, (mode & SS_LAST) ? contacts_dst(S, i) : nullptr);
   if ((mode & SS_LAST) && (mode & SS_GYM)) {
     step_end(S, i, E, (mode & SS_EXPERT) != 0);
   } else {
-    if (mode & SS_LAST) store_contacts(S, i, E);
     if (LANE == 0) {
       fold_flags(S, i, E);
       if (mode & SS_LAST) {
@@ -2208,23 +2251,27 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_substep_kernel(MMXState S, 
 // the phases' LDS loads); the price is the callee-saved register spill / fill per call.
 //
 // Two waves per env (STEP_WG = 128): after the position stage, wave 0 runs the smooth dynamics
-// (RNE, CRBA, actuation, qacc_smooth) while wave 1 runs collision detection; the two phases
-// touch disjoint LDS (M / Ic / bias / qfrc / qacc_s / Lrow scratch vs. contacts / J scratch).
-// Everything else runs on wave 0.  With 4 workgroups per CU (LDS-bound), the second wave is
-// what puts two waves on every SIMD.  MMX_ONE_WAVE builds the single-wave form (64 lanes).
-#ifdef MMX_ONE_WAVE
-#define STEP_WG 64
-#else
+// (RNE, CRBA, actuation, qacc_smooth) while wave 1 runs the collision prune (geom poses, sphere /
+// OBB tests, class lists); then wave 0 runs the GJK/EPA pairs while wave 1 runs the plane and
+// box-box pairs.  Concurrent phases touch disjoint LDS (M / Ic / bias / qfrc / qacc_s / Lrow
+// scratch vs. contacts / J scratch; contacts from both waves meet through an LDS atomic).
+// Everything else runs on wave 0.  This form (MMX_TWO_WAVE) is register-bound at 4 workgroups
+// per CU (2 x 250 VGPRs per SIMD).  The product build is the single-wave form: the env's LDS
+// footprint (27,136 B) admits 6 workgroups per CU, which beats splitting one env over two waves
+// (measured: 1.11 M env steps/s for two waves at 4 / CU vs 1.21 M single-wave at 5 / CU).
+#ifdef MMX_TWO_WAVE
 #define STEP_WG 128
+#else
+#define STEP_WG 64
 #endif
-__device__ __attribute__((noinline)) void substep(int max_iter, float tol) {
+__device__ __attribute__((noinline)) void substep(int max_iter, float tol, float* con_dst) {
   EnvSh& E = g_E;
   float* stats = E.stats;
-#ifdef MMX_ONE_WAVE
+#ifndef MMX_TWO_WAVE
   CLK_DECL;
   ik_wave(E);  // IK on the kinematics left by the previous position stage
   CLK(stats, STAT_T_IK);
-  mj_step_wave(max_iter, tol, E);
+  mj_step_wave(max_iter, tol, E, con_dst);
 #else
   const int w = WAVE_ID;
   if (w == 0) {
@@ -2235,18 +2282,23 @@ __device__ __attribute__((noinline)) void substep(int max_iter, float tol) {
     CLK(stats, STAT_T_KIN);
   }
   XSYNC();
-  if (w == 0) {
+  {
     CLK_DECL;
-    dynamics_wave(E);
-    CLK(stats, STAT_T_DYN);
-  } else {
-    CLK_DECL;
-    collide_wave(E, false);
-    CLK(stats, STAT_T_COL);  // wave 1's lane 0 (its own stats slot)
+    if (w == 0) {
+      dynamics_wave(E);
+      CLK(stats, STAT_T_DYN);
+    } else {
+      collide_prune(E, false);
+    }
+    XSYNC();
+    collide_pairs(E, false, w == 0 ? 2 : 1);  // wave 0: GJK/EPA pairs, wave 1: plane + box-box
+    XSYNC();
+    if (w == 1) CLK(stats, STAT_T_COL);  // wave 1's lane 0 (its own stats slot)
   }
-  XSYNC();
   if (w == 0) {
     CLK_DECL;
+    collide_sort(E);
+    if (con_dst) store_contacts(con_dst, E);  // before the row build reuses contact fields
     make_constraints_wave(E);
     CLK(stats, STAT_T_CON);
     float resid = 0.f;
@@ -2273,7 +2325,7 @@ __device__ __attribute__((noinline)) void substep(int max_iter, float tol) {
 extern "C" __global__ void __launch_bounds__(STEP_WG) __attribute__((amdgpu_waves_per_eu(2, 2)))
 mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert, int base) {
   EnvSh& E = g_E;
-  __shared__ float act[12];
+  float* act = scr_of(E) + SCR_ACT;  // lane 0's decoded action (E.J is free before the substeps)
   const int i = base + blockIdx.x;
   if (i >= S.N) return;
   const bool w0 = STEP_WG == 64 || WAVE_ID == 0;
@@ -2288,7 +2340,8 @@ mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert, int b
     SYNC();
   }
   XSYNC();
-  for (int sub = 0; sub < MMX_NSUBSTEP; sub++) substep(S.solver_max_iter, S.solver_tol);
+  for (int sub = 0; sub < MMX_NSUBSTEP; sub++)
+    substep(S.solver_max_iter, S.solver_tol, sub == MMX_NSUBSTEP - 1 ? contacts_dst(S, i) : nullptr);
   if (w0) {
     step_end(S, i, E, expert != 0);
     store_env(S, i, E);

@@ -14,7 +14,7 @@
 #define MMX_NU_ 8
 #define MMX_NOBS 85
 #define MMX_MAXCON 64
-#define MMX_MAXEFC 320
+#define MMX_MAXEFC 304
 #define MMX_NSUBSTEP 16
 
 // stale kinematics cache read by the IK (controller.py:99-108 reads data.xpos / mj_jac
