@@ -1,15 +1,16 @@
 // Batched camera renderer for gfx950: the overhead and wrist images of
 // PickPlaceGymEnv's observation (gym_env.py:295-339 via cameras.py:9-53, mujoco.Renderer).
 //
-// One workgroup (256 lanes) renders one horizontal band of one camera image of one env:
+// One workgroup (512 lanes) renders one horizontal band (8192 px) of one camera image of one env:
 //   1. body poses of the env (stored by the step / reset / forward kernels in S.rpose) and the
 //      camera pose (overhead: fixed; wrist: on the hand, env.py:52-65) -> LDS;
 //   2. all render vertices (tools/compile_render.py: floor grid, table / bins / cubes as boxes
 //      and prisms, each Panda body as the hull of its visual meshes) to camera space -> LDS;
 //   3. triangles, one lane each: near cull, projection (MuJoCo pinhole, fovy, row 0 at the top),
-//      back-face cull, bounding box clipped to the band.  Small boxes are scanned by the lane
-//      itself; large ones (floor tiles, table top) go to an LDS queue that the whole workgroup
-//      scans pixel-parallel.  Depth test = one 32-bit LDS atomicMax per covered pixel on
+//      back-face cull, bounding box clipped to the band, into one of two LDS queues by box
+//      area.  Small boxes (<= 256 px) are scanned by 16-lane groups, one triangle per group
+//      (every lane of a wave busy however the box sizes vary); large ones (floor tiles, table top)
+//      by the whole workgroup, pixel-parallel.  Depth test = one 32-bit LDS atomicMax per covered pixel on
 //      (inverse depth quantised over the camera's depth range : 20 bits | triangle : 12 bits);
 //   4. shading, 4 pixels per lane: flat per-face light (computed once per triangle in pass 3), MuJoCo's
 //      headlight (ambient 0.3, diffuse 0.6) + the scene's directional (0.8) and point (0.4)
@@ -27,17 +28,24 @@
 #include "mmx_device.h"
 #include "mmx_state.h"
 
-#define RWG 256
+#ifndef MMR_WG
+#define MMR_WG 512
+#endif
+#define RWG MMR_WG
+#ifndef MMR_SKIP
+#define MMR_SKIP 0  // diagnostic builds only: 1 small-triangle raster, 2 large-triangle raster, 4 shading
+#endif
 #define RNSLOT 14
 static_assert(MMR_NTRI <= 4096, "triangle index must fit the 12-bit depth-key field");
 #ifndef MMR_BAND_PX
 #define MMR_BAND_PX 8192
 #endif
 #ifndef MMR_SMALL_AREA
-#define MMR_SMALL_AREA 64
+#define MMR_SMALL_AREA 256
 #endif
 static constexpr int kBandPx = MMR_BAND_PX;      // z-buffer pixels per band (32 KB of LDS)
-static constexpr int kSmallArea = MMR_SMALL_AREA; // bounding boxes up to this many pixels: one lane
+static constexpr int kSmallArea = MMR_SMALL_AREA; // bounding boxes up to this many pixels: a 16-lane group
+static constexpr int kGroup = 16;                // lanes per small triangle
 static constexpr int kMaxBig = 1024;
 
 DEV int rend_band_rows(int S) { return kBandPx / S < S ? kBandPx / S : S; }
@@ -117,6 +125,7 @@ extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, 
   float* cam = reinterpret_cast<float*>(nbig + 4);                                // R (9), p (3)
   uint32_t* tinfo = reinterpret_cast<uint32_t*>(cam + 12);                        // [MMR_NTRI]
   float* mrgb = reinterpret_cast<float*>(tinfo + MMR_NTRI);                       // [MMR_NMAT][8]
+  unsigned short* smallq = reinterpret_cast<unsigned short*>(mrgb + 8 * MMR_NMAT); // [MMR_NTRI]
 
   const int tid = threadIdx.x;
   const int Sz = S.image_size;
@@ -143,6 +152,7 @@ extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, 
   }
   if (tid == 32) {
     nbig[0] = 0;
+    nbig[1] = 0;
     const int c = ci == 0 ? MMX_CAM_OVERHEAD : MMX_CAM_WRIST;
     const M3 lq = qmat(Q4{MMX_cam_quat[4 * c], MMX_cam_quat[4 * c + 1], MMX_cam_quat[4 * c + 2], MMX_cam_quat[4 * c + 3]});
     const V3 lp = V3{MMX_cam_pos[3 * c], MMX_cam_pos[3 * c + 1], MMX_cam_pos[3 * c + 2]};
@@ -189,7 +199,9 @@ extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, 
   const float iz_lo = 1.f / zfar, iz_scale = 1.f / (1.f / znear - 1.f / zfar);
   const V3 l_top = mulT(cR, V3{0.f, 0.f, 1.f});  // toward the directional light (dir 0 0 -1)
   const V3 lp_cam = mulT(cR, V3{0.5f, 0.5f, 1.5f} - cx);
-  for (int t = tid; t < MMR_NTRI; t += RWG) {
+  // the floor's triangles [0, MMR_FLOOR_TRIS) are not rasterised: it lies below everything, so a
+  // pixel no triangle covers shows the floor where its ray meets z = 0 inside the plane, else sky
+  for (int t = MMR_FLOOR_TRIS + tid; t < MMR_NTRI; t += RWG) {
     RTri T;
     if (!rend_setup(vc, t, f, half, znear, Sz, row0, row1, T)) continue;
     {  // flat shading of the face, once: headlight + directional + point light (at the centroid)
@@ -204,16 +216,27 @@ extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, 
     if (area > kSmallArea) {
       const int k = atomicAdd(nbig, 1);
       if (k < kMaxBig) bigq[k] = (unsigned short)t;
-      continue;
+    } else {
+      smallq[atomicAdd(nbig + 1, 1)] = (unsigned short)t;
     }
-    for (int py = T.by0; py <= T.by1; py++)
-      for (int px = T.bx0; px <= T.bx1; px++) {
+  }
+  __syncthreads();
+  {  // small triangles: one per 16-lane group, the group's lanes stride over the box
+    const int ns = (MMR_SKIP & 1) ? 0 : nbig[1];
+    const int grp = tid / kGroup, gl = tid % kGroup;
+    for (int q = grp; q < ns; q += RWG / kGroup) {
+      const int t = smallq[q];
+      RTri T;
+      rend_setup(vc, t, f, half, znear, Sz, row0, row1, T);
+      const int w = T.bx1 - T.bx0 + 1, area = w * (T.by1 - T.by0 + 1);
+      for (int k = gl; k < area; k += kGroup) {
+        const int px = T.bx0 + k % w, py = T.by0 + k / w;
         const uint32_t key = rend_cover(T, t, px, py, iz_lo, iz_scale);
         if (key) atomicMax(&zb[(py - row0) * Sz + px], key);
       }
+    }
   }
-  __syncthreads();
-  const int nb = min(nbig[0], kMaxBig);
+  const int nb = (MMR_SKIP & 2) ? 0 : min(nbig[0], kMaxBig);
   for (int q = 0; q < nb; q++) {  // large triangles: the workgroup scans the box pixel-parallel
     const int t = bigq[q];
     RTri T;
@@ -231,7 +254,7 @@ extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, 
   const int npx = (row1 - row0) * Sz;
   unsigned char* img = S.images + ((size_t)i * 2 + ci) * Sz * Sz * 3 + (size_t)row0 * Sz * 3;
   unsigned char* seg = S.seg + ((size_t)i * 2 + ci) * Sz * Sz + (size_t)row0 * Sz;
-  for (int g = tid; g < npx / 4; g += RWG) {
+  for (int g = tid; g < ((MMR_SKIP & 4) ? 0 : npx / 4); g += RWG) {
     uint32_t rgbw[3] = {0u, 0u, 0u}, segw = 0u;
     for (int u = 0; u < 4; u++) {
       const int p = 4 * g + u;
@@ -240,7 +263,18 @@ extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, 
       const V3 dw = mul(cR, V3{(px + 0.5f - half) / f, -(py + 0.5f - half) / f, -1.f});  // world ray
       float col[3];
       int sid = 0;
-      if (key == 0u) {  // skybox gradient (rgb1 top -> rgb2 bottom, scene.xml:17-18)
+      const float s0 = -cx.z / dw.z;  // ray parameter at the floor plane z = 0
+      const float fx = cx.x + s0 * dw.x, fy = cx.y + s0 * dw.y;
+      if (key == 0u && dw.z < 0.f && fabsf(fx) <= MMR_FLOOR_HALF && fabsf(fy) <= MMR_FLOOR_HALF) {
+        // floor: checker (0.1 m squares) under the same lights as a face, evaluated per pixel
+        const float* mt = mrgb + 8 * MMR_FLOOR_MAT;
+        const V3 pc = mulT(cR, V3{fx, fy, 0.f} - cx);  // camera frame; the normal is l_top
+        const float light = fminf(0.3f + 0.6f * fmaxf(l_top.z, 0.f) + 0.8f +
+                                  0.4f * fmaxf(dot(l_top, normalize(lp_cam - pc)), 0.f), 3.99f);
+        sid = (int)mt[7];
+        const bool alt = ((int)floorf(fx / mt[6]) + (int)floorf(fy / mt[6])) & 1;
+        for (int k = 0; k < 3; k++) col[k] = fminf((alt ? mt[3 + k] : mt[k]) * light, 1.f);
+      } else if (key == 0u) {  // skybox gradient (rgb1 top -> rgb2 bottom, scene.xml:17-18)
         const float sky = 0.5f * (dw.z * rsqrtf(dot(dw, dw)) + 1.f);
         col[0] = 0.3f * sky; col[1] = 0.5f * sky; col[2] = 0.7f * sky;
       } else {
@@ -271,7 +305,7 @@ extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, 
 extern "C" size_t mmx_render_lds_bytes() {
   return sizeof(float4) * MMR_NVERT + sizeof(float) * 19 * 12 + sizeof(uint32_t) * kBandPx +
          sizeof(unsigned short) * kMaxBig + 4 * sizeof(int) + 12 * sizeof(float) + sizeof(uint32_t) * MMR_NTRI +
-         sizeof(float) * 8 * MMR_NMAT;
+         sizeof(float) * 8 * MMR_NMAT + sizeof(unsigned short) * MMR_NTRI;
 }
 
 extern "C" hipError_t mmx_launch_render(const MMXState* S, int base, int count, hipStream_t st) {

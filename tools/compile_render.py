@@ -34,6 +34,7 @@ import compile_model as CM  # noqa: E402
 
 MAX_HULL_VERTS = 96
 FLOOR_GRID = 8
+FLOOR_HALF = 2.0  # floor geom size 2 2 (pick_and_place_scene.xml:40)
 CYL_SIDES = 16
 SEG = {"floor": 1, "table": 2, "bin_red": 3, "bin_green": 4, "bin_blue": 5, "obj_red": 6, "obj_green": 7,
        "obj_blue": 8, "robot": 9}
@@ -123,7 +124,7 @@ def build():
 
     parts = []  # (body id, verts [k,3] body frame, faces, material index)
     # floor: grid over [-2, 2]^2 at z = 0 (body 0)
-    g = np.linspace(-2.0, 2.0, FLOOR_GRID + 1)
+    g = np.linspace(-FLOOR_HALF, FLOOR_HALF, FLOOR_GRID + 1)
     fv = np.array([[x, y, 0.0] for y in g for x in g])
     ff = []
     for j in range(FLOOR_GRID):
@@ -197,7 +198,11 @@ def emit(rm, path):
     L = ["/* generated by tools/compile_render.py -- do not edit */\n#ifndef MMX_RENDER_GEN_H\n"
          "#define MMX_RENDER_GEN_H\n\n#ifndef MMR_QUAL\n#define MMR_QUAL static const\n#endif\n\n"]
     nv, nt, nm = len(rm["verts"]), len(rm["tris"]), len(rm["materials"])
-    L.append(f"#define MMR_NVERT {nv}\n#define MMR_NTRI {nt}\n#define MMR_NMAT {nm}\n\n")
+    L.append(f"#define MMR_NVERT {nv}\n#define MMR_NTRI {nt}\n#define MMR_NMAT {nm}\n")
+    # the floor plane: its triangles come first (material 0, checker); the renderer shades it
+    # analytically behind everything instead of rasterising it
+    L.append(f"#define MMR_FLOOR_TRIS {2 * FLOOR_GRID * FLOOR_GRID}\n#define MMR_FLOOR_HALF {FLOOR_HALF!r}f\n"
+             "#define MMR_FLOOR_MAT 0\n\n")
     L.append(CM.c_array("MMR_vert", "float", rm["verts"], "{:.9g}"))
     L.append(CM.c_array("MMR_vert_body", "unsigned char", rm["vert_body"], "{}"))
     L.append(CM.c_array("MMR_tri", "unsigned short", rm["tris"], "{}"))
