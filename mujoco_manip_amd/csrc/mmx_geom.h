@@ -48,27 +48,38 @@ DEV V3 support(const Geom& G, V3 dir) {
   return G.x + mul(G.R, sl);
 }
 
-DEV bool obb_overlap(const Geom& A, const Geom& B) {
-  const float* ha = &MMX_geom_aabb[3 * A.g];
-  const float* hb = &MMX_geom_aabb[3 * B.g];
+// Oriented-box overlap on the six face axes (a conservative prune), in the relative-rotation
+// form: R = A'B, t = A'd, u = B'd, so each axis costs a 3-term sum instead of two projections.
+DEV bool obb_overlap(const Geom& A, const Geom& B, V3 ha, V3 hb) {
   const V3 d = B.x - A.x;
+  float Rm[3][3], aR[3][3];
 #pragma unroll
-  for (int s = 0; s < 2; s++) {
+  for (int i = 0; i < 3; i++)
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-      const V3 L = col(s ? B.R : A.R, k);
-      const float r1 = ha[0] * fabsf(dot(L, col(A.R, 0))) + ha[1] * fabsf(dot(L, col(A.R, 1))) + ha[2] * fabsf(dot(L, col(A.R, 2)));
-      const float r2 = hb[0] * fabsf(dot(L, col(B.R, 0))) + hb[1] * fabsf(dot(L, col(B.R, 1))) + hb[2] * fabsf(dot(L, col(B.R, 2)));
-      if (fabsf(dot(d, L)) > r1 + r2) return false;
+    for (int j = 0; j < 3; j++) {
+      Rm[i][j] = dot(col(A.R, i), col(B.R, j));
+      aR[i][j] = fabsf(Rm[i][j]);
     }
+  const float hA[3] = {ha.x, ha.y, ha.z}, hB[3] = {hb.x, hb.y, hb.z};
+  bool sep = false;
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    const float t = dot(d, col(A.R, i));
+    sep |= fabsf(t) > hA[i] + hB[0] * aR[i][0] + hB[1] * aR[i][1] + hB[2] * aR[i][2];
   }
-  return true;
+#pragma unroll
+  for (int j = 0; j < 3; j++) {
+    const float u = dot(d, col(B.R, j));
+    sep |= fabsf(u) > hB[j] + hA[0] * aR[0][j] + hA[1] * aR[1][j] + hA[2] * aR[2][j];
+  }
+  (void)Rm;
+  return !sep;
 }
 
 template <class Sink>
-DEV void plane_box(Sink& cs, const Geom& P, const Geom& B) {
+DEV void plane_box(Sink& cs, const Geom& P, const Geom& B, V3 hb) {
   const V3 nz = col(P.R, 2);
-  const float* h = &MMX_geom_size[3 * B.g];
+  const float h[3] = {hb.x, hb.y, hb.z};
   // penetrating corners compacted in corner order, then a selection sort of the 4 deepest, as
   // the oracle does it; every index is static (select chains), so nothing lands in scratch
   float cd[8];
@@ -151,23 +162,36 @@ DEV float self3(float a0, float a1, float a2, int k) { return k == 0 ? a0 : (k =
 
 // poly, tmp: 8 V3 each of per-lane LDS scratch (a quad clipped by 4 half-planes has <= 8 corners)
 template <class Sink>
-DEV void box_box(Sink& cs, const Geom& G1, const Geom& G2, V3* poly, V3* tmp) {
+DEV void box_box(Sink& cs, const Geom& G1, const Geom& G2, V3 hb1, V3 hb2, V3* poly, V3* tmp) {
   CLK_DECL;
-  const float* h1 = &MMX_geom_size[3 * G1.g];
-  const float* h2 = &MMX_geom_size[3 * G2.g];
+  const float h1[3] = {hb1.x, hb1.y, hb1.z}, h2[3] = {hb2.x, hb2.y, hb2.z};
   const V3 A[3] = {col(G1.R, 0), col(G1.R, 1), col(G1.R, 2)};
   const V3 B[3] = {col(G2.R, 0), col(G2.R, 1), col(G2.R, 2)};
   const V3 d = G2.x - G1.x;
+  // SAT in the relative-rotation form (R = A'B, t = A'd, u = B'd): face axes of box 1, of box 2,
+  // then the 9 edge-edge axes A_i x B_j, whose projections are again entries of R (unit axes;
+  // depths divided by |A_i x B_j|).  Same axes, order and strict-minimum tie rule as the
+  // explicit form.
+  float Rm[3][3], aR[3][3], t[3], tu[3];
+#pragma unroll
+  for (int i = 0; i < 3; i++) {
+    t[i] = dot(d, A[i]);
+    tu[i] = dot(d, B[i]);
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      Rm[i][j] = dot(A[i], B[j]);
+      aR[i][j] = fabsf(Rm[i][j]);
+    }
+  }
   float best_face = 3e38f, best_edge = 3e38f;
   int face_axis = 0, ei = -1, ej = -1;
-  V3 eL = V3{0.f, 0.f, 0.f};
+  bool sep = false;
 #pragma unroll
   for (int ax = 0; ax < 6; ax++) {
-    const V3 L = ax < 3 ? A[ax] : B[ax - 3];
-    const float r1 = h1[0] * fabsf(dot(L, A[0])) + h1[1] * fabsf(dot(L, A[1])) + h1[2] * fabsf(dot(L, A[2]));
-    const float r2 = h2[0] * fabsf(dot(L, B[0])) + h2[1] * fabsf(dot(L, B[1])) + h2[2] * fabsf(dot(L, B[2]));
-    const float s = r1 + r2 - fabsf(dot(d, L));
-    if (s < 0.f) return;
+    const float s = ax < 3 ? h1[ax] + h2[0] * aR[ax][0] + h2[1] * aR[ax][1] + h2[2] * aR[ax][2] - fabsf(t[ax])
+                           : h2[ax - 3] + h1[0] * aR[0][ax - 3] + h1[1] * aR[1][ax - 3] + h1[2] * aR[2][ax - 3] -
+                                 fabsf(tu[ax - 3]);
+    sep |= s < 0.f;
     if (s < best_face) {
       best_face = s;
       face_axis = ax;
@@ -177,21 +201,23 @@ DEV void box_box(Sink& cs, const Geom& G1, const Geom& G2, V3* poly, V3* tmp) {
   for (int a = 0; a < 3; a++)
 #pragma unroll
     for (int b = 0; b < 3; b++) {
-      V3 L = cross(A[a], B[b]);
-      const float ln = norm(L);
+      const int a1 = (a + 1) % 3, a2 = (a + 2) % 3, b1 = (b + 1) % 3, b2 = (b + 2) % 3;
+      // A_a x B_b = R[a1][b] A_a2 - R[a2][b] A_a1
+      const float ln = sqrtf(Rm[a1][b] * Rm[a1][b] + Rm[a2][b] * Rm[a2][b]);
       if (ln < 1e-6f) continue;
-      L = L * (1.0f / ln);
-      const float r1 = h1[0] * fabsf(dot(L, A[0])) + h1[1] * fabsf(dot(L, A[1])) + h1[2] * fabsf(dot(L, A[2]));
-      const float r2 = h2[0] * fabsf(dot(L, B[0])) + h2[1] * fabsf(dot(L, B[1])) + h2[2] * fabsf(dot(L, B[2]));
-      const float s = r1 + r2 - fabsf(dot(d, L));
-      if (s < 0.f) return;
+      const float ra = h1[a1] * aR[a2][b] + h1[a2] * aR[a1][b];
+      const float rb = h2[b1] * aR[a][b2] + h2[b2] * aR[a][b1];
+      const float s = (ra + rb - fabsf(t[a2] * Rm[a1][b] - t[a1] * Rm[a2][b])) / ln;
+      sep |= s < 0.f;
       if (s < best_edge) {
         best_edge = s;
         ei = a;
         ej = b;
-        eL = L;
       }
     }
+  if (sep) return;
+  V3 eL = V3{0.f, 0.f, 0.f};
+  if (ei >= 0) eL = normalize(cross(sel3(A[0], A[1], A[2], ei), sel3(B[0], B[1], B[2], ej)));
   PROBEF(8, cs.E->stats, STAT_T_AUX0);
   if (ei >= 0 && best_edge < 0.95f * best_face - 1e-9f) {
     const V3 L = dot(eL, d) < 0.f ? -eL : eL;

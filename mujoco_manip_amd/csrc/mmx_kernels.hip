@@ -84,8 +84,9 @@ static __shared__ EnvSh g_E;
 // dynamics beside the collision prune, which only touches [0, COL_WORK)) and the observation of
 // the step end.  The Newton Hessian staging tile and Cholesky transpose live in E.con instead
 // (contacts are dead once the rows exist; the last substep stores them to HBM first).
-#define COL_GX 0      // [NGEOM][16] world pose (x3, R9), rbound, type
-#define COL_CAND 768  // [COL_LIST] candidate pairs after the sphere test, then grouped by class
+#define COL_GX 0      // [NGEOM][GXS] world pose (x3, R9), rbound, type, -, -, box half extents (3), -
+#define GXS 20
+#define COL_CAND 944  // [COL_LIST] candidate pairs after the sphere test, then grouped by class
 #define COL_LIST 784
 #define COL_WORK (COL_CAND + COL_LIST)  // narrowphase work space: box-box polygons and (beside
 #define COL_POLY 48                     // them) the EPA polytope, then the contact sort
@@ -93,14 +94,14 @@ static __shared__ EnvSh g_E;
 #define COL_EPA (COL_WORK + COL_PLANES * COL_POLY)
 static_assert(COL_EPA + EPA_SCRATCH_FLOATS <= MMX_MAXEFC * 16, "box-box polygons + EPA scratch exceed E.J");
 static_assert(COL_WORK + MMX_MAXCON * CON_F <= MMX_MAXEFC * 16, "contact sort exceeds E.J");
-static_assert(MMX_NGEOM * 16 <= COL_CAND && MMX_NPAIR <= COL_LIST && MMX_NPAIR < 4096, "collision scratch layout");
+static_assert(MMX_NGEOM * GXS <= COL_CAND && MMX_NPAIR <= COL_LIST && MMX_NPAIR < 4096, "collision scratch layout");
 
 #define SCR_DYN COL_WORK           // RNE frc + inertia [12][16], subtree force [12][6] (264), then:
 #define SCR_IC (SCR_DYN + 272)     // composite inertias [12][10]
 #define SCR_AF (SCR_IC + 120)      // actuator forces [8]
 #define SCR_BIAS (SCR_AF + 8)      // RNE bias force of the arm dofs [9]
-#define SCR_OBS 4496               // observation (step end, reset, forward)
-#define SCR_ACT 4592               // raw action of the step (lane 0, before the substeps)
+#define SCR_OBS 4672               // observation (step end, reset, forward)
+#define SCR_ACT 4768               // raw action of the step (lane 0, before the substeps)
 static_assert(SCR_BIAS + 9 <= 4096 && SCR_OBS + MMX_NOBS <= SCR_ACT && SCR_ACT + 12 <= MMX_MAXEFC * 16,
               "E.J scratch layout");
 static_assert(27 * 27 <= MMX_MAXCON * CON_F, "Newton Cholesky transpose exceeds E.con");
@@ -600,8 +601,12 @@ struct WaveSink {
   }
 };
 
+DEV V3 geom_half(const float* gx, int g) {
+  const float* o = gx + GXS * g;
+  return V3{o[16], o[17], o[18]};
+}
 DEV Geom geom_lds(const float* gx, int g) {
-  const float* o = gx + 16 * g;
+  const float* o = gx + GXS * g;
   Geom G;
   G.g = g;
   G.type = __float_as_int(o[13]);
@@ -649,12 +654,15 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
   int* cand = reinterpret_cast<int*>(scr + COL_CAND);
   if (LANE < MMX_NGEOM) {
     const Geom G = geom_pose(E, LANE);
-    float* o = gx + 16 * LANE;
+    float* o = gx + GXS * LANE;
     o[0] = G.x.x; o[1] = G.x.y; o[2] = G.x.z;
 #pragma unroll
     for (int k = 0; k < 9; k++) o[3 + k] = G.R.m[k];
     o[12] = MMX_geom_rbound[LANE];
     o[13] = __int_as_float(G.type);
+    o[16] = MMX_geom_aabb[3 * LANE];  // bounding-box half extents in the geom frame (= size for boxes)
+    o[17] = MMX_geom_aabb[3 * LANE + 1];
+    o[18] = MMX_geom_aabb[3 * LANE + 2];
   }
   SYNC();
   PROBE(2, stats, STAT_T_AUX0);
@@ -674,8 +682,8 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
     if (p < MMX_NPAIR) {
       const int g1 = pg[q] & 255, g2 = pg[q] >> 8;
       if (!only_ro || robot_obstacle(g1, g2)) {
-        const float* o1 = gx + 16 * g1;
-        const float* o2 = gx + 16 * g2;
+        const float* o1 = gx + GXS * g1;
+        const float* o2 = gx + GXS * g2;
         const V3 d = V3{o2[0] - o1[0], o2[1] - o1[1], o2[2] - o1[2]};
         if (__float_as_int(o1[13]) == GT_PLANE) {
           keep = d.x * o1[5] + d.y * o1[8] + d.z * o1[11] <= o2[12];  // distance above the plane
@@ -705,7 +713,7 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
         pair_geoms(gx, p, g1, g2);
         const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
         if (A.type == GT_PLANE) c = 0;
-        else if (obb_overlap(A, B)) c = (A.type == GT_BOX && B.type == GT_BOX) ? 1 : 2;
+        else if (obb_overlap(A, B, geom_half(gx, g1), geom_half(gx, g2))) c = (A.type == GT_BOX && B.type == GT_BOX) ? 1 : 2;
       }
 #pragma unroll
       for (int t = 0; t < 3; t++) ncls[t] += __popcll(__ballot(c == t));
@@ -755,7 +763,7 @@ DEV void collide_pairs(EnvSh& E, bool only_ro, int which) {
       pair_geoms(gx, p, g1, g2);
       const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
       WaveSink cs(&E, p, !only_ro, g1, g2);
-      if (B.type == GT_BOX) plane_box(cs, A, B);
+      if (B.type == GT_BOX) plane_box(cs, A, B, geom_half(gx, g2));
       else if (B.type == GT_MESH) plane_convex(cs, A, B);
     }
     SYNC();
@@ -769,7 +777,7 @@ DEV void collide_pairs(EnvSh& E, bool only_ro, int which) {
         pair_geoms(gx, p, g1, g2);
         const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
         WaveSink cs(&E, p, !only_ro, g1, g2);
-        box_box(cs, A, B, poly, poly + 8);
+        box_box(cs, A, B, geom_half(gx, g1), geom_half(gx, g2), poly, poly + 8);
       }
     }
     SYNC();
