@@ -674,7 +674,9 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
     const int p = min(q * WG + LANE, MMX_NPAIR - 1);
     pg[q] = MMX_pair_packed[p];
   }
-  int nc = 0;
+  // all tests first (ballot masks in SGPRs), compaction stores after: no LDS store between the
+  // passes' gathers, so the compiler may keep several passes' loads in flight
+  unsigned long long km[NPASS];
 #pragma unroll
   for (int q = 0; q < NPASS; q++) {
     const int p = q * WG + LANE;
@@ -693,7 +695,17 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
         }
       }
     }
-    nc = wave_compact(keep, cand, nc, p);
+    km[q] = __ballot(keep);
+  }
+  int nc = 0;
+#pragma unroll
+  for (int q = 0; q < NPASS; q++) {
+    const unsigned long long m = km[q];
+    if ((m >> LANE) & 1ull) {
+      const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+      cand[nc + pos] = q * WG + LANE;
+    }
+    nc += __popcll(m);
   }
   SYNC();
   PROBE(2, stats, STAT_T_AUX1);
