@@ -214,6 +214,7 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
   S.done = dalloc<int>(sim, 3 * n);
   S.con = dalloc<float>(sim, static_cast<size_t>(MMX_MAXCON) * CON_F * n);
   S.stats = dalloc<float>(sim, STAT_N * n);
+  S.efc_ovf = dalloc<float>(sim, static_cast<size_t>(MMX_OVF_F) * n);
   sim->expert_action = dalloc<float>(sim, 4 * n);
   sim->d_mask = dalloc<unsigned char>(sim, n);
   sim->d_task = dalloc<int>(sim, n);
@@ -228,7 +229,7 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
       mmx_destroy(sim);
       return MMX_ENOMEM;
     }
-  if (!S.qpos || !S.con || !sim->d_task) {
+  if (!S.qpos || !S.con || !S.efc_ovf || !sim->d_task) {
     mmx_destroy(sim);
     return MMX_ENOMEM;
   }

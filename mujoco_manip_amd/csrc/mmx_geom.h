@@ -456,8 +456,8 @@ DEV bool gjk(const Geom& A, const Geom& B, SVx& s0, SVx& s1, SVx& s2, SVx& s3, i
   return norm(dir) < 1e-12f;
 }
 
-#define EPA_MAXV 40
-#define EPA_MAXF 80
+#define EPA_MAXV 38
+#define EPA_MAXF 72  // 2 EPA_MAXV - 4: the faces of a closed polytope on EPA_MAXV vertices
 struct EFace {
   int v0, v1, v2;
   V3 n;

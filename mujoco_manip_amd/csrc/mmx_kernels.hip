@@ -63,11 +63,14 @@ struct EnvSh {
   // constraint rows in block format: a row touches at most two dof blocks (arm = 9 dofs,
   // cube k = 6 dofs); J[i][0..n0) holds block b0's columns, J[i][n0..n0+n1) block b1's;
   // J doubles as the contact-sort scratch in collide_wave (rows are built after it)
-  alignas(16) float J[MMX_MAXEFC][16];  // slots past the row's width = 0; slot 15 = the row's aref
+  // Rows past MMX_LDSEFC (a pile of contacts; ~5 % of C3 substeps) live in the env's HBM overflow
+  // block `ovf` (J rows, then D): lane-owned row q >= LDSEFC / 64 is always an HBM row.
+  alignas(16) float J[MMX_LDSEFC][16];  // slots past the row's width = 0; slot 15 = the row's aref
   unsigned char hdr[MMX_MAXEFC];  // b0 | b1 << 4 (block 15 = none); row 0 is the equality
   // D: the row's 1 / R while the rows are built (doubling as the row -> contact map before) and in
   // the solver's setup; then the Newton iterations' active weights s
-  float D[MMX_MAXEFC];
+  float D[MMX_LDSEFC];
+  float* ovf;  // this env's overflow rows (S.efc_ovf + i * MMX_OVF_F)
   int ncon, nefc, flags;
   int ncls[3];    // collision candidates per narrowphase class (plane, box-box, GJK)
   int tbase[11];  // rows are grouped by block-pair type: type t owns rows [tbase[t], tbase[t+1])
@@ -90,25 +93,55 @@ static __shared__ EnvSh g_E;
 #define COL_LIST 784
 #define COL_WORK (COL_CAND + COL_LIST)  // narrowphase work space: box-box polygons and (beside
 #define COL_POLY 48                     // them) the EPA polytope, then the contact sort
-#define COL_PLANES 32                   // lanes that clip box-box polygons at a time
+// lanes that clip box-box polygons at a time (their polygons fill the rest of the LDS rows)
+#define COL_PLANES ((MMX_LDSEFC * 16 - COL_WORK) / COL_POLY < 32 ? (MMX_LDSEFC * 16 - COL_WORK) / COL_POLY : 32)
+#if MMX_TWO_WAVE  // wave 0's GJK/EPA runs beside wave 1's box-box clipping
 #define COL_EPA (COL_WORK + COL_PLANES * COL_POLY)
-static_assert(COL_EPA + EPA_SCRATCH_FLOATS <= MMX_MAXEFC * 16, "box-box polygons + EPA scratch exceed E.J");
-static_assert(COL_WORK + MMX_MAXCON * CON_F <= MMX_MAXEFC * 16, "contact sort exceeds E.J");
+#else  // the GJK/EPA pass follows the box-box pass: the polytope reuses the polygons' space
+#define COL_EPA COL_WORK
+#endif
+static_assert(COL_EPA + EPA_SCRATCH_FLOATS <= MMX_LDSEFC * 16, "box-box polygons + EPA scratch exceed E.J");
+static_assert(COL_WORK + MMX_MAXCON * CON_F <= MMX_LDSEFC * 16, "contact sort exceeds E.J");
+static_assert(COL_PLANES >= 16 && COL_WORK + COL_PLANES * COL_POLY <= MMX_LDSEFC * 16, "box-box polygons exceed E.J");
 static_assert(MMX_NGEOM * GXS <= COL_CAND && MMX_NPAIR <= COL_LIST && MMX_NPAIR < 4096, "collision scratch layout");
 
 #define SCR_DYN COL_WORK           // RNE frc + inertia [12][16], subtree force [12][6] (264), then:
 #define SCR_IC (SCR_DYN + 272)     // composite inertias [12][10]
 #define SCR_AF (SCR_IC + 120)      // actuator forces [8]
 #define SCR_BIAS (SCR_AF + 8)      // RNE bias force of the arm dofs [9]
-#define SCR_OBS 4672               // observation (step end, reset, forward)
-#define SCR_ACT 4768               // raw action of the step (lane 0, before the substeps)
-static_assert(SCR_BIAS + 9 <= 4096 && SCR_OBS + MMX_NOBS <= SCR_ACT && SCR_ACT + 12 <= MMX_MAXEFC * 16,
+#define SCR_OBS 2816               // observation (step end, reset, forward)
+#define SCR_ACT 2912               // raw action of the step (lane 0, before the substeps)
+static_assert(SCR_BIAS + 9 <= 4096 && SCR_OBS + MMX_NOBS <= SCR_ACT && SCR_ACT + 12 <= MMX_LDSEFC * 16,
               "E.J scratch layout");
 static_assert(27 * 27 <= MMX_MAXCON * CON_F, "Newton Cholesky transpose exceeds E.con");
 DEV float* scr_of(EnvSh& E) { return &E.J[0][0]; }
 DEV float* obs_of(EnvSh& E) { return &E.J[0][0] + SCR_OBS; }
 DEV const float* obs_of(const EnvSh& E) { return &E.J[0][0] + SCR_OBS; }
 DEV float* lrow_of(EnvSh& E) { return &E.con[0][0]; }  // [27][27] Newton factor / staging tile
+// Constraint row i: J in E.J[i] and D in E.D[i] for i < MMX_LDSEFC, else in the env's HBM
+// overflow block (J rows [OVFEFC][16], then D [OVFEFC]).  For a lane-owned row i = LANE + 64 q the
+// test folds at compile time (LANE's known bits), so the unrolled loops carry no branch.
+static_assert(MMX_LDSEFC % WG == 0 && MMX_LDSEFC <= MMX_MAXEFC, "LDS rows: whole lane slices");
+DEV float* ovf_j(const EnvSh& E, int i) { return E.ovf + 16 * (i - MMX_LDSEFC); }
+DEV float* ovf_d(const EnvSh& E, int i) { return E.ovf + 16 * MMX_OVFEFC + (i - MMX_LDSEFC); }
+DEV float4 jrow4(const EnvSh& E, int i, int q) {
+  return i < MMX_LDSEFC ? reinterpret_cast<const float4*>(E.J[i])[q] : reinterpret_cast<const float4*>(ovf_j(E, i))[q];
+}
+DEV float jget(const EnvSh& E, int i, int k) { return i < MMX_LDSEFC ? E.J[i][k] : ovf_j(E, i)[k]; }
+DEV void jset(EnvSh& E, int i, int k, float v) {
+  if (i < MMX_LDSEFC) E.J[i][k] = v;
+  else ovf_j(E, i)[k] = v;
+}
+DEV float dget(const EnvSh& E, int i) { return i < MMX_LDSEFC ? E.D[i] : *ovf_d(E, i); }
+DEV void dset(EnvSh& E, int i, float v) {
+  if (i < MMX_LDSEFC) E.D[i] = v;
+  else *ovf_d(E, i) = v;
+}
+// rows written by one lane and read by another: HBM rows need the wave's stores complete first
+// (workgroup scope = s_waitcnt vmcnt(0); the CU's L1 is shared by the wave).  Uniform branch.
+DEV void ovf_fence(int nefc) {
+  if (nefc > MMX_LDSEFC) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+}
 // the last substep's contacts (diagnostic copy, mmx_buffers.contacts), stored once the rows are
 // built: the solver then reuses E.con as scratch
 DEV void store_contacts(float* dst, const EnvSh& E) {
@@ -852,12 +885,12 @@ DEV void row_ref(const float* solref, const float* solimp, float pos, float& imp
 }
 DEV void store_row(EnvSh& E, int row, const float* jv, int hdr, float vel, float imp_ratio, float kid, float B,
                    float diag) {
-  float4* Jr = reinterpret_cast<float4*>(E.J[row]);
+  float4* Jr = reinterpret_cast<float4*>(row < MMX_LDSEFC ? E.J[row] : ovf_j(E, row));
 #pragma unroll
   for (int q = 0; q < 3; q++) Jr[q] = make_float4(jv[4 * q], jv[4 * q + 1], jv[4 * q + 2], jv[4 * q + 3]);
   Jr[3] = make_float4(jv[12], jv[13], jv[14], -B * vel - kid);  // slot 15: aref
   E.hdr[row] = (unsigned char)hdr;
-  E.D[row] = 1.f / fmaxf(imp_ratio * diag, 1e-15f);
+  dset(E, row, 1.f / fmaxf(imp_ratio * diag, 1e-15f));
 }
 
 // per-contact row generator, written by the contact's lane into fields of its own contact record
@@ -955,9 +988,10 @@ DEV void make_constraints_wave(EnvSh& E) {
   const float def_ref[2] = {0.02f, 1.0f};
   const float def_imp[5] = {0.9f, 0.95f, 0.001f, 0.5f, 2.0f};
   const int ncon = E.ncon;
-  // row -> (contact, pyramid edge) map, -1 for the equality / limit rows; it lives in E.D, so the
-  // equality / limit rows (whose store_row writes D) are stored after the contact rows
-  int* rowmap = reinterpret_cast<int*>(E.D);
+  // row -> (contact, pyramid edge) map, -1 for the equality / limit rows; it lives in the rows' D
+  // (dset / dget), so the equality / limit rows (whose store_row writes D) are stored after the
+  // contact rows
+  auto rowmap_set = [&](int r, int m) { dset(E, r, __int_as_float(m)); };
   int nlim = 0, ncr = 0, dim = 0, tc = -1;
   bool lo_act = false, hi_act = false;
   if (LANE < 9) {
@@ -1016,11 +1050,11 @@ DEV void make_constraints_wave(EnvSh& E) {
   }
   int row = arow;
   PROBE(3, stats, STAT_T_AUX0);
-  if (LANE == 0 && row < MMX_MAXEFC) rowmap[row++] = -1;  // finger equality
+  if (LANE == 0 && row < MMX_MAXEFC) rowmap_set(row++, -1);  // finger equality
   if (LANE < 9) {
 #pragma unroll
     for (int side = 0; side < 2; side++)
-      if ((side == 0 ? lo_act : hi_act) && row < MMX_MAXEFC) rowmap[row++] = -1;  // joint limits
+      if ((side == 0 ? lo_act : hi_act) && row < MMX_MAXEFC) rowmap_set(row++, -1);  // joint limits
   }
   PROBE(3, stats, STAT_T_AUX1);
   if (LANE < ncon) {  // contact generator: mixed parameters, reference terms
@@ -1040,12 +1074,13 @@ DEV void make_constraints_wave(EnvSh& E) {
     c[CG_IR] = impr * rot;
     c[CG_KID] = kid;
     c[CG_B] = B;
-    for (int rr = 0; rr < ncr && brow + rr < MMX_MAXEFC; rr++) rowmap[brow + rr] = LANE | (rr << 8);
+    for (int rr = 0; rr < ncr && brow + rr < MMX_MAXEFC; rr++) rowmap_set(brow + rr, LANE | (rr << 8));
   }
+  ovf_fence(nefc);
   SYNC();
   PROBE(3, stats, STAT_T_AUX3);
   for (int r = LANE; r < nefc; r += WG) {
-    const int m = rowmap[r];
+    const int m = __float_as_int(dget(E, r));
     if (m >= 0) contact_row(E, r, m & 255, m >> 8);
   }
   row = arow;
@@ -1076,6 +1111,7 @@ DEV void make_constraints_wave(EnvSh& E) {
       }
     }
   }
+  ovf_fence(nefc);
   SYNC();
   PROBE(3, stats, STAT_T_AUX2);
 }
@@ -1096,11 +1132,10 @@ DEV float readlane_f(float v, int l) { return __int_as_float(__builtin_amdgcn_re
 DEV float row_dot16(const EnvSh& E, int i, const float* x) {
   const int h = E.hdr[i], b0 = h & 15, b1 = (h >> 4) & 15;
   const int d0 = blk_d0(b0), n0 = blk_size(b0), d1 = b1 == BLK_NONE ? 0 : blk_d0(b1);
-  const float4* Jr = reinterpret_cast<const float4*>(E.J[i]);
   float jv[16];
 #pragma unroll
   for (int q = 0; q < 4; q++) {
-    const float4 v = Jr[q];
+    const float4 v = jrow4(E, i, q);
     jv[4 * q] = v.x;
     jv[4 * q + 1] = v.y;
     jv[4 * q + 2] = v.z;
@@ -1157,11 +1192,12 @@ DEV void cost2_wave(const EnvSh& E, const float* xa, const float* xb, float& ca,
     vb[q] = 0.f;
     if (i < E.nefc) {
       const bool eq = i == 0;  // row 0: the finger equality
-      const float aref = E.J[i][15];
+      const float aref = jget(E, i, 15);
       va[q] = row_dot16(E, i, xa) - aref;
       vb[q] = row_dot16(E, i, xb) - aref;
-      if (eq || va[q] < 0.f) c0 += 0.5f * E.D[i] * va[q] * va[q];
-      if (eq || vb[q] < 0.f) c1 += 0.5f * E.D[i] * vb[q] * vb[q];
+      const float D = dget(E, i);
+      if (eq || va[q] < 0.f) c0 += 0.5f * D * va[q] * va[q];
+      if (eq || vb[q] < 0.f) c1 += 0.5f * D * vb[q] * vb[q];
     }
   }
   ca = wave_sum(c0);
@@ -1193,6 +1229,7 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
     if (r1 <= r0) continue;
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
     for (int s0 = r0; s0 < r1; s0 += 8) {  // 2 MFMA steps per trip, loads first
+      const bool all_lds = s0 + 8 <= MMX_LDSEFC;  // uniform: the trip's rows are all LDS rows
       float jv[2], w[2];
       bool valid[2];
 #pragma unroll
@@ -1200,8 +1237,13 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
         const int r = s0 + 4 * u + rk;
         valid[u] = r < r1;
         const int rc = valid[u] ? r : r0;
-        jv[u] = E.J[rc][col];  // slot 15 holds w r
-        w[u] = E.D[rc];        // active weight s
+        if (all_lds) {
+          jv[u] = E.J[rc][col];  // slot 15 holds w r
+          w[u] = E.D[rc];        // active weight s
+        } else {
+          jv[u] = jget(E, rc, col);
+          w[u] = dget(E, rc);
+        }
       }
 #pragma unroll
       for (int u = 0; u < 2; u++) {
@@ -1382,7 +1424,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
 #pragma unroll
   for (int q = 0; q < RPL; q++) {
     const int i = LANE + WG * q;
-    dd[q] = i < nefc ? E.D[i] : 0.f;
+    dd[q] = i < nefc ? dget(E, i) : 0.f;
     eq[q] = i == 0;  // row 0: the finger equality (always present)
     rr[q] = from_ws ? ra[q] : rs[q];
     jp[q] = 0.f;
@@ -1403,10 +1445,11 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
       if (i < nefc) {
         const float v = rr[q];
         const float w = (eq[q] || v < 0.f) ? dd[q] : 0.f;
-        E.J[i][15] = w * v;  // w r for the gradient (the row's aref slot is dead after the setup)
-        E.D[i] = w;          // s (D itself is in registers since the setup)
+        jset(E, i, 15, w * v);  // w r for the gradient (the row's aref slot is dead after the setup)
+        dset(E, i, w);          // s (D itself is in registers since the setup)
       }
     }
+    ovf_fence(nefc);
     SYNC();
     PROBE(1, stats, STAT_T_AUX0);
     float hrow[32];
@@ -2138,6 +2181,7 @@ DEV void load_env(const MMXState& S, int i, EnvSh& E) {
   if (LANE < 4) E.target[LANE] = S.target[(size_t)i * 4 + LANE];
   if (LANE < STAT_N) E.stats[LANE] = S.stats[(size_t)i * STAT_N + LANE];
   if (LANE == 0) {
+    E.ovf = S.efc_ovf + (size_t)i * MMX_OVF_F;
     E.flags = 0;
     E.ncon = 0;
     E.nefc = 0;

@@ -15,6 +15,13 @@
 #define MMX_NOBS 85
 #define MMX_MAXCON 64
 #define MMX_MAXEFC 304
+// constraint rows [0, MMX_LDSEFC) live in the workgroup's LDS, rows [MMX_LDSEFC, MMX_MAXEFC) in the
+// env's HBM overflow block (efc_ovf); 192 rows keep the env's LDS under 20 KB (8 envs per CU)
+#ifndef MMX_LDSEFC
+#define MMX_LDSEFC 192
+#endif
+#define MMX_OVFEFC (MMX_MAXEFC - MMX_LDSEFC)
+#define MMX_OVF_F (MMX_OVFEFC * 17)  // floats per env: J rows [OVFEFC][16], then D [OVFEFC]
 #define MMX_NSUBSTEP 16
 
 // stale kinematics cache read by the IK (controller.py:99-108 reads data.xpos / mj_jac
@@ -89,6 +96,7 @@ struct MMXState {
   // diagnostics
   float* con;    // [N][MAXCON][CON_F] contacts of the last substep
   float* stats;  // [N][STAT_N]
+  float* efc_ovf;  // [N][MMX_OVF_F] constraint rows past the LDS ones (scratch, rarely touched)
   // camera images (image_size > 0 only, else null)
   float* rpose;            // [N][14][12] body poses (R row-major, p) of the last position stage
   unsigned char* images;   // [N][2][S][S][3] overhead, wrist RGB

@@ -52,16 +52,18 @@ def oracle_states(n=40):
     return [states[i] for i in idx]
 
 
-def _physics_parity(nsub):
+def _physics_parity(nsub, sts=None, nefc_out=None):
     import oracle_py as O
     from mujoco_manip_amd import _lib
 
-    sts = oracle_states()
+    sts = oracle_states() if sts is None else sts
     qpos, qvel, ctrl, ws = [np.stack([s[k] for s in sts]).astype(np.float32) for k in range(4)]
     sim = _lib.Sim(len(sts))
     sim.set_state(qpos, qvel, ctrl, ws)
     sim.physics_step(nsub)
     gq, gv, _, _ = sim.get_state()
+    if nefc_out is not None:  # constraint rows of the run (summed over its substeps), per env
+        nefc_out.append(sim.view("stats", _lib.STAT_N)[:, 0].cpu().numpy().copy())
     err_q, err_v = [], []
     for k in range(len(sts)):
         e = O.OracleEnv()
@@ -84,6 +86,46 @@ def test_physics_parity_one_substep():  # L1: fp32 GPU vs fp64 oracle, contacts 
 
 def test_physics_parity_one_env_step():  # L1: 16 substeps; SURVEY bound qpos <= 1e-4
     dq, dv = _physics_parity(16)
+    assert dq.max() < 1e-4, dq.max()
+    assert dv.max() < 2e-2, dv.max()
+
+
+def _pile_states(n_want=6, min_mean_nefc=215.0):
+    """States (qpos, qvel, ctrl, warm start) just before C3 env steps whose substeps averaged more
+    than `min_mean_nefc` constraint rows: piles of contacts whose rows past MMX_LDSEFC (192) live
+    in the env's HBM overflow block instead of LDS."""
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    import oracle_py as O
+
+    env = PickPlaceVecEnv(1024, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
+                          autoreset=True, image_size=0)
+    env.reset(seed=[O.episode_seed(42, i) for i in range(1024)])
+    found = []
+    for _ in range(400):
+        snap = env.sim.get_state()
+        before = env.stats[:, 0].clone()
+        env.step(env.expert_plan(16))
+        mean = ((env.stats[:, 0] - before) / 16).cpu().numpy()
+        for k in np.where(mean > min_mean_nefc)[0]:
+            found.append(tuple(a[k].astype(float) for a in snap))
+        if len(found) >= n_want:
+            break
+    env.close()
+    return found[:n_want]
+
+
+def test_physics_parity_hbm_overflow_rows():  # L1 on contact piles: rows 192..303 live in HBM
+    sts = _pile_states()
+    assert len(sts) >= 4, f"only {len(sts)} pile states in 400 C3 steps"
+    rows1, rows16 = [], []
+    dq, dv = _physics_parity(1, sts, rows1)
+    print(f"pile states: rows of the first substep {rows1[0].astype(int).tolist()}, errors qpos {dq.max():.2e} "
+          f"qvel {dv.max():.2e}")
+    assert (rows1[0] > 192).any(), f"no substep used the overflow rows: {rows1[0]}"
+    assert dq.max() < 1e-5, dq.max()
+    assert dv.max() < 5e-3, dv.max()
+    dq, dv = _physics_parity(16, sts, rows16)
     assert dq.max() < 1e-4, dq.max()
     assert dv.max() < 2e-2, dv.max()
 
