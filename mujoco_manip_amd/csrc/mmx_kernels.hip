@@ -2321,8 +2321,10 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_substep_kernel(MMXState S, 
 // scratch vs. contacts / J scratch; contacts from both waves meet through an LDS atomic).
 // Everything else runs on wave 0.  This form (MMX_TWO_WAVE) is register-bound at 4 workgroups
 // per CU (2 x 250 VGPRs per SIMD).  The product build is the single-wave form: the env's LDS
-// footprint (27,136 B) admits 6 workgroups per CU, which beats splitting one env over two waves
-// (measured: 1.11 M env steps/s for two waves at 4 / CU vs 1.21 M single-wave at 5 / CU).
+// footprint (19,232 B with rows past MMX_LDSEFC in HBM) admits 8 workgroups per CU, which beats
+// splitting one env over two waves (measured: 1.11 M env steps/s for two waves at 4 / CU vs 1.21 M
+// single-wave at 5 / CU).  The two-wave form needs -DMMX_LDSEFC=304 (its EPA scratch sits beside
+// the box-box polygons).
 #ifdef MMX_TWO_WAVE
 #define STEP_WG 128
 #else
