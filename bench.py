@@ -99,8 +99,10 @@ def cpu_baseline(seconds: float = 12.0, workers: int | None = None) -> dict:
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=500)   # >= 500 timed env steps
-    ap.add_argument("--warmup", type=int, default=50)   # 50 warm-up env steps
+    # >= 500 timed env steps after >= 50 warm-up steps; multiples of the fused
+    # launch length (16 env steps per launch) keep every timed dispatch the same size
+    ap.add_argument("--steps", type=int, default=512)
+    ap.add_argument("--warmup", type=int, default=64)
     ap.add_argument("--envs-per-gpu", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -172,7 +174,10 @@ def main():
     if dist:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps  # per launch
+    # each lane runs ceil(K / spl) launches of up to spl env steps of its envs, back to back
+    spl = env.sim.rollout_steps_per_launch
+    launches = -(-args.steps // spl)
+    kern_ms = ev0.elapsed_time(ev1) / launches  # per launch
     if dist:
         t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -181,14 +186,16 @@ def main():
     env_steps = args.steps * N * world
     value = env_steps / elapsed
     ms_per_step = 1000.0 * elapsed / args.steps
-    # one env step of the batch = `lanes` concurrent mmx_env_step_kernel dispatches of N / lanes
-    # envs each; they run side by side for the whole span, so a dispatch lasts ~kern_ms (rocprof's
-    # per-dispatch average agrees) and the chip-level rate is lanes x one dispatch's bytes / kern_ms
+    # spl env steps of the batch = `lanes` concurrent mmx_env_step_kernel dispatches of N / lanes
+    # envs x spl steps each; they run side by side for the whole span, so a dispatch lasts ~kern_ms
+    # (rocprof's per-dispatch average agrees) and the chip-level rate is lanes x one dispatch's
+    # bytes / kern_ms
     lanes = env.sim.rollout_lanes
     envs_per_launch = N / lanes
-    bytes_per_launch = algorithmic_bytes_per_env_step(solver["mean_nefc"]) * envs_per_launch
+    steps_per_launch = args.steps / launches
+    bytes_per_launch = algorithmic_bytes_per_env_step(solver["mean_nefc"]) * envs_per_launch * steps_per_launch
     achieved = lanes * bytes_per_launch / (kern_ms * 1e-3) / 1e9
-    min_bytes = min_hbm_bytes_per_env_step() * envs_per_launch
+    min_bytes = min_hbm_bytes_per_env_step() * envs_per_launch * steps_per_launch
 
     stats_all = None
     if dist:
@@ -224,6 +231,7 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "mmx_env_step_kernel", "kernel_ms": kern_ms,
                          "concurrent_launches": lanes, "envs_per_launch": envs_per_launch,
+                         "env_steps_per_launch": steps_per_launch,
                          "algorithmic_bytes_per_env_step": algorithmic_bytes_per_env_step(solver["mean_nefc"]),
                          "algorithmic_bytes_per_launch": bytes_per_launch, "mean_nefc": solver["mean_nefc"],
                          "traffic_note": "traffic = PMC FETCH_SIZE x2 + WRITE_SIZE per dispatch "

@@ -118,6 +118,12 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps);
  * range per 1024 envs).  Single-step calls always run as one launch on cfg.stream. */
 int mmx_rollout_lanes(const mmx_sim* sim);
 
+/* Env steps one mmx_env_step_kernel launch runs per env in mmx_rollout_expert: 1 with cameras
+ * (every step is rendered), else up to 16 (env MMX_FUSE overrides).  A fused launch runs its
+ * envs' steps back to back inside each workgroup; the trajectories are bit-identical to one
+ * launch per step.  0 for a null sim. */
+int mmx_rollout_steps_per_launch(const mmx_sim* sim);
+
 /* Physics-level entry points (parity harnesses): n x mujoco.mj_step with the current ctrl
  * (env.py:119-121), optionally preceded by IKController.compute toward the decoded target
  * each substep; and the mj_forward position stage (kinematics + IK cache). */

@@ -52,7 +52,8 @@ class MMXBuffers(C.Structure):
 
 EXPORTED = ("mmx_config_default", "mmx_create", "mmx_destroy", "mmx_last_error", "mmx_reset", "mmx_step",
             "mmx_expert_plan", "mmx_rollout_expert", "mmx_physics_step", "mmx_forward", "mmx_get_buffers",
-            "mmx_synchronize", "mmx_get_state", "mmx_set_state", "mmx_episode_seed", "mmx_rollout_lanes")
+            "mmx_synchronize", "mmx_get_state", "mmx_set_state", "mmx_episode_seed", "mmx_rollout_lanes",
+            "mmx_rollout_steps_per_launch")
 
 _lib = None
 
@@ -83,6 +84,8 @@ def load(build_if_missing: bool = True):
     L.mmx_physics_step.argtypes = [vp, C.c_int32, C.c_int32]
     L.mmx_rollout_lanes.argtypes = [vp]
     L.mmx_rollout_lanes.restype = C.c_int
+    L.mmx_rollout_steps_per_launch.argtypes = [vp]
+    L.mmx_rollout_steps_per_launch.restype = C.c_int
     L.mmx_forward.argtypes = [vp]
     L.mmx_get_buffers.argtypes = [vp, C.POINTER(MMXBuffers)]
     L.mmx_synchronize.argtypes = [vp]
@@ -210,6 +213,10 @@ class Sim:
     @property
     def rollout_lanes(self) -> int:
         return int(self.L.mmx_rollout_lanes(self.ptr))
+
+    @property
+    def rollout_steps_per_launch(self) -> int:
+        return int(self.L.mmx_rollout_steps_per_launch(self.ptr))
 
     def physics_step(self, n: int = 1, with_ik: bool = False):
         self._check(self.L.mmx_physics_step(self.ptr, n, int(with_ik)), "mmx_physics_step")

@@ -18,7 +18,7 @@
 
 extern "C" hipError_t mmx_launch_reset(const MMXState* S, const unsigned char* mask, const int* task, hipStream_t st);
 extern "C" hipError_t mmx_launch_step(const MMXState* S, const float* action, int adim, int expert_autoreset,
-                                      int base, int count, hipStream_t st);
+                                      int base, int count, int nsteps, hipStream_t st);
 extern "C" hipError_t mmx_launch_expert(const MMXState* S, int n, float* action, hipStream_t st);
 extern "C" hipError_t mmx_launch_physics(const MMXState* S, int n, int with_ik, hipStream_t st);
 extern "C" hipError_t mmx_launch_forward(const MMXState* S, hipStream_t st);
@@ -38,6 +38,8 @@ struct mmx_sim {
   // so one range's last-wave tail overlaps the next step of the others.
   static constexpr int kMaxLanes = 8;
   int nlanes = 1;
+  // env steps per mmx_env_step_kernel launch in expert rollouts without cameras (MMX_FUSE overrides)
+  int fuse = 16;
   hipStream_t lane[kMaxLanes] = {};
   hipEvent_t ev_fork = nullptr, ev_join[kMaxLanes] = {};
 };
@@ -249,6 +251,7 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
   // 1024 resident step workgroups), at most kMaxLanes
   int lanes = N / 1024;
   if (const char* v = std::getenv("MMX_STREAMS")) lanes = std::atoi(v);
+  if (const char* v = std::getenv("MMX_FUSE")) sim->fuse = std::max(1, std::atoi(v));
   lanes = std::max(1, std::min(lanes, std::min(N, int(mmx_sim::kMaxLanes))));
   if (hipEventCreateWithFlags(&sim->ev_fork, hipEventDisableTiming) != hipSuccess) lanes = 1;
   for (int l = 1; l < lanes; l++)
@@ -331,7 +334,7 @@ int mmx_step(mmx_sim* sim, const float* action_dev, int32_t action_dim) {
   if (!sim || !action_dev) return MMX_EINVAL;
   static const int kDim[5] = {4, 8, 10, 8, 10};
   if (action_dim < kDim[sim->S.action_mode]) return fail(sim, MMX_EINVAL, "action_dim too small for action_mode");
-  hipError_t e = mmx_launch_step(&sim->S, action_dev, action_dim, 0, 0, sim->S.N, sim->stream);
+  hipError_t e = mmx_launch_step(&sim->S, action_dev, action_dim, 0, 0, sim->S.N, 1, sim->stream);
   if (e == hipSuccess) e = mmx_launch_render(&sim->S, 0, sim->S.N, sim->stream);
   return hip_check(sim, e, "mmx_step");
 }
@@ -350,14 +353,18 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
     for (int l = 1; l < L && e == hipSuccess; l++) e = hipStreamWaitEvent(sim->lane[l], sim->ev_fork, 0);
   }
   // the step kernel plans with the FSM itself (expert=1); step k of range l only depends on step
-  // k-1 of range l
-  for (int k = 0; k < n_env_steps && e == hipSuccess; k++)
+  // k-1 of range l.  Without cameras a launch runs up to `fuse` consecutive steps of its envs
+  // (mmx_rollout_steps_per_launch); with cameras every step is rendered, one step per launch.
+  const int fuse = sim->S.image_size > 0 ? 1 : sim->fuse;
+  for (int k = 0; k < n_env_steps && e == hipSuccess; k += fuse) {
+    const int ns = std::min(fuse, n_env_steps - k);
     for (int l = 0; l < L && e == hipSuccess; l++) {
       const int b0 = (int)((long)N * l / L), b1 = (int)((long)N * (l + 1) / L);
       hipStream_t st = l ? sim->lane[l] : sim->stream;
-      e = mmx_launch_step(&sim->S, sim->expert_action, 4, 1, b0, b1 - b0, st);
+      e = mmx_launch_step(&sim->S, sim->expert_action, 4, 1, b0, b1 - b0, ns, st);
       if (e == hipSuccess) e = mmx_launch_render(&sim->S, b0, b1 - b0, st);
     }
+  }
   if (L > 1)  // join: the caller's stream sees the whole rollout, as with a single launch chain
     for (int l = 1; l < L; l++) {
       hipError_t j = hipEventRecord(sim->ev_join[l], sim->lane[l]);
@@ -368,6 +375,10 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
 }
 
 int mmx_rollout_lanes(const mmx_sim* sim) { return sim ? sim->nlanes : 0; }
+
+int mmx_rollout_steps_per_launch(const mmx_sim* sim) {
+  return sim ? (sim->S.image_size > 0 ? 1 : sim->fuse) : 0;
+}
 
 int mmx_physics_step(mmx_sim* sim, int32_t n, int32_t with_ik) {
   if (!sim || n < 0) return MMX_EINVAL;

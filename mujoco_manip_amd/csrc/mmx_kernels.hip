@@ -2385,16 +2385,24 @@ __device__ __attribute__((noinline)) void substep(int max_iter, float tol, float
 #endif
 }
 
-// The whole PickPlaceGymEnv.step in ONE launch per env step (product path): the 16 substeps
-// loop inside the workgroup, so per-env cost variation averages out over the step instead of
-// stretching 16 separate launch tails (measured: one launch per substep ran 40 % slower).
+// The whole PickPlaceGymEnv.step in ONE launch (product path): the 16 substeps loop inside the
+// workgroup, so per-env cost variation averages out over the step instead of stretching 16
+// separate launch tails (measured: one launch per substep ran 40 % slower).  With the on-device
+// FSM expert (expert = 1) a launch may also run `nsteps` consecutive env steps of its env: each
+// iteration is exactly one launch's body (record loaded, stepped, stored), so the trajectory is
+// bit-identical to nsteps single-step launches, minus nsteps - 1 launch tails.
 extern "C" __global__ void __launch_bounds__(STEP_WG) __attribute__((amdgpu_waves_per_eu(2, 2)))
-mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert, int base) {
+mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert, int base, int nsteps) {
   EnvSh& E = g_E;
   float* act = scr_of(E) + SCR_ACT;  // lane 0's decoded action (E.J is free before the substeps)
   const int i = base + blockIdx.x;
   if (i >= S.N) return;
   const bool w0 = STEP_WG == 64 || WAVE_ID == 0;
+  for (int k = 0; k < nsteps; k++) {
+  if (k) {  // the previous step's record stores complete before this step reloads it
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    XSYNC();
+  }
   if (w0) {
     load_env(S, i, E);
     if (LANE == 0) {
@@ -2411,6 +2419,7 @@ mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert, int b
   if (w0) {
     step_end(S, i, E, expert != 0);
     store_env(S, i, E);
+  }
   }
 }
 
@@ -2465,9 +2474,10 @@ extern "C" hipError_t mmx_launch_reset(const MMXState* S, const unsigned char* m
 }
 // envs [base, base+count): independent env ranges may run on separate streams
 extern "C" hipError_t mmx_launch_step(const MMXState* S, const float* action, int adim, int expert, int base,
-                                      int count, hipStream_t st) {
-  if (count <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mmx_env_step_kernel, dim3(count), dim3(STEP_WG), 0, st, *S, action, adim, expert, base);
+                                      int count, int nsteps, hipStream_t st) {
+  if (count <= 0 || nsteps <= 0) return hipSuccess;
+  if (nsteps > 1 && !expert) return hipErrorInvalidValue;  // host actions: one env step per launch
+  hipLaunchKernelGGL(mmx_env_step_kernel, dim3(count), dim3(STEP_WG), 0, st, *S, action, adim, expert, base, nsteps);
   return hipGetLastError();
 }
 extern "C" hipError_t mmx_launch_expert(const MMXState* S, int n, float* action, hipStream_t st) {

@@ -343,6 +343,36 @@ def test_rollout_lanes_bit_identical(monkeypatch):
     np.testing.assert_array_equal(outs[0], outs[1])
 
 
+def test_fused_rollout_bit_identical(monkeypatch):
+    """Several env steps per launch (mmx_rollout_steps_per_launch) change nothing but timing:
+    state, episode records, observations, rewards, flags and solver stats match one launch per
+    step bit for bit, incl. autoresets inside a fused launch and a ragged last chunk (40 = 5 x 7 + 5)."""
+    import oracle_py as O
+    from mujoco_manip_amd import _lib
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    seeds = [O.episode_seed(5, i) for i in range(12)]
+    outs = []
+    for lanes, fuse in (("1", "1"), ("1", "7"), ("3", "32")):
+        monkeypatch.setenv("MMX_STREAMS", lanes)
+        monkeypatch.setenv("MMX_FUSE", fuse)
+        env = PickPlaceVecEnv(12, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
+                              autoreset=True, image_size=0, max_episode_steps=25)
+        assert env.sim.rollout_steps_per_launch == int(fuse)
+        env.reset(seed=seeds)
+        env.rollout_expert(40)
+        torch.cuda.synchronize()
+        q, v, _, _ = env.sim.get_state()
+        s = env.sim
+        outs.append(np.concatenate([q, v, s.view("episode_i", _lib.EPI_N, "<i4").cpu().numpy().view(np.float32),
+                                    s.view("obs", _lib.NOBS).cpu().numpy(), s.view("reward", 1).cpu().numpy()[:, None],
+                                    s.view("done", 3, "<i4").cpu().numpy().view(np.float32),
+                                    env.stats[:, :4].cpu().numpy()], 1))
+        env.close()
+    np.testing.assert_array_equal(outs[0], outs[1])
+    np.testing.assert_array_equal(outs[0], outs[2])
+
+
 def _lib_epi_n():
     from mujoco_manip_amd import _lib
 

@@ -10,12 +10,12 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/prof
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-STEPS=${PROF_STEPS:-40}
+STEPS=${PROF_STEPS:-48}  # multiples of the 16-step fused launch: equal-size dispatches
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
-  python3 $ROOT/bench.py --steps $STEPS --warmup 5 --no-cpu-baseline > $OUT/bench_trace.log 2>&1
+  python3 $ROOT/bench.py --steps $STEPS --warmup 16 --no-cpu-baseline > $OUT/bench_trace.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- \
-  python3 $ROOT/bench.py --steps 8 --warmup 2 --no-cpu-baseline > $OUT/bench_fetch.log 2>&1
+  python3 $ROOT/bench.py --steps 16 --warmup 16 --no-cpu-baseline > $OUT/bench_fetch.log 2>&1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- \
-  python3 $ROOT/bench.py --steps 8 --warmup 2 --no-cpu-baseline > $OUT/bench_write.log 2>&1
+  python3 $ROOT/bench.py --steps 16 --warmup 16 --no-cpu-baseline > $OUT/bench_write.log 2>&1
 cd $ROOT
 python3 tools/pmc_traffic.py --round $ROUND --prof $OUT
