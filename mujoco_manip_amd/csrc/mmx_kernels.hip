@@ -2391,35 +2391,42 @@ __device__ __attribute__((noinline)) void substep(int max_iter, float tol, float
 // FSM expert (expert = 1) a launch may also run `nsteps` consecutive env steps of its env: each
 // iteration is exactly one launch's body (record loaded, stepped, stored), so the trajectory is
 // bit-identical to nsteps single-step launches, minus nsteps - 1 launch tails.
-extern "C" __global__ void __launch_bounds__(STEP_WG) __attribute__((amdgpu_waves_per_eu(2, 2)))
-mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert, int base, int nsteps) {
+// The step's prologue (record load, FSM plan, action decode) and epilogue (position stage, reward,
+// observation, autoreset, record store) are out of line like the substep: inlined into the fused
+// step loop they kept ~280 VGPRs of hoisted values live across iterations (scratch spills).
+__device__ __attribute__((noinline)) void step_begin(const MMXState& S, int i, const float* action, int adim,
+                                                     int expert) {
   EnvSh& E = g_E;
   float* act = scr_of(E) + SCR_ACT;  // lane 0's decoded action (E.J is free before the substeps)
+  load_env(S, i, E);
+  if (LANE == 0) {
+    if (expert) expert_plan(S, i, obj_pos(E, EPI(EPI_OBJ)), hand_pos(E), MMX_NSUBSTEP, act);
+    else
+      for (int k = 0; k < adim && k < 12; k++) act[k] = action[(size_t)i * adim + k];
+    decode_lane0(S, i, E, act);
+  }
+  SYNC();
+}
+__device__ __attribute__((noinline)) void step_finish(const MMXState& S, int i, int expert) {
+  EnvSh& E = g_E;
+  step_end(S, i, E, expert != 0);
+  store_env(S, i, E);
+}
+extern "C" __global__ void __launch_bounds__(STEP_WG) __attribute__((amdgpu_waves_per_eu(2, 2)))
+mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert, int base, int nsteps) {
   const int i = base + blockIdx.x;
   if (i >= S.N) return;
   const bool w0 = STEP_WG == 64 || WAVE_ID == 0;
   for (int k = 0; k < nsteps; k++) {
-  if (k) {  // the previous step's record stores complete before this step reloads it
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-    XSYNC();
-  }
-  if (w0) {
-    load_env(S, i, E);
-    if (LANE == 0) {
-      if (expert) expert_plan(S, i, obj_pos(E, EPI(EPI_OBJ)), hand_pos(E), MMX_NSUBSTEP, act);
-      else
-        for (int k = 0; k < adim && k < 12; k++) act[k] = action[(size_t)i * adim + k];
-      decode_lane0(S, i, E, act);
+    if (k) {  // the previous step's record stores complete before this step reloads it
+      __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+      XSYNC();
     }
-    SYNC();
-  }
-  XSYNC();
-  for (int sub = 0; sub < MMX_NSUBSTEP; sub++)
-    substep(S.solver_max_iter, S.solver_tol, sub == MMX_NSUBSTEP - 1 ? contacts_dst(S, i) : nullptr);
-  if (w0) {
-    step_end(S, i, E, expert != 0);
-    store_env(S, i, E);
-  }
+    if (w0) step_begin(S, i, action, adim, expert);
+    XSYNC();
+    for (int sub = 0; sub < MMX_NSUBSTEP; sub++)
+      substep(S.solver_max_iter, S.solver_tol, sub == MMX_NSUBSTEP - 1 ? contacts_dst(S, i) : nullptr);
+    if (w0) step_finish(S, i, expert);
   }
 }
 
