@@ -23,8 +23,13 @@ ARCH = os.environ.get("MMX_OFFLOAD_ARCH", "gfx950")
 # The env-step kernel is VALU-issue-bound at 8 envs per CU: -11 % VALU instructions in the substep,
 # +3.7 % env steps/s (C3), parity tolerances unchanged.  Host code keeps IEEE semantics.
 DEVICE_MATH = ["-Xarch_device", "-freciprocal-math", "-Xarch_device", "-fapprox-func"]
+# gfx950 machine scheduler: the iterative ILP strategy (schedules for latency within the 256-VGPR
+# budget the 2-waves-per-SIMD occupancy allows) measured +6.4 % env steps/s over the default
+# occupancy-driven scheduler on the C3 bench (max-ilp +2 %, max-memory-clause +0 %).  The option
+# is an LLVM backend flag; the host compile accepts and ignores it.
+DEVICE_SCHED = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
 # extra compiler flags (experiments only; the committed build uses none)
-FLAGS = DEVICE_MATH + os.environ.get("MMX_EXTRA_FLAGS", "").split()
+FLAGS = DEVICE_MATH + DEVICE_SCHED + os.environ.get("MMX_EXTRA_FLAGS", "").split()
 
 
 def lib_path(profile: bool = False) -> str:
