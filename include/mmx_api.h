@@ -115,7 +115,7 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps);
 
 /* Number of independent env ranges a multi-step rollout runs concurrently (one internal stream
  * each, forked from and joined back to cfg.stream; env MMX_STREAMS overrides the default of one
- * range per 1024 envs).  Single-step calls always run as one launch on cfg.stream. */
+ * range per 1024 envs, at most 4).  Single-step calls always run as one launch on cfg.stream. */
 int mmx_rollout_lanes(const mmx_sim* sim);
 
 /* Env steps one mmx_env_step_kernel launch runs per env in mmx_rollout_expert: 1 with cameras
