@@ -2336,7 +2336,12 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_substep_kernel(MMXState S, 
 #else
 #define STEP_WG 64
 #endif
-__device__ __attribute__((noinline)) void substep(int max_iter, float tol, float* con_dst) {
+#ifdef MMX_SUBSTEP_INLINE  // experiment: the substep inlined into the step loop (spills hoisted values)
+#define MMX_SUBSTEP_ATTR always_inline
+#else
+#define MMX_SUBSTEP_ATTR noinline
+#endif
+__device__ __attribute__((MMX_SUBSTEP_ATTR)) void substep(int max_iter, float tol, float* con_dst) {
   EnvSh& E = g_E;
   float* stats = E.stats;
 #ifndef MMX_TWO_WAVE
