@@ -14,7 +14,9 @@
  *  - sim-owned buffers returned by mmx_get_buffers stay valid until mmx_destroy;
  *  - all launches are asynchronous on the sim's stream (cfg.stream, or the null stream);
  *  - one sim per host thread at a time (not re-entrant); per-env faults go to the
- *    env_error buffer, never to return codes.
+ *    env_error buffer, never to return codes;
+ *  - every entry point makes the sim's device (cfg.device) current for its HIP calls and
+ *    restores the caller's current device before returning.
  */
 #ifndef MMX_API_H
 #define MMX_API_H
@@ -70,11 +72,18 @@ typedef struct {
   float* reward;             /* [N] */
   int32_t* done;             /* [N][3] terminated, truncated, success */
   float* reward_components;  /* [N][6] staged breakdown (gym_env.py:568-573) */
-  int32_t* episode_i;        /* [N][14] obj, bin, step_count, flags, fsm_state, fsm_task_index,
+  int32_t* episode_i;        /* [N][18] obj, bin, step_count, flags, fsm_state, fsm_task_index,
                                 fsm_settle, fsm_gripper_open, fsm_has_target, env_error, ncon, nefc,
-                                episodes, rng_has32 */
+                                episodes (resets so far), rng_has32, then sticky counters never
+                                cleared by a reset: successes (episodes that ended with
+                                info["success"] under autoreset), placed (episodes that ended with
+                                the target cube in the target bin), error_resets (autoresets forced by
+                                a diverged state: NaN / Inf / |qvel| or |qacc| >= 1e10, reported
+                                as truncated), and fsm_phases (bitmask of the FSM states visited
+                                since the last reset) */
   float* episode_f;          /* [N][28] T_init(12), hwm(5), target_kp(4), fsm_target(3), transit(3), return */
-  float* kin;                /* [N][54] hand pos/mat + arm joint axes/anchors of the last position stage */
+  float* kin;                /* [N][63] hand pos/mat, arm joint axes/anchors and cube positions of the
+                                last position stage (what data.xpos holds after mj_step) */
   float* stats;              /* [N][17] sum nefc, sum ncon, sum solver iterations, substeps, max residual,
                                 then shader-clock cycles spent per phase: ik, kinematics, dynamics,
                                 collision, constraints, solver, integrate, step end (reward/obs/reset),
@@ -84,6 +93,8 @@ typedef struct {
                                 rendered after every reset / step / forward; NULL when image_size = 0 */
   uint8_t* seg;              /* [N][2][S][S] segment ids: 0 sky, 1 floor, 2 table, 3-5 bins (red, green,
                                 blue), 6-8 cubes (red, green, blue), 9 robot; NULL when image_size = 0 */
+  float* target;             /* [N][4] decoded EE target (IKController.compute's target_pos) + gripper
+                                value of the current step; writable for physics-level harnesses */
 } mmx_buffers;
 
 void mmx_config_default(mmx_config* cfg);
@@ -129,6 +140,21 @@ int mmx_rollout_steps_per_launch(const mmx_sim* sim);
  * each substep; and the mj_forward position stage (kinematics + IK cache). */
 int mmx_physics_step(mmx_sim* sim, int32_t n, int32_t with_ik);
 int mmx_forward(mmx_sim* sim);
+
+/* Per-physics-step expert loop (main.py:65-91; tests/test_pick_and_place.py:147-166):
+ * n x (PickAndPlaceTask.update() = plan(1) + _actuate() (pick_and_place.py:279-304) ;
+ * mujoco.mj_step), the FSM reading data.xpos as the previous mj_step left it.  No gym
+ * bookkeeping (no reward, observation or autoreset); the FSM state is in episode_i. */
+int mmx_expert_physics(mmx_sim* sim, int32_t n_physics_steps);
+
+/* Reward-layer parity harness (gym_env.py:341-470, 562-573).  For every env: the object at
+ * obj_dev[N][3], the EE at ee_dev[N][3], gripper ctrl ctrl7_dev[N] and this step's contacts as
+ * geom-id pairs pairs_dev[N][max_pairs][2] (int32, a negative id ends the list; geom ids as in the
+ * compiled model = MuJoCo's).  Evaluates _compute_reward, updating the sticky flags and
+ * high-water marks like a step, and writes reward, reward_components, done[0] (terminated) and
+ * done[2] (success).  All pointers are device pointers. */
+int mmx_eval_reward(mmx_sim* sim, const float* obj_dev, const float* ee_dev, const float* ctrl7_dev,
+                    const int32_t* pairs_dev, int32_t max_pairs);
 
 int mmx_get_buffers(mmx_sim* sim, mmx_buffers* out);
 int mmx_synchronize(mmx_sim* sim);

@@ -17,9 +17,11 @@ from . import _build
 
 NQ, NV, NU, NOBS = 30, 27, 8, 85
 MAXCON, CON_F = 64, 12
-EPI_N, EPF_N, KIN_N, STAT_N = 14, 28, 54, 17
+EPI_N, EPF_N, KIN_N, STAT_N = 18, 28, 63, 17
 EPI_FIELDS = ("obj", "bin", "step_count", "flags", "fsm_state", "fsm_task_index", "fsm_settle", "fsm_gripper_open",
-              "fsm_has_target", "env_error", "ncon", "nefc", "episodes", "rng_has32")
+              "fsm_has_target", "env_error", "ncon", "nefc", "episodes", "rng_has32", "successes", "placed", "error_resets",
+              "fsm_phases")
+EPI = {name: k for k, name in enumerate(EPI_FIELDS)}
 STAT_FIELDS = ("sum_nefc", "sum_ncon", "sum_solver_iter", "substeps", "max_resid", "cyc_ik", "cyc_kinematics",
                "cyc_dynamics", "cyc_collision", "cyc_constraints", "cyc_solver", "cyc_integrate", "cyc_step_end",
                "cyc_aux0", "cyc_aux1", "cyc_aux2", "cyc_aux3")
@@ -46,14 +48,14 @@ class MMXBuffers(C.Structure):
         ("qacc_warmstart", C.c_void_p), ("obs", C.c_void_p), ("reward", C.c_void_p), ("done", C.c_void_p),
         ("reward_components", C.c_void_p), ("episode_i", C.c_void_p), ("episode_f", C.c_void_p),
         ("kin", C.c_void_p), ("stats", C.c_void_p), ("contacts", C.c_void_p),
-        ("images", C.c_void_p), ("seg", C.c_void_p),
+        ("images", C.c_void_p), ("seg", C.c_void_p), ("target", C.c_void_p),
     ]
 
 
 EXPORTED = ("mmx_config_default", "mmx_create", "mmx_destroy", "mmx_last_error", "mmx_reset", "mmx_step",
             "mmx_expert_plan", "mmx_rollout_expert", "mmx_physics_step", "mmx_forward", "mmx_get_buffers",
             "mmx_synchronize", "mmx_get_state", "mmx_set_state", "mmx_episode_seed", "mmx_rollout_lanes",
-            "mmx_rollout_steps_per_launch")
+            "mmx_rollout_steps_per_launch", "mmx_expert_physics", "mmx_eval_reward")
 
 _lib = None
 
@@ -87,6 +89,8 @@ def load(build_if_missing: bool = True):
     L.mmx_rollout_steps_per_launch.argtypes = [vp]
     L.mmx_rollout_steps_per_launch.restype = C.c_int
     L.mmx_forward.argtypes = [vp]
+    L.mmx_expert_physics.argtypes = [vp, C.c_int32]
+    L.mmx_eval_reward.argtypes = [vp, vp, vp, vp, vp, C.c_int32]
     L.mmx_get_buffers.argtypes = [vp, C.POINTER(MMXBuffers)]
     L.mmx_synchronize.argtypes = [vp]
     L.mmx_get_state.argtypes = [vp, fp, fp, fp, fp]
@@ -94,7 +98,8 @@ def load(build_if_missing: bool = True):
     L.mmx_episode_seed.restype = C.c_uint32
     L.mmx_episode_seed.argtypes = [C.c_uint64, C.c_int32]
     for name in ("mmx_create", "mmx_reset", "mmx_step", "mmx_expert_plan", "mmx_rollout_expert", "mmx_physics_step",
-                 "mmx_forward", "mmx_get_buffers", "mmx_synchronize", "mmx_get_state", "mmx_set_state"):
+                 "mmx_forward", "mmx_get_buffers", "mmx_synchronize", "mmx_get_state", "mmx_set_state",
+                 "mmx_expert_physics", "mmx_eval_reward"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L
@@ -223,6 +228,16 @@ class Sim:
 
     def forward(self):
         self._check(self.L.mmx_forward(self.ptr), "mmx_forward")
+
+    def expert_physics(self, n_physics_steps: int):
+        """n x (PickAndPlaceTask.update() ; mj_step), main.py:65-91."""
+        self._check(self.L.mmx_expert_physics(self.ptr, n_physics_steps), "mmx_expert_physics")
+
+    def eval_reward(self, obj_ptr: int, ee_ptr: int, ctrl7_ptr: int, pairs_ptr: int | None, max_pairs: int):
+        """Reward-layer harness (device pointers): _compute_reward at the given positions / contacts."""
+        self._check(self.L.mmx_eval_reward(self.ptr, C.c_void_p(obj_ptr), C.c_void_p(ee_ptr), C.c_void_p(ctrl7_ptr),
+                                           C.c_void_p(pairs_ptr) if pairs_ptr else None, max_pairs),
+                    "mmx_eval_reward")
 
     def synchronize(self):
         self._check(self.L.mmx_synchronize(self.ptr), "mmx_synchronize")

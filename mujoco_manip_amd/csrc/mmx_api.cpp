@@ -23,6 +23,9 @@ extern "C" hipError_t mmx_launch_expert(const MMXState* S, int n, float* action,
 extern "C" hipError_t mmx_launch_physics(const MMXState* S, int n, int with_ik, hipStream_t st);
 extern "C" hipError_t mmx_launch_forward(const MMXState* S, hipStream_t st);
 extern "C" hipError_t mmx_launch_render(const MMXState* S, int base, int count, hipStream_t st);
+extern "C" hipError_t mmx_launch_expert_physics(const MMXState* S, int n, hipStream_t st);
+extern "C" hipError_t mmx_launch_reward(const MMXState* S, const float* obj, const float* ee, const float* ctrl7,
+                                        const int* pairs, int max_pairs, hipStream_t st);
 
 struct mmx_sim {
   MMXState S;
@@ -112,6 +115,22 @@ void pcg64_seed(uint64_t seed, uint64_t out[4]) {
   out[3] = static_cast<uint64_t>(inc);
 }
 
+// Makes the sim's device current for the duration of an entry point (NULL-stream launches and
+// hipMemcpy go to the current device) and restores the caller's device afterwards.
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(const mmx_sim* sim) {
+    if (sim && hipGetDevice(&prev) == hipSuccess && prev != sim->cfg.device) {
+      if (hipSetDevice(sim->cfg.device) != hipSuccess) prev = -1;
+    } else {
+      prev = -1;
+    }
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
 int fail(mmx_sim* sim, int code, const std::string& msg) {
   if (sim) sim->err = msg;
   return code;
@@ -170,10 +189,12 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
     if (cfg->task_obj[k] < 0 || cfg->task_obj[k] > 2 || cfg->task_bin[k] < 0 || cfg->task_bin[k] > 2) return MMX_EINVAL;
   mmx_sim* sim = new mmx_sim();
   sim->cfg = *cfg;
-  if (hipSetDevice(cfg->device) != hipSuccess) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || cfg->device < 0 || cfg->device >= ndev) {
     delete sim;
     return MMX_EDEVICE;
   }
+  DeviceGuard guard(sim);  // allocations and streams on cfg->device; the caller's device restored
   sim->stream = static_cast<hipStream_t>(cfg->stream);
   const int N = cfg->num_envs;
   MMXState& S = sim->S;
@@ -269,6 +290,7 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
 
 void mmx_destroy(mmx_sim* sim) {
   if (!sim) return;
+  DeviceGuard guard(sim);
   (void)hipDeviceSynchronize();
   for (void* p : sim->allocs)
     if (p) (void)hipFree(p);
@@ -285,6 +307,7 @@ const char* mmx_last_error(const mmx_sim* sim) { return sim ? sim->err.c_str() :
 int mmx_reset(mmx_sim* sim, const uint64_t* seeds, const uint8_t* seed_given, const int32_t* task_override,
               const uint8_t* env_mask) {
   if (!sim) return MMX_EINVAL;
+  DeviceGuard guard(sim);
   MMXState& S = sim->S;
   const size_t n = static_cast<size_t>(S.N);
   if (seeds) {
@@ -333,6 +356,7 @@ int mmx_reset(mmx_sim* sim, const uint64_t* seeds, const uint8_t* seed_given, co
 
 int mmx_step(mmx_sim* sim, const float* action_dev, int32_t action_dim) {
   if (!sim || !action_dev) return MMX_EINVAL;
+  DeviceGuard guard(sim);
   static const int kDim[5] = {4, 8, 10, 8, 10};
   if (action_dim < kDim[sim->S.action_mode]) return fail(sim, MMX_EINVAL, "action_dim too small for action_mode");
   hipError_t e = mmx_launch_step(&sim->S, action_dev, action_dim, 0, 0, sim->S.N, 1, sim->stream);
@@ -342,11 +366,13 @@ int mmx_step(mmx_sim* sim, const float* action_dev, int32_t action_dim) {
 
 int mmx_expert_plan(mmx_sim* sim, int32_t n_steps, float* action_dev_out) {
   if (!sim || n_steps < 0) return MMX_EINVAL;
+  DeviceGuard guard(sim);
   return hip_check(sim, mmx_launch_expert(&sim->S, n_steps, action_dev_out, sim->stream), "mmx_expert_plan");
 }
 
 int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
   if (!sim || sim->S.action_mode != MMX_ACTION_ABS_POS) return MMX_EINVAL;
+  DeviceGuard guard(sim);
   const int N = sim->S.N, L = n_env_steps > 1 ? sim->nlanes : 1;
   hipError_t e = hipSuccess;
   if (L > 1) {  // fork: every lane starts after the work already queued on the caller's stream
@@ -383,11 +409,29 @@ int mmx_rollout_steps_per_launch(const mmx_sim* sim) {
 
 int mmx_physics_step(mmx_sim* sim, int32_t n, int32_t with_ik) {
   if (!sim || n < 0) return MMX_EINVAL;
+  DeviceGuard guard(sim);
   return hip_check(sim, mmx_launch_physics(&sim->S, n, with_ik, sim->stream), "mmx_physics_step");
+}
+
+int mmx_expert_physics(mmx_sim* sim, int32_t n) {
+  if (!sim || n < 0) return MMX_EINVAL;
+  DeviceGuard guard(sim);
+  hipError_t e = hipSuccess;
+  for (int k = 0; k < n && e == hipSuccess; k += 256)  // bounded launches (a few ms each)
+    e = mmx_launch_expert_physics(&sim->S, std::min(256, n - k), sim->stream);
+  return hip_check(sim, e, "mmx_expert_physics");
+}
+
+int mmx_eval_reward(mmx_sim* sim, const float* obj, const float* ee, const float* ctrl7, const int32_t* pairs,
+                    int32_t max_pairs) {
+  if (!sim || !obj || !ee || !ctrl7 || max_pairs < 0 || (max_pairs > 0 && !pairs)) return MMX_EINVAL;
+  DeviceGuard guard(sim);
+  return hip_check(sim, mmx_launch_reward(&sim->S, obj, ee, ctrl7, pairs, max_pairs, sim->stream), "mmx_eval_reward");
 }
 
 int mmx_forward(mmx_sim* sim) {
   if (!sim) return MMX_EINVAL;
+  DeviceGuard guard(sim);
   hipError_t e = mmx_launch_forward(&sim->S, sim->stream);
   if (e == hipSuccess) e = mmx_launch_render(&sim->S, 0, sim->S.N, sim->stream);
   return hip_check(sim, e, "mmx_forward");
@@ -412,16 +456,19 @@ int mmx_get_buffers(mmx_sim* sim, mmx_buffers* b) {
   b->contacts = S.con;
   b->images = S.images;
   b->seg = S.seg;
+  b->target = S.target;
   return MMX_OK;
 }
 
 int mmx_synchronize(mmx_sim* sim) {
   if (!sim) return MMX_EINVAL;
+  DeviceGuard guard(sim);
   return hip_check(sim, hipStreamSynchronize(sim->stream), "mmx_synchronize");
 }
 
 int mmx_get_state(mmx_sim* sim, float* qpos, float* qvel, float* ctrl, float* ws) {
   if (!sim) return MMX_EINVAL;
+  DeviceGuard guard(sim);
   const size_t n = static_cast<size_t>(sim->S.N);
   hipError_t e = hipStreamSynchronize(sim->stream);
   if (e == hipSuccess && qpos) e = hipMemcpy(qpos, sim->S.qpos, MMX_NQ_ * n * 4, hipMemcpyDeviceToHost);
@@ -433,6 +480,7 @@ int mmx_get_state(mmx_sim* sim, float* qpos, float* qvel, float* ctrl, float* ws
 
 int mmx_set_state(mmx_sim* sim, const float* qpos, const float* qvel, const float* ctrl, const float* ws) {
   if (!sim) return MMX_EINVAL;
+  DeviceGuard guard(sim);
   const size_t n = static_cast<size_t>(sim->S.N);
   hipError_t e = hipStreamSynchronize(sim->stream);
   if (e == hipSuccess && qpos) e = hipMemcpy(sim->S.qpos, qpos, MMX_NQ_ * n * 4, hipMemcpyHostToDevice);

@@ -152,16 +152,17 @@ DEV float* contacts_dst(const MMXState& S, int i) { return S.con + (size_t)i * M
 enum { SHF_ROBOT_OBST = 1, SHF_CON_OVF = 2, SHF_EFC_OVF = 4, SHF_NAN = 8 };
 
 DEV int body_slot(int b) { return b <= 11 ? b - 1 : b - 5; }
-// The IK's kinematics cache (KIN_*: hand pose, arm joint axes and anchors of the last position
-// stage, the HBM record's kin[]) is not a separate LDS array: its entries ARE the position
-// stage's outputs (hand slot of bx / bR, angular part of S, joint bodies' bx), which stay
+// The IK's kinematics cache (KIN_*: hand pose, arm joint axes and anchors, cube positions of the
+// last position stage, the HBM record's kin[]) is not a separate LDS array: its entries ARE the
+// position stage's outputs (hand slot of bx / bR, angular part of S, joint and cube bodies' bx), which stay
 // untouched from one position stage to the next IK.  load_env scatters the record into them,
 // store_env gathers it back.
 DEV float& kin_ref(EnvSh& E, int k) {
   if (k < KIN_HAND_MAT) return E.bx[body_slot(MMX_BODY_HAND)][k - KIN_HAND_POS];
   if (k < KIN_AXIS) return E.bR[body_slot(MMX_BODY_HAND)][k - KIN_HAND_MAT];
   if (k < KIN_ANCHOR) return E.S[(k - KIN_AXIS) / 3][(k - KIN_AXIS) % 3];
-  return E.bx[body_slot(MMX_jnt_body[(k - KIN_ANCHOR) / 3])][(k - KIN_ANCHOR) % 3];
+  if (k < KIN_OBJ) return E.bx[body_slot(MMX_jnt_body[(k - KIN_ANCHOR) / 3])][(k - KIN_ANCHOR) % 3];
+  return E.bx[11 + (k - KIN_OBJ) / 3][(k - KIN_OBJ) % 3];
 }
 DEV float kin_get(const EnvSh& E, int k) { return kin_ref(const_cast<EnvSh&>(E), k); }
 DEV int body_block(int b) { return (b >= 2 && b <= 11) ? 0 : (b >= 16 ? b - 15 : -1); }
@@ -895,9 +896,9 @@ DEV void store_row(EnvSh& E, int row, const float* jv, int hdr, float vel, float
 
 // per-contact row generator, written by the contact's lane into fields of its own contact record
 // that the rows no longer need (distance, torsional friction, geom ids) and read by its rows'
-// lanes: impedance ratio x translational / rotational invweight, K imp pos, B.  The contacts are
+// lanes: impedance ratio x translational invweight, K imp pos, B.  The contacts are
 // copied to HBM (last substep) before this overwrite.
-enum { CG_IT = CON_DIST, CG_IR = CON_MU2, CG_KID = CON_G1, CG_B = CON_G2 };
+enum { CG_IT = CON_DIST, CG_KID = CON_G1, CG_B = CON_G2 };
 DEV V3 contact_t1(V3 n) {  // mju_makeFrame's first tangent
   const V3 y = (n.y < 0.5f && n.y > -0.5f) ? V3{0.f, 1.f, 0.f} : V3{0.f, 0.f, 1.f};
   return normalize(y - n * dot(n, y));
@@ -921,7 +922,10 @@ DEV void contact_row(EnvSh& E, int row, int c, int rr) {
     if (k == 0) u = n + t1 * sg;
     else if (k == 1) u = n + cross(n, t1) * sg;
     else w = n * sg;
-    idiag = cc[CG_IT] + mu * mu * (k < 2 ? cc[CG_IT] : cc[CG_IR]);
+    // pyramidal cone: one R for every edge, the first edge's diagApprox (tran + mu0^2 tran) x
+    // 2 mu0^2 / impratio (impratio = 1; MuJoCo mj_makeImpedance, as in oracle/or_physics.c)
+    const float mu0 = cc[CON_MU0];
+    idiag = 2.f * mu0 * mu0 * (cc[CG_IT] + mu0 * mu0 * cc[CG_IT]);
   }
   const int k1 = body_block(b1), k2 = body_block(b2);
   int rb0 = k1 >= 0 ? k1 : k2, rb1 = (k1 >= 0 && k2 >= 0 && k2 != k1) ? k2 : BLK_NONE;
@@ -1069,9 +1073,7 @@ DEV void make_constraints_wave(EnvSh& E) {
     float impr, kid, B;
     row_ref(solref, solimp, c[CON_DIST], impr, kid, B);
     const float tran = MMX_body_invweight0[2 * b1] + MMX_body_invweight0[2 * b2];
-    const float rot = MMX_body_invweight0[2 * b1 + 1] + MMX_body_invweight0[2 * b2 + 1];
-    c[CG_IT] = impr * tran;
-    c[CG_IR] = impr * rot;
+    c[CG_IT] = impr * tran;  // (the pyramid's common R needs only the translational invweight)
     c[CG_KID] = kid;
     c[CG_B] = B;
     for (int rr = 0; rr < ncr && brow + rr < MMX_MAXEFC; rr++) rowmap_set(brow + rr, LANE | (rr << 8));
@@ -1579,8 +1581,9 @@ DEV void integrate_wave(EnvSh& E) {
     E.ws[LANE] = E.x[LANE];  // warm start keeps the constraint solver's qacc
     const float v = E.qvel[LANE] + kDt * qa;
     E.qvel[LANE] = v;
-    bad = (__float_as_uint(v) & 0x7fffffffu) >= 0x501502F9u;  // |v| >= 1e10, Inf or NaN (a bit test,
-                                                            // exact under any fp-math flags)
+    // |v| or |qacc| >= 1e10, Inf or NaN (MuJoCo's mj_checkVel / mj_checkAcc bound mjMAXVAL; a bit
+    // test, exact under any fp-math flags)
+    bad = (__float_as_uint(v) & 0x7fffffffu) >= 0x501502F9u || (__float_as_uint(qa) & 0x7fffffffu) >= 0x501502F9u;
     if (LANE < 9) E.qpos[LANE] += kDt * v;
   }
   if (__ballot(bad) != 0ull && LANE == 0) E.flags |= SHF_NAN;
@@ -2044,8 +2047,15 @@ DEV void reset_lane0(const MMXState& S, int i, EnvSh& E, int task_override) {
   EPI(EPI_FSM_SETTLE) = 0;
   EPI(EPI_FSM_GRIP) = 1;
   EPI(EPI_FSM_HASTGT) = 0;
+  EPI(EPI_PHASES) = 1;  // IDLE
   EPI(EPI_EPISODES) += 1;
   obs_lane0(S, i, E);
+}
+
+// the target cube inside the target bin (the success test of gym_env.py:436-447)
+DEV bool in_target_bin(const MMXState& S, int i, const EnvSh& E) {
+  const V3 o = obj_pos(E, EPI(EPI_OBJ)), b = bin_pos(EPI(EPI_BIN));
+  return sqrtf((o.x - b.x) * (o.x - b.x) + (o.y - b.y) * (o.y - b.y)) < 0.05f && o.z < b.z + 0.06f;
 }
 
 // reward (gym_env.py:352-470); returns reward, sets success (staged: all HWM >= 0.9)
@@ -2143,6 +2153,7 @@ DEV void expert_plan(const MMXState& S, int i, V3 o, V3 ee, int n, float* act4) 
   const int ng = go1 || go8 ? 1 : (go3 ? 0 : grip);
   const int nhas = go1 ? 1 : has;
   EPI(EPI_FSM_STATE) = ns; EPI(EPI_FSM_TASKIDX) = go0 ? ti + 1 : ti; EPI(EPI_FSM_SETTLE) = nset;
+  EPI(EPI_PHASES) |= 1 << ns;
   EPI(EPI_FSM_GRIP) = ng; EPI(EPI_FSM_HASTGT) = nhas;
   EPF(EPF_FSM_TARGET) = tx; EPF(EPF_FSM_TARGET + 1) = ty; EPF(EPF_FSM_TARGET + 2) = tz;
   if (go5) {
@@ -2230,8 +2241,33 @@ DEV void fold_flags(const MMXState& S, int i, const EnvSh& E) {  // lane 0
   if (E.flags & SHF_NAN) EPI(EPI_ERROR) |= ERR_NAN;
 }
 
+// reward, termination and info of the current state (gym_env.py:562-573): writes the reward and
+// the reward components, adds the reward to the episode return; lane 0
+DEV void reward_outputs(const MMXState& S, int i, EnvSh& E, bool robot_obstacle, int& terminated, int& succ_flag) {
+  int success = 0;
+  const float r = reward_lane0(S, i, E, robot_obstacle, success);
+  float* rc = S.reward_components + (size_t)i * 6;
+  if (S.reward_type == 2) {
+    terminated = (r < 0.f) || success;
+    succ_flag = success && r >= 0.f;
+    float sum = 0.f;
+    for (int k = 0; k < 5; k++) {
+      const float h = EPF(EPF_HWM + k) / 5.f;
+      rc[1 + k] = h;
+      sum += h;
+    }
+    rc[0] = sum;
+  } else {
+    terminated = success;
+    succ_flag = success;
+    for (int k = 0; k < 6; k++) rc[k] = 0.f;
+  }
+  S.reward[i] = r;
+  EPF(EPF_EP_RETURN) += r;
+}
+
 // end of PickPlaceGymEnv.step: position stage, staged-penalty contact scan, reward, obs, autoreset
-DEV void step_end(const MMXState& S, int i, EnvSh& E, bool expert) {
+DEV void step_end(const MMXState& S, int i, EnvSh& E) {
   float* stats = E.stats;
   CLK_DECL;
   // mj_forward position stage (gym_env.py:560): kinematics + contacts for the staged penalty
@@ -2243,36 +2279,28 @@ DEV void step_end(const MMXState& S, int i, EnvSh& E, bool expert) {
   if (S.reward_type == 2) collide_wave(E, true);
   if (LANE == 0) {
     EPI(EPI_STEP) += 1;
-    int success = 0;
-    const float r = reward_lane0(S, i, E, (E.flags & SHF_ROBOT_OBST) != 0, success);
     int terminated, succ_flag;
-    float* rc = S.reward_components + (size_t)i * 6;
-    if (S.reward_type == 2) {
-      terminated = (r < 0.f) || success;
-      succ_flag = success && r >= 0.f;
-      float sum = 0.f;
-      for (int k = 0; k < 5; k++) {
-        const float h = EPF(EPF_HWM + k) / 5.f;
-        rc[1 + k] = h;
-        sum += h;
-      }
-      rc[0] = sum;
-    } else {
-      terminated = success;
-      succ_flag = success;
-      for (int k = 0; k < 6; k++) rc[k] = 0.f;
-    }
+    reward_outputs(S, i, E, (E.flags & SHF_ROBOT_OBST) != 0, terminated, succ_flag);
     const int truncated = EPI(EPI_STEP) >= S.max_episode_steps;
-    S.reward[i] = r;
     S.done[3 * (size_t)i] = terminated;
     S.done[3 * (size_t)i + 1] = truncated;
     S.done[3 * (size_t)i + 2] = succ_flag;
-    EPF(EPF_EP_RETURN) += r;
     fold_flags(S, i, E);
     obs_lane0(S, i, E);
+    // the FSM state only moves when the expert plans (mmx_expert_plan, or inside the rollout's
+    // step launch), so host-action steps never see DONE: expert_plan + step autoresets exactly like
+    // the fused rollout
     const bool fsm_done = EPI(EPI_FSM_STATE) == 10;
     const bool err = (EPI(EPI_ERROR) & ERR_NAN) != 0;
-    if (S.autoreset && (terminated || truncated || err || (expert && fsm_done))) {
+    if (S.autoreset && (terminated || truncated || err || fsm_done)) {
+      if (err) {  // a diverged env ends its episode as truncated, not as a silent reset
+        S.done[3 * (size_t)i + 1] = 1;
+        S.done[3 * (size_t)i + 2] = 0;
+        EPI(EPI_NERROR) += 1;
+      } else {
+        EPI(EPI_NSUCCESS) += succ_flag;
+        EPI(EPI_NPLACED) += in_target_bin(S, i, E) ? 1 : 0;
+      }
       EPI(EPI_ERROR) = 0;
       reset_lane0(S, i, E, -1);
     }
@@ -2303,7 +2331,7 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_substep_kernel(MMXState S, 
   }
   mj_step_wave(S.solver_max_iter, S.solver_tol, E, (mode & SS_LAST) ? contacts_dst(S, i) : nullptr);
   if ((mode & SS_LAST) && (mode & SS_GYM)) {
-    step_end(S, i, E, (mode & SS_EXPERT) != 0);
+    step_end(S, i, E);
   } else {
     if (LANE == 0) {
       fold_flags(S, i, E);
@@ -2418,9 +2446,9 @@ __device__ __attribute__((noinline)) void step_begin(const MMXState& S, int i, c
   }
   SYNC();
 }
-__device__ __attribute__((noinline)) void step_finish(const MMXState& S, int i, int expert) {
+__device__ __attribute__((noinline)) void step_finish(const MMXState& S, int i) {
   EnvSh& E = g_E;
-  step_end(S, i, E, expert != 0);
+  step_end(S, i, E);
   store_env(S, i, E);
 }
 extern "C" __global__ void __launch_bounds__(STEP_WG) __attribute__((amdgpu_waves_per_eu(2, 2)))
@@ -2437,7 +2465,7 @@ mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert, int b
     XSYNC();
     for (int sub = 0; sub < MMX_NSUBSTEP; sub++)
       substep(S.solver_max_iter, S.solver_tol, sub == MMX_NSUBSTEP - 1 ? contacts_dst(S, i) : nullptr);
-    if (w0) step_finish(S, i, expert);
+    if (w0) step_finish(S, i);
   }
 }
 
@@ -2470,6 +2498,68 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_reset_kernel(MMXState S, co
   }
   store_env(S, i, E);
   store_obs(S, i, E);
+}
+
+// Per-physics-step expert loop (main.py:65-91, tests/test_pick_and_place.py:147-166): n x
+// (PickAndPlaceTask.update() = plan(1) + _actuate() (pick_and_place.py:279-304) ; mj_step).  plan
+// reads data.xpos as the previous mj_step left it: the hand pose and cube positions of
+// the last position stage (the kin cache), not the integrated qpos.  No gym bookkeeping.
+extern "C" __global__ void __launch_bounds__(WG) __attribute__((amdgpu_waves_per_eu(2, 2)))
+mmx_expert_physics_kernel(MMXState S, int n) {
+  EnvSh& E = g_E;
+  const int i = blockIdx.x;
+  if (i >= S.N) return;
+  load_env(S, i, E);
+  for (int k = 0; k < n; k++) {
+    if (LANE == 0) {
+      float act[4];
+      const int ob = EPI(EPI_OBJ);
+      expert_plan(S, i, V3{E.bx[11 + ob][0], E.bx[11 + ob][1], E.bx[11 + ob][2]}, hand_pos(E), 1, act);
+      // _actuate: gripper open / closed, then IK toward the target once there is one
+      E.ctrl[7] = EPI(EPI_FSM_GRIP) ? 255.f : 0.f;
+      E.target[0] = EPF(EPF_FSM_TARGET);
+      E.target[1] = EPF(EPF_FSM_TARGET + 1);
+      E.target[2] = EPF(EPF_FSM_TARGET + 2);
+      E.target[3] = EPI(EPI_FSM_HASTGT) ? act[3] : -1.f;  // < 0: no target yet, no IK
+    }
+    SYNC();
+    if (E.target[3] >= 0.f) ik_wave(E);
+    SYNC();
+    mj_step_wave(S.solver_max_iter, S.solver_tol, E, k == n - 1 ? contacts_dst(S, i) : nullptr);
+  }
+  if (LANE == 0) fold_flags(S, i, E);
+  store_env(S, i, E);
+}
+
+// Reward-layer parity harness (gym_env.py:341-470, 562-573): the reward of every env at the given
+// object / EE positions and gripper command, with the step's contacts given as geom-id pairs (-1
+// ends a list; robot x obstacle pairs are classified by the same geom classes as the collision
+// scan).  Updates the sticky flags / high-water marks like a step; writes reward, reward
+// components, terminated and success.
+extern "C" __global__ void __launch_bounds__(WG) mmx_reward_kernel(MMXState S, const float* obj, const float* ee,
+                                                                  const float* ctrl7, const int* pairs, int max_pairs) {
+  EnvSh& E = g_E;
+  const int i = blockIdx.x;
+  if (i >= S.N || LANE != 0) return;
+  const int ob = EPI(EPI_OBJ);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    E.qpos[9 + 7 * ob + k] = obj[3 * (size_t)i + k];
+    kin_ref(E, KIN_HAND_POS + k) = ee[3 * (size_t)i + k];
+  }
+  E.ctrl[7] = ctrl7[i];
+  bool ro = false;
+  for (int p = 0; p < max_pairs; p++) {
+    const int g1 = pairs[2 * ((size_t)i * max_pairs + p)], g2 = pairs[2 * ((size_t)i * max_pairs + p) + 1];
+    if (g1 < 0 || g2 < 0 || g1 >= MMX_NGEOM || g2 >= MMX_NGEOM) break;
+    const int c1 = MMX_geom_class[g1], c2 = MMX_geom_class[g2];
+    ro |= (c1 == 1 && c2 == 2) || (c1 == 2 && c2 == 1);
+  }
+  int terminated, succ_flag;
+  reward_outputs(S, i, E, ro, terminated, succ_flag);
+  S.done[3 * (size_t)i] = terminated;
+  S.done[3 * (size_t)i + 1] = 0;
+  S.done[3 * (size_t)i + 2] = succ_flag;
 }
 
 // FSM expert plan(n) for every env -> abs_pos action [N][4] (one lane per env: tiny)
@@ -2507,6 +2597,15 @@ extern "C" hipError_t mmx_launch_physics(const MMXState* S, int n, int with_ik, 
     const int mode = (with_ik ? SS_IK : 0) | (sub == n - 1 ? SS_LAST : 0);
     hipLaunchKernelGGL(mmx_substep_kernel, dim3(S->N), dim3(WG), 0, st, *S, nullptr, 0, mode);
   }
+  return hipGetLastError();
+}
+extern "C" hipError_t mmx_launch_expert_physics(const MMXState* S, int n, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(mmx_expert_physics_kernel, dim3(S->N), dim3(WG), 0, st, *S, n);
+  return hipGetLastError();
+}
+extern "C" hipError_t mmx_launch_reward(const MMXState* S, const float* obj, const float* ee, const float* ctrl7,
+                                        const int* pairs, int max_pairs, hipStream_t st) {
+  hipLaunchKernelGGL(mmx_reward_kernel, dim3(S->N), dim3(WG), 0, st, *S, obj, ee, ctrl7, pairs, max_pairs);
   return hipGetLastError();
 }
 extern "C" hipError_t mmx_launch_forward(const MMXState* S, hipStream_t st) {

@@ -31,13 +31,21 @@ enum {
   KIN_HAND_MAT = 3,    // 9 (row-major)
   KIN_AXIS = 12,       // 7 x 3 arm joint axes (world)
   KIN_ANCHOR = 33,     // 7 x 3 arm joint anchors (world)
-  KIN_N = 54
+  KIN_OBJ = 54,        // 3 x 3 cube positions (data.xpos of obj_red/green/blue: the per-physics-step
+                       // FSM reads them stale, pick_and_place.py:167-277 via env.get_body_pos)
+  KIN_N = 63
 };
 
 // per-env integer episode / FSM state
 enum {
   EPI_OBJ = 0, EPI_BIN, EPI_STEP, EPI_FLAGS, EPI_FSM_STATE, EPI_FSM_TASKIDX, EPI_FSM_SETTLE,
   EPI_FSM_GRIP, EPI_FSM_HASTGT, EPI_ERROR, EPI_NCON, EPI_NEFC, EPI_EPISODES, EPI_RNG_HAS32,
+  // sticky counters (never cleared by a reset): episodes that ended with info["success"], episodes
+  // that ended with the target cube in the target bin (the success test of gym_env.py:436-447:
+  // xy < 0.05 and z < bin z + 0.06), and autoresets forced by a diverged state (ERR_NAN: NaN / Inf
+  // / |qvel| or |qacc| >= 1e10, MuJoCo's mj_checkVel / mj_checkAcc); then the bitmask of the FSM
+  // states visited since the last reset
+  EPI_NSUCCESS, EPI_NPLACED, EPI_NERROR, EPI_PHASES,
   EPI_N
 };
 // per-env float episode / FSM state

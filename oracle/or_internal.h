@@ -13,6 +13,7 @@
 #define NU OM_NU
 #define NC OM_NCAM
 #define MINVAL 1e-15
+#define OR_IMPRATIO 1.0 /* MuJoCo default <option impratio>; the model does not set it */
 
 enum { EFC_EQUALITY = 0, EFC_LIMIT = 1, EFC_CONTACT = 2 };
 

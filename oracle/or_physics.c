@@ -396,10 +396,19 @@ static void make_constraints(or_env* e) {
       add_row(e, EFC_CONTACT, Jt[0], con->dist, tran, con->solref, con->solimp);
       continue;
     }
+    /* Pyramidal regulariser: every edge of the contact gets ONE common R, taken from the first
+     * edge's diagApprox (tran + mu0^2 tran) scaled by 2 mu0^2 / impratio (MuJoCo 3.x
+     * mj_makeImpedance's pyramidal-cone branch; the same expression is MJX's
+     * constraint.py `invweight * 2 * fri[0]**2 / m.opt.impratio`).  impratio = 1: neither
+     * pick_and_place_scene.xml nor panda.xml sets <option impratio>.  Neither the MuJoCo source nor
+     * its docs are in this image, so this is restated from the published implementation as
+     * remembered, not checked against it. */
+    (void)rot;
+    const double mu0 = con->friction[0];
+    const double diag = 2.0 * mu0 * mu0 / OR_IMPRATIO * (tran + mu0 * mu0 * tran);
     for (int k = 0; k < con->dim - 1; k++) {
       const double* Jk = k < 2 ? Jt[k + 1] : Jr[0];
       double mu = con->friction[k];
-      double diag = tran + mu * mu * (k < 2 ? tran : rot);
       for (int s = 0; s < 2; s++) {
         double sg = s == 0 ? 1 : -1;
         for (int d = 0; d < NV; d++) J[d] = Jt[0][d] + sg * mu * Jk[d];

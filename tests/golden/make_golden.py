@@ -352,9 +352,88 @@ def main():
     G["episode_seeds"] = {"root": 42, "seeds": [int(c.generate_state(1)[0]) for c in ss.spawn(16)]}
     G["pcg64_raw"] = {str(s): [int(x) for x in np.random.PCG64(np.random.SeedSequence(s)).random_raw(8)]
                       for s in (0, 42, 4091952314)}
+
+    # (viii) observation assembly + keypoints (gym_env.py:283-339 _get_obs, reset's target keypoints
+    # gym_env.py:519-531, cameras.py:56-130 project_3d_to_2d / compute_keypoints).  States: C3
+    # episodes (randomized reset from the episode seed, then FSM-expert steps) on the fp64 oracle,
+    # whose position stage supplies xpos / xmat / camera poses to the reference code through the stub
+    # MjData: the fixture pins the reference's observation math given the kinematics.
+    G["obs"] = obs_goldens(gymenv, importlib.import_module("mujoco_manip.cameras"), robot_mod)
     with open(os.path.join(HERE, "golden.json"), "w") as f:
         json.dump(G, f)
     print("wrote", os.path.join(HERE, "golden.json"), {k: (len(v) if isinstance(v, list) else 1) for k, v in G.items()})
+
+
+def _qmat(q):
+    w, x, y, z = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+def obs_goldens(gymenv, cams_mod, robot_mod, n_episodes=6, states_per_episode=5):
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    sys.path.insert(0, REPO)
+    import oracle_py as O
+
+    from mujoco_manip_amd.constants import ALL_TASKS, BINS, OBJECTS
+
+    pool = [(OBJECTS.index(o), BINS.index(b)) for o, b in ALL_TASKS]
+    hand = BODY_NAMES.index("hand")
+    cam_names = [c["name"] for c in MODEL["cameras"]]
+
+    def fill(env, data, oe):
+        for b in range(len(BODY_NAMES)):
+            p, R = oe.body(b)
+            data.xpos[b] = p
+            data.xmat[b] = R.ravel()
+        q, _, ctrl, _ = oe.get_state()
+        data.qpos[:] = q
+        data.ctrl[:] = ctrl
+        for k, c in enumerate(MODEL["cameras"]):  # camera pose = body pose x camera offset
+            Rb = data.xmat[c["body"]].reshape(3, 3) if c["body"] else np.eye(3)
+            pb = data.xpos[c["body"]] if c["body"] else np.zeros(3)
+            data.cam_xpos[k] = pb + Rb @ np.array(c["pos"])
+            data.cam_xmat[k] = (Rb @ _qmat(c["quat"])).ravel()
+
+    out = []
+    for ep in range(n_episodes):
+        seed = int(np.random.SeedSequence(42).spawn(n_episodes)[ep].generate_state(1)[0])
+        oe = O.OracleEnv(action_mode="abs_pos", reward_type="staged", randomize_objects=True, tasks=pool)
+        oe.reset(seed=seed)
+        oi, bi = oe.task()
+        env = object.__new__(gymenv.PickPlaceGymEnv)
+        data = FakeData()
+        env._env = types.SimpleNamespace(model=FakeModel(), data=data)
+        env._robot = robot_mod.PandaRobot(env._env.model, data)
+        env._renderer = types.SimpleNamespace(render=lambda d, cam: None)
+        env._image_size = 224
+        env._obj_name, env._bin_name = OBJECTS[oi], BINS[bi]
+        fill(env, data, oe)
+        env._initial_ee_se3 = np.eye(4)
+        env._initial_ee_se3[:3, :3] = data.xmat[hand].reshape(3, 3)
+        env._initial_ee_se3[:3, 3] = data.xpos[hand]
+        env._target_obj_kp_overhead = cams_mod.project_3d_to_2d(
+            env._env.model, data, "overhead", data.xpos[BODY_NAMES.index(env._obj_name)][None], 224).flatten()
+        env._target_bin_kp_overhead = cams_mod.project_3d_to_2d(
+            env._env.model, data, "overhead", data.xpos[BODY_NAMES.index(env._bin_name)][None], 224).flatten()
+        oe.fsm_init([(oi, bi)])
+        states = []
+        for t in range(400):
+            if t % 17 == 0 and len(states) < states_per_episode:
+                fill(env, data, oe)
+                o = env._get_obs()
+                q, _, ctrl, _ = oe.get_state()
+                states.append({"t": t, "qpos": q.tolist(), "ctrl": ctrl.tolist(),
+                               "obs": {k: np.asarray(v, np.float64).ravel().tolist() for k, v in o.items()
+                                       if not k.startswith("image_")}})
+            if oe.fsm_plan(16) == 10:
+                break
+            f = oe.fsm_get()
+            oe.step(np.array([*f["target"], float(f["gripper_open"])], np.float32))
+        assert cam_names.index("overhead") == 0
+        out.append({"seed": seed, "task": [OBJECTS[oi], BINS[bi]], "states": states})
+    return out
 
 
 if __name__ == "__main__":

@@ -54,8 +54,13 @@ def test_state_layout_constants_match_header():
     from mujoco_manip_amd import _lib
 
     assert f"#define MMX_MAXCON {_lib.MAXCON}" in src
-    assert "KIN_N = 54" in src and _lib.KIN_N == 54
-    assert len(_lib.EPI_FIELDS) == _lib.EPI_N
+    assert f"KIN_N = {_lib.KIN_N}" in src
+    # the episode_i enum: names up to EPI_N, in order (comments stripped)
+    body = re.search(r"enum \{\s*(EPI_OBJ.*?)EPI_N\s*\}", src, re.S).group(1)
+    body = re.sub(r"//[^\n]*", "", body)
+    names = [t.strip() for t in body.replace("\n", " ").split(",") if t.strip()]
+    assert len(names) == _lib.EPI_N == len(_lib.EPI_FIELDS)
+    assert [n.split("=")[0].strip() for n in names][-4:] == ["EPI_NSUCCESS", "EPI_NPLACED", "EPI_NERROR", "EPI_PHASES"]
 
 
 def test_obs_layout_covers_reference_keys():

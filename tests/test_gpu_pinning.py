@@ -1,0 +1,459 @@
+"""GPU tests that pin the benched path and drive the reference's golden vectors through the device.
+
+Every value under test comes out of the HIP kernels through the C-ABI (libmmx.so); the fp64
+oracle (oracle/) and the reference-generated fixtures (tests/golden/golden.json) are the checkers.
+
+  * the path bench.py times (mmx_rollout_expert: FSM plan fused into the step launch, many env
+    steps per launch, concurrent env ranges) is bit-identical to expert_plan(16) -> step, one call
+    per env step, including autoresets;
+  * whole C3 episodes: success / placement equal, length within +-2 env steps,
+    final cube position within 1 cm of the oracle's run_episode;
+  * autoreset continues each env's PCG64 stream (gym_env.py:491, 515-517);
+  * reward sequences (dense / sparse / staged, high-water marks, collision branch), IK edge
+    states, SE(3) encodings and the whole 85-float observation against the reference's outputs;
+  * physics with the IK in the loop from oracle states; the per-physics-step FSM loop (main.py).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("needs an MI355X")
+    from mujoco_manip_amd import _lib
+
+    _lib.load(build_if_missing=False)
+
+
+def _c3_env(n, **kw):
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    args = dict(tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True, image_size=0)
+    args.update(kw)
+    return PickPlaceVecEnv(n, **args)
+
+
+def _record(env):
+    from mujoco_manip_amd import _lib
+
+    s = env.sim
+    q, v, c, w = s.get_state()
+    parts = [q, v, c, w, s.view("episode_i", _lib.EPI_N, "<i4").cpu().numpy().view(np.float32),
+             s.view("episode_f", _lib.EPF_N).cpu().numpy(), s.view("kin", _lib.KIN_N).cpu().numpy(),
+             s.view("obs", _lib.NOBS).cpu().numpy(), s.view("reward", 1).cpu().numpy()[:, None],
+             s.view("done", 3, "<i4").cpu().numpy().view(np.float32), env.stats[:, :4].cpu().numpy()]
+    return np.concatenate(parts, 1)
+
+
+# --------------------------------------------------------------------------- the benched path
+def test_rollout_expert_equals_plan_then_step(monkeypatch):
+    """mmx_rollout_expert(n) == n x (mmx_expert_plan(16) -> mmx_step) bit for bit on C3 seeds, with
+    truncation and FSM-done autoresets inside the window (max_episode_steps = 40)."""
+    from mujoco_manip_amd import _lib
+
+    N, K = 24, 120
+    seeds = [_lib.episode_seed(42, i) for i in range(N)]
+    outs = []
+    for mode in ("rollout", "split"):
+        monkeypatch.setenv("MMX_STREAMS", "3")
+        monkeypatch.setenv("MMX_FUSE", "16")
+        env = _c3_env(N, autoreset=True, max_episode_steps=40)
+        env.reset(seed=seeds)
+        if mode == "rollout":
+            env.rollout_expert(K)
+        else:
+            for _ in range(K):
+                env.step(env.expert_plan(16))
+        torch.cuda.synchronize()
+        outs.append(_record(env))
+        epi = env._epi.cpu().numpy()
+        env.close()
+    np.testing.assert_array_equal(outs[0], outs[1])
+    assert (epi[:, 12] >= 3).all(), epi[:, 12]  # every env went through >= 2 autoresets
+
+
+def _oracle_run_episode(seed, pool):
+    """scripts/generate_dataset.py:140-196 on the oracle (C3: task from the env's own RNG)."""
+    import oracle_py as O
+
+    e = O.OracleEnv(action_mode="abs_pos", reward_type="staged", randomize_objects=True, tasks=pool)
+    e.reset(seed=seed)
+    o, b = e.task()
+    e.fsm_init([(o, b)])
+    n, succ = 0, False
+    for _ in range(500):
+        if e.fsm_plan(16) == 10:
+            break
+        f = e.fsm_get()
+        _, _, _, _, info = e.step(np.array([*f["target"], float(f["gripper_open"])], np.float32))
+        succ |= info["success"]
+        n += 1
+    q = e.get_state()[0]
+    obj = q[9 + 7 * o: 12 + 7 * o]
+    bp = e.body(13 + b)[0]
+    placed = np.hypot(*(obj[:2] - bp[:2])) < 0.05 and obj[2] < bp[2] + 0.06
+    return (o, b), n, succ, obj, placed
+
+
+def test_c3_episodes_match_oracle():
+    """SURVEY §8d L2 over 48 C3 episodes (episode seeds SeedSequence(42), all 9 tasks): success
+    flag and placement equal, episode length within +-2 env steps, final cube within 1 cm."""
+    from mujoco_manip_amd import _lib
+    from mujoco_manip_amd.constants import BINS, OBJECTS, TASK_SETS
+
+    pool = [(OBJECTS.index(o), BINS.index(b)) for o, b in TASK_SETS["all"]]
+    N = 48
+    seeds = [_lib.episode_seed(42, i) for i in range(N)]
+    env = _c3_env(N)
+    env.reset(seed=seeds)
+    tasks = env._epi[:, :2].cpu().numpy()
+    length = np.full(N, -1)
+    final = np.zeros((N, 3), np.float32)
+    succ = np.zeros(N, bool)
+    for t in range(500):
+        act = env.expert_plan(16)
+        fsm = env.fsm_state.cpu().numpy()
+        new = (length < 0) & (fsm == 10)
+        if new.any():
+            q = env.qpos.cpu().numpy()
+            for k in np.where(new)[0]:
+                final[k] = q[k, 9 + 7 * tasks[k, 0]: 12 + 7 * tasks[k, 0]]
+            length[new] = t
+        if (length >= 0).all():
+            break
+        _, _, _, _, info = env.step(act)
+        succ |= info["success"].cpu().numpy() & (length < 0)
+    assert (length >= 0).all(), np.where(length < 0)
+    assert (env.env_error.cpu().numpy() == 0).all()
+    assert len({tuple(t) for t in tasks}) == 9, "the 48 C3 seeds must cover all 9 tasks"
+    bad = []
+    for k in range(N):
+        task, n, rs, robj, rplaced = _oracle_run_episode(seeds[k], pool)
+        assert tuple(tasks[k]) == task
+        b = tasks[k, 1]
+        bp = np.array([(-0.3, 0.55, 0.24), (0.0, 0.65, 0.24), (0.3, 0.55, 0.24)][b])
+        placed = np.hypot(*(final[k, :2] - bp[:2])) < 0.05 and final[k, 2] < bp[2] + 0.06
+        d = float(np.linalg.norm(final[k] - robj))
+        if abs(int(length[k]) - n) > 2 or d > 0.01 or bool(succ[k]) != rs or placed != rplaced:
+            bad.append((k, task, int(length[k]), n, round(d, 4), bool(succ[k]), rs, placed, rplaced))
+    print(f"lengths {length.tolist()}")
+    assert not bad, bad
+
+
+def test_autoreset_continues_rng_stream():
+    """Autoreset without reseeding (C3): episodes 2 and 3 of each env spawn the cubes and draw the
+    task from the continued PCG64 stream (gym_env.py:491, 515-517; randomization.py:70-87)."""
+    import oracle_py as O
+    from mujoco_manip_amd import _lib
+    from mujoco_manip_amd.constants import BINS, OBJECTS, TASK_SETS
+
+    pool = [(OBJECTS.index(o), BINS.index(b)) for o, b in TASK_SETS["all"]]
+    N = 16
+    seeds = [_lib.episode_seed(42, i) for i in range(N)]
+    env = _c3_env(N, autoreset=True, max_episode_steps=2)
+    env.reset(seed=seeds)
+    refs = [O.OracleEnv(action_mode="abs_pos", reward_type="staged", randomize_objects=True, tasks=pool)
+            for _ in range(N)]
+    for r, s in zip(refs, seeds):
+        r.reset(seed=s)
+    a = torch.tensor([[0.0, 0.45, 0.45, 1.0]] * N, device="cuda")
+    for episode in (2, 3):
+        for t in range(2):
+            _, _, term, trunc, _ = env.step(a)
+        assert bool(trunc.all())
+        assert (env._epi[:, 12].cpu().numpy() == episode).all()
+        q = env.qpos.cpu().numpy()
+        for k, r in enumerate(refs):
+            r.reset(seed=None)  # stream continues
+            assert tuple(env._epi[k, :2].cpu().numpy()) == r.task(), (episode, k)
+            np.testing.assert_array_equal(q[k, 9:30], r.get_state()[0][9:30].astype(np.float32))
+
+
+def test_diverged_env_autoresets_as_truncated():
+    """A NaN state with autoreset on: the step reports truncated (not a silent reset), the sticky
+    error_resets counter counts it and the env starts a fresh episode."""
+    from mujoco_manip_amd import _lib
+
+    env = _c3_env(4, autoreset=True)
+    env.reset(seed=[1, 2, 3, 4])
+    q, v, c, w = env.sim.get_state()
+    v[1, 3] = np.nan
+    v[2, 0] = 3e10
+    env.sim.set_state(q, v, c, w)
+    _, _, term, trunc, info = env.step(env.expert_plan(16))
+    epi = env._epi.cpu().numpy()
+    assert trunc.cpu().numpy().tolist() == [False, True, True, False]
+    assert epi[:, _lib.EPI["error_resets"]].tolist() == [0, 1, 1, 0]
+    assert (epi[:, _lib.EPI["env_error"]] == 0).all() and (epi[:, _lib.EPI["step_count"]] == [1, 0, 0, 1]).all()
+    assert np.isfinite(env.qvel.cpu().numpy()).all()
+
+
+# --------------------------------------------------------------------------- reference goldens on device
+def test_reward_goldens_on_device(golden):
+    """Reference reward sequences (gym_env.py:341-470): dense / sparse / staged, high-water marks,
+    sticky flags and the staged robot x obstacle collision branch, evaluated by the device reward
+    layer (mmx_eval_reward) from the fixture's positions, gripper command and contact pairs."""
+    from mujoco_manip_amd import _lib
+    from mujoco_manip_amd.constants import BINS, OBJECTS
+
+    for rtype in ("dense", "sparse", "staged"):
+        fx = [c for c in golden["rewards"] if c["reward_type"] == rtype]
+        n = len(fx)
+        sim = _lib.Sim(n, action_mode="abs_pos", reward_type=rtype, image_size=0)
+        sim.reset()
+        epi, epf = sim.view("episode_i", _lib.EPI_N, "<i4"), sim.view("episode_f", _lib.EPF_N)
+        for k, c in enumerate(fx):
+            T = np.array(c["T_init"])
+            epi[k, 0], epi[k, 1], epi[k, 3] = OBJECTS.index(c["obj"]), BINS.index(c["bin"]), 0
+            epf[k, 0:9] = torch.tensor(T[:3, :3].ravel(), dtype=torch.float32)
+            epf[k, 9:12] = torch.tensor(T[:3, 3], dtype=torch.float32)
+            epf[k, 12:17] = 0.0
+        maxp = 4
+        for t in range(len(fx[0]["seq"])):
+            st = [c["seq"][t] for c in fx]
+            obj = torch.tensor([s["obj"] for s in st], dtype=torch.float32, device="cuda")
+            ee = torch.tensor([s["ee"] for s in st], dtype=torch.float32, device="cuda")
+            g = torch.tensor([s["ctrl7"] for s in st], dtype=torch.float32, device="cuda")
+            pairs = torch.full((n, maxp, 2), -1, dtype=torch.int32)
+            for k, s in enumerate(st):
+                for p, (a, b) in enumerate(s["contacts"]):
+                    pairs[k, p] = torch.tensor([a, b])
+            pairs = pairs.cuda()
+            sim.eval_reward(obj.data_ptr(), ee.data_ptr(), g.data_ptr(), pairs.data_ptr(), maxp)
+            torch.cuda.synchronize()
+            rew = sim.view("reward", 1).cpu().numpy()
+            done = sim.view("done", 3, "<i4").cpu().numpy()
+            for k, s in enumerate(st):
+                assert abs(float(rew[k]) - s["reward"]) < 2e-5, (rtype, k, t, float(rew[k]), s["reward"])
+                assert bool(done[k, 2]) == s["success"] or (rtype == "staged" and s["reward"] < 0), (rtype, k, t)
+                if s["hwm"] is not None:
+                    np.testing.assert_allclose(epf[k, 12:17].cpu().numpy(), s["hwm"], atol=2e-6)
+        sim.close()
+    # the collision branch was exercised: the staged fixture holds a -1 (robot x obstacle) step
+    assert any(s["reward"] == -1.0 for c in golden["rewards"] if c["reward_type"] == "staged" for s in c["seq"])
+
+
+def _oracle_states(n=40):
+    import oracle_py as O
+
+    e = O.OracleEnv()
+    e.reset_keyframe()
+    e.fsm_init([(0, 0)])
+    states, targets = [], []
+    for _ in range(200):
+        st = e.fsm_plan(16)
+        f = e.fsm_get()
+        states.append(e.get_state())
+        targets.append(f["target"].copy() if f["state"] != 0 else e.body(9)[0])
+        e.fsm_actuate()
+        for _ in range(16):
+            e.mj_step()
+        if st == 10:
+            break
+    idx = np.linspace(0, len(states) - 1, n).astype(int)
+    return [states[i] for i in idx], [targets[i] for i in idx]
+
+
+def _ik_parity(states, targets, nsub):
+    """GPU: physics_step(nsub, with_ik) toward `targets`; oracle: nsub x (IKController.compute ->
+    set_arm_ctrl -> mj_step), both from a consistent position stage (mj_forward)."""
+    import oracle_py as O
+    from mujoco_manip_amd import _lib
+
+    qpos, qvel, ctrl, ws = [np.stack([s[k] for s in states]).astype(np.float32) for k in range(4)]
+    n = len(states)
+    sim = _lib.Sim(n, action_mode="abs_pos", image_size=0)
+    sim.set_state(qpos, qvel, ctrl, ws)
+    sim.forward()
+    tgt = sim.view("target", 4)
+    tgt[:, :3] = torch.tensor(np.asarray(targets), dtype=torch.float32)
+    tgt[:, 3] = 1.0
+    sim.physics_step(nsub, with_ik=True)
+    gq, gv, gc, _ = sim.get_state()
+    errs = sim.view("episode_i", _lib.EPI_N, "<i4")[:, 9].cpu().numpy()
+    sim.close()
+    assert (errs == 0).all()
+    out = []
+    for k in range(n):
+        e = O.OracleEnv()
+        e.set_state(*(a[k].astype(float) for a in (qpos, qvel, ctrl, ws)))
+        e.mj_forward()
+        for _ in range(nsub):
+            e.set_arm_ctrl(e.ik(np.asarray(targets[k], float)))
+            e.mj_step()
+        rq, rv, rc, _ = e.get_state()
+        out.append((np.abs(gq[k] - rq).max(), np.abs(gv[k] - rv).max(), np.abs(gc[k, :7] - rc[:7]).max()))
+    return np.array(out)
+
+
+def test_physics_parity_with_ik_from_oracle_states():
+    """L1 with the IK in the loop (SURVEY A.5 stale kinematics at substeps >= 1): 40 states along an
+    oracle expert episode incl. grasps and contacts, toward the FSM's own targets."""
+    states, targets = _oracle_states()
+    e1 = _ik_parity(states, targets, 1)
+    assert e1[:, 2].max() < 2e-5, e1[:, 2].max()  # IK output (ctrl[:7]) after one compute
+    assert e1[:, 0].max() < 1e-5 and e1[:, 1].max() < 5e-3, e1.max(0)
+    e16 = _ik_parity(states, targets, 16)
+    assert e16[:, 0].max() < 1e-4 and e16[:, 1].max() < 2e-2, e16.max(0)
+
+
+def test_ik_edge_states():
+    """IKController.compute edge cases (controller.py:21-43, 125-135) on device vs the oracle: the
+    ||dq|| > 5 clamp (far targets), the joint-range clip (joints at / past their limits) and a hand
+    rotated ~pi about its axis from TARGET_ORI (orientation error near pi)."""
+    import oracle_py as O
+
+    base = O.OracleEnv()
+    base.reset_keyframe()
+    q0, v0, c0, w0 = base.get_state()
+    cases = []
+    for far in ([2.0, 2.0, 2.0], [-1.5, 0.2, 1.5], [0.0, -2.0, 0.1]):  # dq clamp
+        cases.append((q0.copy(), np.array(far)))
+    for j, val in ((0, 2.89), (1, -1.76), (3, -3.05), (5, 3.74), (6, -2.89)):  # at / past a limit
+        q = q0.copy()
+        q[j] = val
+        cases.append((q, np.array([0.1, 0.5, 0.35])))
+    for q7 in (0.785 - np.pi + 0.05, 0.785 + np.pi - 0.3):  # hand rotated ~pi about its axis
+        q = q0.copy()
+        q[6] = np.clip(q7, -2.8973, 2.8973)
+        cases.append((q, np.array([0.0, 0.45, 0.42])))
+    states = [(q, v0, c0, w0) for q, _ in cases]
+    targets = [t for _, t in cases]
+    # the reference clamps ||dq|| at 5: confirm the far cases reach it on the oracle
+    e = O.OracleEnv()
+    e.set_state(q0, v0, c0, w0)
+    e.mj_forward()
+    assert np.linalg.norm(e.ik(targets[0]) - q0[:7]) > 1.0
+    err = _ik_parity(states, targets, 1)
+    assert err[:, 2].max() < 5e-5, err[:, 2]
+    assert err[:, 0].max() < 1e-5, err[:, 0]
+
+
+def test_se3_encode_golden_on_device(golden):
+    """pose_utils se3_to_pos_quat_g / se3_to_pos_rot6d_g (golden "se3_encode") computed by the
+    device observation: T_init is set so that inv(T_init) T_cur equals the golden pose, and the
+    device's relative EE encodings (obs state.ee.*_rel) must reproduce the golden vectors."""
+    from mujoco_manip_amd import _lib
+    from mujoco_manip_amd.constants import OBS_SLICES
+
+    cases = golden["se3_encode"]
+    n = len(cases)
+    sim = _lib.Sim(n, action_mode="abs_pos", image_size=0)
+    sim.reset()
+    q, v, c, w = sim.get_state()
+    c[:, 7] = [255.0 * x["g"] for x in cases]
+    sim.set_state(q, v, c, w)
+    sim.forward()
+    kin = sim.view("kin", _lib.KIN_N).cpu().numpy().astype(np.float64)
+    epf = sim.view("episode_f", _lib.EPF_N)
+    for k, x in enumerate(cases):
+        Tc = np.eye(4)
+        Tc[:3, 3], Tc[:3, :3] = kin[k, 0:3], kin[k, 3:12].reshape(3, 3)
+        Ti = Tc @ np.linalg.inv(np.array(x["T"]))
+        epf[k, 0:9] = torch.tensor(Ti[:3, :3].ravel(), dtype=torch.float32)
+        epf[k, 9:12] = torch.tensor(Ti[:3, 3], dtype=torch.float32)
+    sim.forward()
+    obs = sim.view("obs", _lib.NOBS).cpu().numpy()
+    a8, b8, _ = OBS_SLICES["state.ee.pos_quat_g_rel"]
+    a10, b10, _ = OBS_SLICES["state.ee.pos_rot6d_g_rel"]
+    for k, x in enumerate(cases):
+        np.testing.assert_allclose(obs[k, a8:b8], x["q8"], atol=3e-5, err_msg=str(k))
+        np.testing.assert_allclose(obs[k, a10:b10], x["r10"], atol=3e-5, err_msg=str(k))
+    sim.close()
+
+
+def test_observation_goldens_on_device(golden):
+    """The device's whole 85-float observation vs the reference's _get_obs (gym_env.py:283-339,
+    cameras.py:56-130, target keypoints of reset gym_env.py:519-531): at the randomized C3 reset
+    and at later states of each episode (set_state + mj_forward)."""
+    from mujoco_manip_amd import _lib
+    from mujoco_manip_amd.constants import OBS_SLICES
+
+    eps = golden["obs"]
+    n = len(eps)
+    env = _c3_env(n)
+    obs, _ = env.reset(seed=[ep["seed"] for ep in eps])
+    assert [tuple(t) for t in env.tasks] == [tuple(ep["task"]) for ep in eps]
+
+    def flat(d):
+        return np.concatenate([np.asarray(d[k], float).ravel() for k in OBS_SLICES])
+
+    got = env.sim.view("obs", _lib.NOBS).cpu().numpy()
+    for k, ep in enumerate(eps):
+        np.testing.assert_allclose(got[k], flat(ep["states"][0]["obs"]), atol=2e-5, err_msg=f"reset {k}")
+    for j in range(1, len(eps[0]["states"])):
+        q, v, c, w = env.sim.get_state()
+        for k, ep in enumerate(eps):
+            q[k] = ep["states"][j]["qpos"]
+            c[k] = ep["states"][j]["ctrl"]
+        env.sim.set_state(q, v, c, w)
+        env.sim.forward()
+        got = env.sim.view("obs", _lib.NOBS).cpu().numpy()
+        for k, ep in enumerate(eps):
+            # wrist keypoints: the camera sits ~0.1 m from the cubes, fp32 kinematics error x ~10
+            np.testing.assert_allclose(got[k], flat(ep["states"][j]["obs"]), atol=5e-5, err_msg=f"ep {k} state {j}")
+
+
+# --------------------------------------------------------------------------- per-physics-step FSM
+def test_expert_physics_parity_with_oracle():
+    """main.py:65-91 loop (update() = plan(1) + _actuate(), then mj_step) on device vs the oracle
+    over the first 400 physics steps of 4 tasks from the keyframe (approach + grasp descent)."""
+    import oracle_py as O
+    from mujoco_manip_amd import _lib
+
+    tasks = [(0, 0), (1, 2), (2, 1), (0, 2)]
+    n = len(tasks)
+    sim = _lib.Sim(n, action_mode="abs_pos", image_size=0)
+    sim.reset(task_override=np.array([(o << 4) | b for o, b in tasks], np.int32))
+    refs = []
+    for o, b in tasks:
+        e = O.OracleEnv()
+        e.reset_keyframe()
+        e.mj_forward()
+        e.fsm_init([(o, b)])
+        refs.append(e)
+    for chunk in range(4):
+        sim.expert_physics(100)
+        gq = sim.get_state()[0]
+        epi = sim.view("episode_i", _lib.EPI_N, "<i4").cpu().numpy()
+        for k, e in enumerate(refs):
+            for _ in range(100):
+                e.fsm_plan(1)
+                e.fsm_actuate()
+                e.mj_step()
+            assert epi[k, 4] == e.fsm_get()["state"], (chunk, k)
+            np.testing.assert_allclose(gq[k], e.get_state()[0], atol=2e-4, err_msg=f"chunk {chunk} env {k}")
+    sim.close()
+
+
+def test_expert_physics_completes_kat():
+    """tests/test_pick_and_place.py:147-166 on the GPU batch: the per-physics-step FSM finishes
+    within 20 000 physics steps and visits >= 6 phases."""
+    from mujoco_manip_amd import _lib
+
+    tasks = [(o, b) for o in range(3) for b in range(3)]
+    n = len(tasks)
+    sim = _lib.Sim(n, action_mode="abs_pos", image_size=0)
+    sim.reset(task_override=np.array([(o << 4) | b for o, b in tasks], np.int32))
+    steps = 0
+    while steps < 20000:
+        sim.expert_physics(1000)
+        steps += 1000
+        epi = sim.view("episode_i", _lib.EPI_N, "<i4").cpu().numpy()
+        if (epi[:, 4] == 10).all():
+            break
+    assert (epi[:, 4] == 10).all(), f"unfinished after {steps} physics steps: {epi[:, 4]}"
+    phases = [bin(int(m)).count("1") for m in epi[:, _lib.EPI["fsm_phases"]]]
+    assert min(phases) >= 6, phases
+    assert (epi[:, _lib.EPI["env_error"]] == 0).all()
+    print(f"finished within {steps} physics steps; phases visited {phases}")

@@ -142,3 +142,41 @@ def test_geom_classes_match_reference(golden):  # gym_env.py:137-152
     names = [b["name"] for b in model["bodies"]]
     rob = [i for i, g in enumerate(model["col_geoms"]) if names[model["geoms"][g]["body"]] in robot_names]
     assert rob == golden["robot_geoms"]
+
+
+def test_se3_encode_host_codec(golden):  # pose_utils.py:104-130 (se3_to_pos_quat_g / se3_to_pos_rot6d_g)
+    from mujoco_manip_amd import pose_utils as P
+
+    for c in golden["se3_encode"]:
+        T = np.array(c["T"])
+        np.testing.assert_allclose(P.se3_to_pos_quat_g(T, c["g"]), c["q8"], atol=1e-7)
+        np.testing.assert_allclose(P.se3_to_pos_rot6d_g(T, c["g"]), c["r10"], atol=1e-7)
+        # the oracle's quaternion codec (branch-exact) on the same rotation
+        np.testing.assert_allclose(O.rotmat_to_quat_xyzw(T[:3, :3]), c["q8"][3:7], atol=1e-7)
+        # and back: decode of the encodings recovers the translation (gym_env.py:252-281)
+        tgt, g = O.decode_action("ee_pos_quat_g", np.array(c["q8"], np.float32), np.eye(4))
+        np.testing.assert_allclose(tgt, T[:3, 3], atol=1e-6)
+        assert g == c["g"]
+
+
+def _flat_obs(d):
+    from mujoco_manip_amd.constants import OBS_SLICES
+
+    return np.concatenate([np.asarray(d[k], float).ravel() for k in OBS_SLICES])
+
+
+def test_oracle_observation_matches_reference_get_obs(golden):  # gym_env.py:283-339, cameras.py:56-130
+    """The oracle's 85-float observation vs the reference's _get_obs on the same kinematics: at the
+    randomized reset (incl. target keypoints and T_init) and at later states of the episode."""
+    from mujoco_manip_amd.constants import TASK_SETS
+
+    pool = [(OBJ.index(o), BIN.index(b)) for o, b in TASK_SETS["all"]]
+    for ep in golden["obs"]:
+        e = O.OracleEnv(action_mode="abs_pos", reward_type="staged", randomize_objects=True, tasks=pool)
+        obs0 = e.reset(seed=ep["seed"])
+        assert (OBJ[e.task()[0]], BIN[e.task()[1]]) == tuple(ep["task"])
+        np.testing.assert_allclose(obs0, _flat_obs(ep["states"][0]["obs"]), atol=1e-6)
+        for st in ep["states"][1:]:
+            e.set_state(qpos=np.array(st["qpos"]), ctrl=np.array(st["ctrl"]))
+            e.mj_forward()
+            np.testing.assert_allclose(e.obs(), _flat_obs(st["obs"]), atol=1e-6, err_msg=f"t={st['t']}")
