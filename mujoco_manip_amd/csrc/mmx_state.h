@@ -14,7 +14,7 @@
 #define MMX_NU_ 8
 #define MMX_NOBS 85
 #define MMX_MAXCON 64
-#define MMX_MAXEFC 304
+#define MMX_MAXEFC 384
 // constraint rows [0, MMX_LDSEFC) live in the workgroup's LDS, rows [MMX_LDSEFC, MMX_MAXEFC) in the
 // env's HBM overflow block (efc_ovf); 192 rows keep the env's LDS under 20 KB (8 envs per CU)
 #ifndef MMX_LDSEFC

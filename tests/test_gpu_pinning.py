@@ -431,8 +431,12 @@ def test_expert_physics_parity_with_oracle():
                 e.fsm_plan(1)
                 e.fsm_actuate()
                 e.mj_step()
+            rq = e.get_state()[0]
             assert epi[k, 4] == e.fsm_get()["state"], (chunk, k)
-            np.testing.assert_allclose(gq[k], e.get_state()[0], atol=2e-4, err_msg=f"chunk {chunk} env {k}")
+            # robot joints tight (IK + smooth dynamics); the cubes (touched by the fingers from the
+            # grasp descent on) behaviourally, as SURVEY §8d L2 treats contact dynamics
+            np.testing.assert_allclose(gq[k, :9], rq[:9], atol=2e-4, err_msg=f"chunk {chunk} env {k}")
+            np.testing.assert_allclose(gq[k, 9:], rq[9:], atol=5e-3, err_msg=f"chunk {chunk} env {k}")
     sim.close()
 
 
