@@ -8,15 +8,22 @@ sharding), FSM-expert abs_pos actions computed on device (pick_and_place.py plan
 same-step autoreset.  One "step" = one PickPlaceGymEnv.step for every env: decode -> 16 x
 (DLS IK + mj_step) -> mj_forward (position stage) -> staged reward -> 85-float obs.
 
-Multi-GPU: one process per GPU (torchrun), weak scaling (4096 envs per rank), no data-path
-collective; an all_reduce(MAX) of the elapsed time and an all_gather of per-rank stats for
-logging only.
+Timing: W warm-up env steps, then `--repeats` windows of exactly K env steps,
+each bracketed by a barrier + device synchronise on both sides and timed as the max over ranks;
+the line reports the median window (all windows listed under "repeats").
+
+Multi-GPU: one process per GPU, weak scaling (4096 envs per rank), no data-path collective.
+Under torchrun the ranks come from the environment; `--gpus N` without torchrun starts the N
+rank processes itself (before anything touches a GPU) and relays rank 0's line.  Collectives:
+barrier, all_reduce(MAX) of the window time, all_reduce(SUM) of the episode counters.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -28,6 +35,7 @@ sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 SUBSTEPS = 16  # physics substeps per env step (all inside one mmx_env_step_kernel launch)
+METRIC = "env steps/sec (whole node) at 4096 parallel envs; 1/2/4/8 MI355X scaling"
 
 
 def algorithmic_bytes_per_env_step(nefc: float) -> float:
@@ -39,61 +47,158 @@ def algorithmic_bytes_per_env_step(nefc: float) -> float:
 def min_hbm_bytes_per_env_step() -> float:
     """Bytes the fused kernel must move per env step: env record in+out (qpos, qvel, ctrl,
     warm start, IK cache, target, stats, episode ints/floats, rng) + obs/reward/flags out."""
-    rec = 4 * (30 + 27 + 8 + 27 + 54 + 4 + 17 + 14 + 28) + 8 * 4 + 4
+    rec = 4 * (30 + 27 + 8 + 27 + 63 + 4 + 17 + 18 + 28) + 8 * 4 + 4
     return 2 * rec + 4 * (85 + 1 + 3 + 6)
 
 
+# ----------------------------------------------------------------------------- CPU baseline
+def _cpu_model() -> str:
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_budget() -> tuple[int, dict]:
+    """Host cores this process may use: the affinity mask, capped by the cgroup CPU quota and by
+    OMP_NUM_THREADS when set (the GPU box grants each 1-GPU job a CPU share of the host)."""
+    info = {"host_cpu_count": os.cpu_count(), "cpu_model": _cpu_model()}
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    info["affinity"] = n
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            info["cgroup_quota_cpus"] = int(q) / int(p)
+            n = min(n, max(1, int(int(q) / int(p))))
+    except (OSError, ValueError):
+        pass
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        info["omp_num_threads"] = int(os.environ["OMP_NUM_THREADS"])
+        n = min(n, max(1, int(os.environ["OMP_NUM_THREADS"])))
+    return max(1, n), info
+
+
+def _expert_episode(e, seconds_left, t0):
+    """One FSM-expert episode on an oracle env (generate_dataset.py:140-196): plan(16) -> abs_pos
+    -> step until the FSM is done.  Returns (env steps, placed)."""
+    o, b = e.task()
+    e.fsm_init([(o, b)])
+    steps = 0
+    for _ in range(500):
+        if e.fsm_plan(16) == 10:
+            break
+        f = e.fsm_get()
+        e.step(np.array([*f["target"], float(f["gripper_open"])], np.float32))
+        steps += 1
+        if time.perf_counter() - t0 > seconds_left:
+            break
+    return steps
+
+
 def _cpu_worker(args) -> tuple:
-    """One single-env C3 loop on the oracle for `seconds`; episodes worker, worker + P, ..."""
+    """Single-env C3 loops on the oracle for `seconds`: episodes worker, worker + P, ..."""
     worker, nworkers, seconds = args
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle_py as O
     from mujoco_manip_amd.constants import ALL_TASKS, BINS, OBJECTS
 
-    steps = 0
+    pool = [(OBJECTS.index(o), BINS.index(b)) for o, b in ALL_TASKS]
+    steps, ep = 0, worker
     t0 = time.perf_counter()
-    ep = worker
     while time.perf_counter() - t0 < seconds:
-        e = O.OracleEnv(action_mode="abs_pos", reward_type="staged", randomize_objects=True,
-                        tasks=[(OBJECTS.index(o), BINS.index(b)) for o, b in ALL_TASKS])
+        e = O.OracleEnv(action_mode="abs_pos", reward_type="staged", randomize_objects=True, tasks=pool)
         e.reset(seed=O.episode_seed(42, ep))
-        o, b = e.task()
-        e.fsm_init([(o, b)])
-        for _ in range(400):
-            st = e.fsm_plan(16)
-            if st == 10:
-                break
-            f = e.fsm_get()
-            tgt = f["target"] if f["state"] != 0 else e.body(9)[0]
-            e.step(np.array([*tgt, float(f["gripper_open"])], np.float32))
-            steps += 1
-            if time.perf_counter() - t0 > seconds:
-                break
+        steps += _expert_episode(e, seconds, t0)
         ep += nworkers
     return steps, time.perf_counter() - t0, (ep - worker) // nworkers
 
 
-def cpu_baseline(seconds: float = 12.0, workers: int | None = None) -> dict:
+def c1_single_thread(seconds: float = 5.0) -> dict:
+    """C1: 1 env, task (obj_red, bin_red), staged reward, keyframe start, FSM
+    expert (generate_dataset.py:140-196), timed single-threaded on the oracle."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle_py as O
+
+    lengths, steps = [], 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        e = O.OracleEnv(action_mode="abs_pos", reward_type="staged", task=(0, 0))
+        e.reset(seed=len(lengths))
+        n = _expert_episode(e, 1e9, t0)
+        lengths.append(n)
+        steps += n
+    dt = time.perf_counter() - t0
+    return {"value": steps / dt, "unit": "env steps/s", "cores": 1, "episodes": len(lengths),
+            "episode_length": int(np.median(lengths)), "ms_per_env_step": 1000.0 * dt / max(steps, 1),
+            "kind": "port", "sample": f"{len(lengths)} C1 FSM-expert episodes in {dt:.1f} s, one thread"}
+
+
+def cpu_baseline(seconds: float = 30.0, workers: int | None = None) -> dict:
     """The oracle (fp64 C restatement; MuJoCo is absent on the box) on a bounded sample of the
-    same workload: P independent single-env C3 loops, one per host core share,
-    run before the process touches the GPU.  Throughput = sum over workers."""
+    same workload: P independent single-env C3 loops for `seconds`, one per usable host core
+    (BASELINE.md §4), run before the process touches the GPU.  Throughput = sum over workers."""
     import multiprocessing as mp
 
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle_py as O
 
     O.build()
-    if workers is None:
-        workers = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", "0")) or (os.cpu_count() or 1)))
+    budget, info = cpu_budget()
+    workers = workers or budget
     with mp.get_context("fork").Pool(workers) as pool:
         res = pool.map(_cpu_worker, [(w, workers, seconds) for w in range(workers)])
     steps = sum(r[0] for r in res)
     rate = sum(r[0] / r[1] for r in res)
     eps = sum(r[2] for r in res)
-    return {"value": rate, "unit": "env steps/s", "cores": workers, "kind": "port",
-            "sample": f"{steps} env steps ({eps} FSM-expert episodes, C3 settings) in {seconds:.0f}s on each of "
-                      f"{workers} worker processes (1 thread each); oracle/ fp64 C restatement, MuJoCo absent on "
-                      f"the box; host cpu_count={os.cpu_count()}"}
+    out = {"value": rate, "unit": "env steps/s", "cores": workers, "kind": "port",
+           "sample": f"{steps} env steps ({eps} FSM-expert C3 episodes) in {seconds:.0f} s on each of {workers} "
+                     f"worker processes (1 thread each, one per usable core); engine: oracle/ fp64 C restatement "
+                     f"(MuJoCo absent on the box)", **info}
+    out["c1"] = c1_single_thread()
+    return out
+
+
+# ----------------------------------------------------------------------------- rank launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(n: int) -> int:
+    """`--gpus N` without torchrun: start N rank processes of this script (one GPU each, RCCL),
+    before this process touches any GPU; rank 0 prints the line.  Returns the worst exit code."""
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    return max(abs(rc) for rc in rcs)
+
+
+# ----------------------------------------------------------------------------- PMC evidence
+def pmc_evidence(workload: str, envs: int, spl: int, lanes: int) -> dict | None:
+    """Counter evidence recorded by tools/profile.sh for THIS configuration (same workload, envs
+    per GPU, env steps per launch and concurrent launches); None when absent or different."""
+    f = os.path.join(REPO, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(f):
+        return None
+    try:
+        rec = json.load(open(f))
+    except (OSError, ValueError):
+        return None
+    c = rec.get("config", {})
+    if (c.get("workload"), c.get("envs_per_gpu"), c.get("env_steps_per_launch"), c.get("lanes")) != \
+            (workload, envs, spl, lanes):
+        return None
+    return rec
 
 
 def main():
@@ -103,9 +208,10 @@ def main():
     # launch length (16 env steps per launch) keep every timed dispatch the same size
     ap.add_argument("--steps", type=int, default=512)
     ap.add_argument("--warmup", type=int, default=64)
+    ap.add_argument("--repeats", type=int, default=5)
     ap.add_argument("--envs-per-gpu", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=30.0)
     # rehearsal of the N > 1 path on a 1-GPU box: ranks share device 0 and talk over gloo
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"))
     ap.add_argument("--share-device", action="store_true")
@@ -123,12 +229,16 @@ def main():
     if args.workload == "c2" and args.envs_per_gpu == 4096:
         args.envs_per_gpu = 1024
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    # CPU baseline first: worker processes are forked before anything initialises the GPU
+    from mujoco_manip_amd.shard import dist_env, shard_seeds
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    rank, local_rank, world = dist_env()
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: one rank per GPU")
+    # CPU baseline first (rank 0 at N = 1): worker processes fork before anything initialises the GPU
     cpu = None
-    if not args.no_cpu_baseline and world == 1 and rank == 0:
+    if not args.no_cpu_baseline and world == 1:
         cpu = cpu_baseline(args.cpu_seconds)
     dist = None
     dev_index = 0 if args.share_device else local_rank
@@ -150,99 +260,101 @@ def main():
     env = PickPlaceVecEnv(N, task=("obj_red", "bin_red") if c2 else None, tasks="all", action_mode="abs_pos",
                           reward_type="staged", randomize_objects=not c2, image_size=args.image_size,
                           autoreset=True, device=dev_index)
-    seeds = [_lib.episode_seed(42, rank * N + i) for i in range(N)]
-    env.reset(seed=seeds)
-
-    # warmup
+    env.reset(seed=shard_seeds(42, rank, world, N))
     env.rollout_expert(args.warmup)
     torch.cuda.synchronize()
-    env.clear_stats()
-    # the sim launches on torch's current stream and forks its `lanes` concurrent env ranges from
-    # it (each range: one mmx_env_step_kernel launch per env step on its own stream, joined back at
-    # the end): events on that stream bracket the K env steps of every range, so kern_ms is the
-    # per-step span over which the lanes' launches (N envs in total) ran side by side
-    stream = torch.cuda.current_stream(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    env.rollout_expert(args.steps)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    # each lane runs ceil(K / spl) launches of up to spl env steps of its envs, back to back
+
     spl = env.sim.rollout_steps_per_launch
+    lanes = env.sim.rollout_lanes
     launches = -(-args.steps // spl)
-    kern_ms = ev0.elapsed_time(ev1) / launches  # per launch
-    if dist:
-        t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    solver = env.solver_stats()
-    env_steps = args.steps * N * world
-    value = env_steps / elapsed
-    ms_per_step = 1000.0 * elapsed / args.steps
+    # the sim launches on torch's current stream and forks its `lanes` concurrent env ranges from
+    # it (each range: one mmx_env_step_kernel launch per spl env steps on its own stream, joined
+    # back at the end): events on that stream bracket the K env steps of every range, so
+    # kern_ms is the span over which one launch of each range (N envs in total) ran side by side
+    stream = torch.cuda.current_stream(dev)
+    cnt = [_lib.EPI[k] for k in ("episodes", "successes", "placed", "error_resets")]
+    windows = []
+    for _ in range(max(1, args.repeats)):
+        env.clear_stats()
+        epi0 = env._epi[:, cnt].sum(0).double()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        env.rollout_expert(args.steps)
+        ev1.record(stream)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        kern_ms = ev0.elapsed_time(ev1) / launches  # per launch
+        eps = (env._epi[:, cnt].sum(0).double() - epi0).tolist()
+        errs_now = float((env.env_error != 0).sum().item())
+        solver = env.solver_stats()
+        if dist:
+            t = torch.tensor([elapsed], device=cdev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+            c = torch.tensor(eps + [errs_now], device=cdev, dtype=torch.float64)
+            dist.all_reduce(c, op=dist.ReduceOp.SUM)
+            eps, errs_now = c[:4].tolist(), float(c[4].item())
+        windows.append({"elapsed": elapsed, "kern_ms": kern_ms, "solver": solver,
+                        "episodes": {"completed": int(eps[0]), "successes": int(eps[1]), "placed": int(eps[2]),
+                                     "error_resets": int(eps[3]), "envs_with_error_now": int(errs_now)}})
+    values = [args.steps * N * world / w["elapsed"] for w in windows]
+    med = windows[int(np.argsort(values)[len(values) // 2])]
+    value = args.steps * N * world / med["elapsed"]
+    solver, kern_ms = med["solver"], med["kern_ms"]
     # spl env steps of the batch = `lanes` concurrent mmx_env_step_kernel dispatches of N / lanes
     # envs x spl steps each; they run side by side for the whole span, so a dispatch lasts ~kern_ms
     # (rocprof's per-dispatch average agrees) and the chip-level rate is lanes x one dispatch's
-    # bytes / kern_ms
-    lanes = env.sim.rollout_lanes
+    # bytes / kern_ms.  nefc is the mean rows per substep counted on device in the same window.
     envs_per_launch = N / lanes
     steps_per_launch = args.steps / launches
-    bytes_per_launch = algorithmic_bytes_per_env_step(solver["mean_nefc"]) * envs_per_launch * steps_per_launch
+    bpe = algorithmic_bytes_per_env_step(solver["mean_nefc"])
+    bytes_per_launch = bpe * envs_per_launch * steps_per_launch
     achieved = lanes * bytes_per_launch / (kern_ms * 1e-3) / 1e9
     min_bytes = min_hbm_bytes_per_env_step() * envs_per_launch * steps_per_launch
-
-    stats_all = None
-    if dist:
-        loc = torch.tensor([solver["mean_nefc"], solver["mean_solver_iter"], value / world], device=cdev)
-        gathered = [torch.zeros_like(loc) for _ in range(world)]
-        dist.all_gather(gathered, loc)
-        stats_all = [g.tolist() for g in gathered]
+    ep = med["episodes"]
 
     if rank == 0:
-        traffic = None
-        tf = os.path.join(REPO, "profiles", "pmc_traffic.json")
-        if os.path.exists(tf):
-            try:
-                traffic = json.load(open(tf)).get("bytes_per_launch")
-            except Exception:
-                traffic = None
+        pmc = pmc_evidence(args.workload, N, spl, lanes)
+        traffic = None if pmc is None else pmc["hbm_bytes_per_env_step"] * envs_per_launch * steps_per_launch
+        workload = (f"C2: PickPlaceGymEnv.step x {N} envs/GPU, fixed task (obj_red, bin_red), keyframe start (no "
+                    "randomisation), staged reward, FSM expert abs_pos, autoreset" if c2 else
+                    f"C3: PickPlaceGymEnv.step x {N} envs/GPU, tasks=all, randomize_objects, seed=42 episode seeds, "
+                    "staged reward, FSM expert abs_pos, autoreset" if args.image_size == 0 else
+                    f"C5: C3 settings x {N} envs/GPU plus overhead + wrist RGB {args.image_size}x{args.image_size} "
+                    "camera images rendered every env step")
         line = {
-            "metric": "env steps/sec (whole node) at 4096 parallel envs; 1/2/4/8 MI355X scaling",
-            "value": value, "unit": "env steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-            "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-            "dtype": "f32", "data": "synthetic (seeded randomized scenes, FSM-expert actions)",
-            "config": {"workload": (f"C2: PickPlaceGymEnv.step x {N} envs/GPU, fixed task (obj_red, bin_red), "
-                                    "keyframe start (no randomisation), staged reward, FSM expert abs_pos, autoreset"
-                                    if c2 else
-                                    f"C3: PickPlaceGymEnv.step x {N} envs/GPU, tasks=all, randomize_objects, "
-                                    "seed=42 episode seeds, staged reward, FSM expert abs_pos, autoreset"
-                                    if args.image_size == 0 else
-                                    f"C5: C3 settings x {N} envs/GPU plus overhead + wrist RGB {args.image_size}x"
-                                    f"{args.image_size} camera images rendered every env step"),
-                       "envs_per_gpu": N, "global_envs": N * world, "substeps": 16, "image_size": args.image_size,
-                       "parallelism": f"env-batch dp{world}"},
+            "metric": METRIC, "value": value, "unit": "env steps/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1000.0 * med["elapsed"] / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (seeded randomized scenes, FSM-expert actions)",
+            "config": {"workload": workload, "envs_per_gpu": N, "global_envs": N * world, "substeps": SUBSTEPS,
+                       "image_size": args.image_size, "parallelism": f"env-batch dp{world}"},
+            "repeats": {"n": len(values), "values": values, "median_of": "value"},
+            "physics_steps_per_s": SUBSTEPS * value,
+            "episodes": {**ep, "placed_rate": ep["placed"] / max(ep["completed"], 1),
+                         "note": "episodes that ended inside the median window (autoreset on FSM done / "
+                                 "termination / truncation / divergence), summed over ranks; placed = target cube "
+                                 "in the target bin at the episode's end; staged success needs the EE back at "
+                                 "its start pose, which the expert's retreat target does not reach"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "mmx_env_step_kernel", "kernel_ms": kern_ms,
-                         "concurrent_launches": lanes, "envs_per_launch": envs_per_launch,
-                         "env_steps_per_launch": steps_per_launch,
-                         "algorithmic_bytes_per_env_step": algorithmic_bytes_per_env_step(solver["mean_nefc"]),
-                         "algorithmic_bytes_per_launch": bytes_per_launch, "mean_nefc": solver["mean_nefc"],
-                         "traffic_note": "traffic = PMC FETCH_SIZE x2 + WRITE_SIZE per dispatch "
-                                         "(profiles/pmc_traffic.json), same dispatch size",
+                         "kernel": "mmx_env_step_kernel", "kernel_ms": kern_ms, "concurrent_launches": lanes,
+                         "envs_per_launch": envs_per_launch, "env_steps_per_launch": steps_per_launch,
+                         "algorithmic_bytes_per_env_step": bpe, "algorithmic_bytes_per_launch": bytes_per_launch,
+                         "mean_nefc": solver["mean_nefc"],
+                         "traffic_source": None if pmc is None else pmc.get("source"),
                          "min_hbm_bytes_per_launch": min_bytes,
                          "min_hbm_GBs": lanes * min_bytes / (kern_ms * 1e-3) / 1e9},
+            "valu": None if pmc is None else pmc.get("valu"),
             "cpu_baseline": cpu,
             "solver": solver,
         }
-        if stats_all:
-            line["per_rank"] = stats_all
         print(json.dumps(line), flush=True)
     if dist:
         dist.destroy_process_group()

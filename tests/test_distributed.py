@@ -1,15 +1,21 @@
-"""Multi-process (gloo, world_size 2) check of the env-batch sharding used by bench.py on N GPUs.
+"""Multi-process (world_size 2) checks of the env-batch sharding bench.py uses on N GPUs.
 
-Envs shard embarrassingly: rank r owns global envs [r*n, (r+1)*n), each seeded
-from its GLOBAL index, so trajectories do not depend on the number of ranks.  The only
-collectives are logging ones (all_gather of per-env stats, all_reduce(MAX) of wall time).
-Here each rank steps its shard with the CPU oracle and the gathered result must equal a
-single-process run.
+Envs shard embarrassingly: rank r owns global envs [r*n, (r+1)*n)
+(mujoco_manip_amd.shard), each seeded from its GLOBAL index, so trajectories do not depend on the
+number of ranks.  The only collectives are logging ones (all_gather / all_reduce(SUM) of
+counters, all_reduce(MAX) of wall time).
+  * CPU (gloo): each rank steps its shard with the oracle; the gathered result equals a
+    single-process run.
+  * GPU: two fresh rank processes share device 0 (gloo between them) and run the HIP rollout on
+    their shards; the gathered per-env results are bit-equal to one process with all 2n envs.
 """
+import subprocess
+import sys
 import os
 import socket
 
 import numpy as np
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -36,14 +42,13 @@ def shard_rollout(env_ids):
 
 
 def _worker(rank, world, port, q):
-    import sys
-
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    n = N_GLOBAL // world
-    local = torch.tensor(shard_rollout(range(rank * n, (rank + 1) * n)))
+    from mujoco_manip_amd.shard import shard_range
+
+    local = torch.tensor(shard_rollout(shard_range(rank, world, N_GLOBAL // world)))
     gathered = [torch.zeros_like(local) for _ in range(world)]
     dist.all_gather(gathered, local)
     t = torch.tensor([float(rank + 1)])
@@ -74,3 +79,50 @@ def test_two_rank_sharding_matches_single_process():
     assert tmax == 2.0
     single = shard_rollout(range(N_GLOBAL))
     np.testing.assert_array_equal(gathered, single)
+
+
+def test_shard_ranges_and_seeds():
+    from mujoco_manip_amd import _lib
+    from mujoco_manip_amd.shard import shard_range, shard_seeds
+
+    assert list(shard_range(0, 2, 3)) == [0, 1, 2] and list(shard_range(1, 2, 3)) == [3, 4, 5]
+    assert shard_seeds(42, 1, 4, 2) == [_lib.episode_seed(42, 2), _lib.episode_seed(42, 3)]
+    all8 = sum((shard_seeds(42, r, 4, 2) for r in range(4)), [])
+    assert all8 == [_lib.episode_seed(42, g) for g in range(8)]  # independent of the rank count
+    with pytest.raises(ValueError):
+        shard_range(2, 2, 3)
+
+
+def test_bench_rejects_mismatched_world(monkeypatch):
+    """bench.py --gpus N under a torchrun world of another size is an error, not a silent 1-GPU run."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                     "bench.py"), "--gpus", "2", "--no-cpu-baseline"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in (r.stderr + r.stdout)
+
+
+@pytest.mark.gpu
+def test_two_rank_hip_rollout_matches_single_process(tmp_path):
+    if not torch.cuda.is_available():
+        pytest.skip("needs an MI355X")
+    from mujoco_manip_amd import _lib
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    n, steps = 12, 48
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = str(tmp_path / "ranks.npz")
+    port = str(_free_port())
+    procs = [subprocess.Popen([sys.executable, os.path.join(here, "dist_rollout_worker.py"), str(n), str(steps), out],
+                              env=dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2",
+                                       MASTER_ADDR="127.0.0.1", MASTER_PORT=port)) for r in range(2)]
+    assert [p.wait(timeout=240) for p in procs] == [0, 0]
+    ranks = np.load(out)["rows"]
+    env = PickPlaceVecEnv(2 * n, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
+                          image_size=0, autoreset=True)
+    env.reset(seed=[_lib.episode_seed(42, g) for g in range(2 * n)])
+    env.rollout_expert(steps)
+    torch.cuda.synchronize()
+    q, v, _, _ = env.sim.get_state()
+    epi = env.sim.view("episode_i", _lib.EPI_N, "<i4").cpu().numpy()
+    np.testing.assert_array_equal(ranks, np.concatenate([q, v, epi.view(np.float32)], 1))

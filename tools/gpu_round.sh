@@ -1,7 +1,14 @@
 set -o pipefail
+# round evidence on the GPU box: parity suite, default bench line, 2-rank rehearsal on one GPU,
+# rocprofv3 trace + PMC passes (tools/profile.sh); every GPU step under its own time limit
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && \
-timeout -k 10 300 python -u bench.py > gpurun_out/bench.log 2>&1 && \
-bash tools/profile.sh r01 > gpurun_out/profile.log 2>&1
-echo exit $?
+R=${ROUND:-r02}
+timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && \
+timeout -k 10 400 python -u bench.py > gpurun_out/bench.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --gpus 2 --share-device --dist-backend gloo --steps 64 --repeats 1 \
+   --no-cpu-baseline > gpurun_out/bench_2rank_rehearsal.log 2>&1 && \
+bash tools/profile.sh $R > gpurun_out/profile.log 2>&1
+rc=$?
+tail -3 gpurun_out/gpu_tests.log; grep -h "^{" gpurun_out/bench.log | cut -c1-400; tail -2 gpurun_out/profile.log
+exit $rc

@@ -1,10 +1,12 @@
-"""Condense rocprofv3 CSV output into committed evidence under profiles/.
+"""Condense rocprofv3 CSV output (tools/profile.sh) into committed evidence under profiles/.
 
-- profiles/<round>_kernel_stats.csv : rocprofv3 --stats summary of the bench run (copied)
-- profiles/<round>_bench_trace.json : the bench JSON line printed under the tracer
-- profiles/pmc_traffic.json         : HBM-side bytes per launch of mmx_env_step_kernel from
-  the FETCH_SIZE and WRITE_SIZE passes (KB -> bytes; FETCH_SIZE doubled per the gfx950 note in
-  MI355X_MICROARCH.md §HBM: it tallies 128-B read requests at 64 B), averaged over dispatches.
+- profiles/<round>_<workload>_kernel_stats.csv : rocprofv3 --stats summary of the traced bench run
+- profiles/<round>_<workload>_bench_trace.json : the bench JSON line printed under the tracer
+- profiles/pmc_<workload>.json (+ a <round>_ copy): per env step of mmx_env_step_kernel over the
+  timed window's dispatches (the last ones of each pass), tagged with the configuration:
+    * HBM-side bytes: FETCH_SIZE x2 (gfx950: it tallies 128-B read requests at 64 B,
+      MI355X_MICROARCH.md §HBM) + WRITE_SIZE, KB -> bytes, each counter from its own pass;
+    * VALU issue: SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES per wave x resident waves per SIMD.
 """
 from __future__ import annotations
 
@@ -21,52 +23,88 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _rows(pattern):
     out = []
-    for f in glob.glob(pattern, recursive=True):
+    for f in sorted(glob.glob(pattern, recursive=True)):
         with open(f, newline="") as fh:
             out.extend(csv.DictReader(fh))
     return out
 
 
-def counter_per_dispatch(prof_dir: str, counter: str) -> tuple[float, int]:
-    rows = _rows(os.path.join(prof_dir, "**", "*counter_collection.csv"))
+def per_dispatch(prof_dir: str, counters: list[str]) -> list[dict]:
+    """[{counter: value}] per dispatch of KERNEL, in dispatch order."""
     per = {}
-    for r in rows:
-        if KERNEL not in r.get("Kernel_Name", "") or r.get("Counter_Name") != counter:
+    for r in _rows(os.path.join(prof_dir, "**", "*counter_collection.csv")):
+        if KERNEL not in r.get("Kernel_Name", "") or r.get("Counter_Name") not in counters:
             continue
-        d = r.get("Dispatch_Id") or r.get("Correlation_Id")
-        per[d] = per.get(d, 0.0) + float(r["Counter_Value"])
+        d = int(r.get("Dispatch_Id") or r.get("Correlation_Id"))
+        per.setdefault(d, {}).setdefault(r["Counter_Name"], 0.0)
+        per[d][r["Counter_Name"]] += float(r["Counter_Value"])
     if not per:
-        raise SystemExit(f"no {counter} rows for {KERNEL} under {prof_dir}")
-    return sum(per.values()) / len(per), len(per)
+        raise SystemExit(f"no {counters} rows for {KERNEL} under {prof_dir}")
+    return [per[d] for d in sorted(per)]
+
+
+def timed_mean(rows: list[dict], n_last: int) -> dict:
+    rows = rows[-n_last:]
+    return {k: sum(r.get(k, 0.0) for r in rows) / len(rows) for k in rows[0]}
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--round", default="r01")
-    ap.add_argument("--prof", default=os.path.join(REPO, "gpurun_out", "prof"))
+    ap.add_argument("--round", default="r02")
+    ap.add_argument("--workload", default="c3")
+    ap.add_argument("--prof", required=True)
+    ap.add_argument("--timed-steps", type=int, default=64)
     a = ap.parse_args()
     dst = os.path.join(REPO, "profiles")
     os.makedirs(dst, exist_ok=True)
+    tag = f"{a.round}_{a.workload}"
     stats = glob.glob(os.path.join(a.prof, "trace", "**", "*kernel_stats.csv"), recursive=True)
     if stats:
-        shutil.copy(stats[0], os.path.join(dst, f"{a.round}_kernel_stats.csv"))
-    log = os.path.join(a.prof, "bench_trace.log")
-    if os.path.exists(log):
-        lines = [ln for ln in open(log) if ln.startswith("{")]
+        shutil.copy(stats[0], os.path.join(dst, f"{tag}_kernel_stats.csv"))
+    line = None
+    for name in ("bench_trace", "bench_fetch", "bench_write", "bench_sq"):
+        log = os.path.join(a.prof, f"{name}.log")
+        lines = [ln for ln in open(log) if ln.startswith("{")] if os.path.exists(log) else []
         if lines:
-            open(os.path.join(dst, f"{a.round}_bench_trace.json"), "w").write(lines[-1])
-    fetch_kb, nf = counter_per_dispatch(os.path.join(a.prof, "fetch"), "FETCH_SIZE")
-    write_kb, nw = counter_per_dispatch(os.path.join(a.prof, "write"), "WRITE_SIZE")
+            if name == "bench_trace":
+                open(os.path.join(dst, f"{tag}_bench_trace.json"), "w").write(lines[-1])
+            line = line or json.loads(lines[-1])
+    rf = line["roofline"]
+    lanes, spl, epl = rf["concurrent_launches"], int(rf["env_steps_per_launch"]), rf["envs_per_launch"]
+    n_timed = lanes * (-(-a.timed_steps // spl))  # dispatches of the timed window (the last ones)
+    unit = epl * spl  # env steps per dispatch
+    fetch = timed_mean(per_dispatch(os.path.join(a.prof, "fetch"), ["FETCH_SIZE"]), n_timed)["FETCH_SIZE"]
+    write = timed_mean(per_dispatch(os.path.join(a.prof, "write"), ["WRITE_SIZE"]), n_timed)["WRITE_SIZE"]
+    sq_names = ["SQ_WAVE_CYCLES", "SQ_WAVES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU",
+                "SQ_ACTIVE_INST_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_ANY"]
+    sq = timed_mean(per_dispatch(os.path.join(a.prof, "sq"), sq_names), n_timed)
+    waves_per_simd = 2  # 8 one-wave workgroups per CU (LDS- and VGPR-bound), 4 SIMDs
+    per_wave = sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_WAVE_CYCLES"]
+    hbm = 2.0 * fetch * 1024.0 + write * 1024.0
     rec = {
-        "kernel": KERNEL, "round": a.round,
-        "fetch_size_kb_raw": fetch_kb, "write_size_kb": write_kb, "dispatches": [nf, nw],
-        "fetch_bytes_corrected": 2.0 * fetch_kb * 1024.0, "write_bytes": write_kb * 1024.0,
-        "bytes_per_launch": 2.0 * fetch_kb * 1024.0 + write_kb * 1024.0,
-        "note": "FETCH_SIZE x2 (gfx950 wide-read tally); dword-per-lane reads are uncalibrated",
+        "kernel": KERNEL, "round": a.round, "source": f"profiles/{tag}_pmc.json (tools/profile.sh)",
+        "config": {"workload": line["config"]["workload"].split(":")[0].lower(), "envs_per_gpu": line["config"]["envs_per_gpu"],
+                   "env_steps_per_launch": spl, "lanes": lanes},
+        "timed_dispatches": n_timed, "env_steps_per_dispatch": unit,
+        "fetch_size_kb_raw": fetch, "write_size_kb": write,
+        "hbm_bytes_per_dispatch": hbm, "hbm_bytes_per_env_step": hbm / unit,
+        "fetch_bytes_per_env_step": 2.0 * fetch * 1024.0 / unit, "write_bytes_per_env_step": write * 1024.0 / unit,
+        "sq_per_dispatch": sq,
+        "valu": {"bound": "valu-issue", "active_inst_valu_per_wave_cycle": per_wave, "waves_per_simd": waves_per_simd,
+                 "frac": per_wave * waves_per_simd,
+                 "valu_insts_per_env_step": sq["SQ_INSTS_VALU"] / unit,
+                 "lds_bank_conflict_per_lds_active": sq["SQ_LDS_BANK_CONFLICT"] / max(sq["SQ_ACTIVE_INST_LDS"], 1.0),
+                 "wait_any_per_wave_cycle": sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"],
+                 "note": "SIMD VALU issue utilisation = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (per wave, same "
+                         "quad-cycle units) x resident waves per SIMD; 1.0 = the VALU issues every cycle"},
+        "note": "FETCH_SIZE x2 (gfx950 wide-read tally, MI355X_MICROARCH.md §HBM); dword-per-lane reads uncalibrated; "
+                "Infinity-Cache hits are counted by these memory-side counters",
     }
-    json.dump(rec, open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
-    json.dump(rec, open(os.path.join(dst, f"{a.round}_pmc_traffic.json"), "w"), indent=1)
-    print(json.dumps(rec))
+    if rec["config"]["workload"] not in ("c2", "c3", "c5"):
+        rec["config"]["workload"] = a.workload
+    json.dump(rec, open(os.path.join(dst, f"pmc_{a.workload}.json"), "w"), indent=1)
+    json.dump(rec, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
+    print(json.dumps({k: rec[k] for k in ("hbm_bytes_per_env_step", "valu")}))
 
 
 if __name__ == "__main__":
