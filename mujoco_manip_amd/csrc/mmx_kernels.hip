@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #define MMX_MODEL_QUAL static __constant__
 #include "mmx_model_gen.h"
 #include "mmx_device.h"
@@ -62,16 +64,25 @@ struct EnvSh {
   int conkey[MMX_MAXCON];
   // constraint rows in block format: a row touches at most two dof blocks (arm = 9 dofs,
   // cube k = 6 dofs); J[i][0..n0) holds block b0's columns, J[i][n0..n0+n1) block b1's;
-  // J doubles as the contact-sort scratch in collide_wave (rows are built after it)
-  // Rows past MMX_LDSEFC (a pile of contacts; ~5 % of C3 substeps) live in the env's HBM overflow
-  // block `ovf` (J rows, then D): lane-owned row q >= LDSEFC / 64 is always an HBM row.
+  // J doubles as the contact-sort scratch in collide_wave (rows are built after it).
+  // Rows come in aligned groups of 4: the equality / joint-limit rows (padded to a multiple of 4),
+  // then per contact its 4 BASIS rows (normal, tangent 1, tangent 2, torsion; rows the contact's
+  // condim does not use are zero rows).  MuJoCo's pyramid edges J_n +/- mu_k J_k are never
+  // stored: the solver forms them from the basis rows (2/3 of the storage and MFMA steps).
+  // Rows past MMX_LDSEFC (a pile of contacts) live in the env's HBM overflow block `ovf` (J rows,
+  // then D, then NC): lane-owned row q >= LDSEFC / 64 is always an HBM row.
   alignas(16) float J[MMX_LDSEFC][16];  // slots past the row's width = 0; slot 15 = the row's aref
   unsigned char hdr[MMX_MAXEFC];  // b0 | b1 << 4 (block 15 = none); row 0 is the equality
   // D: the row's 1 / R while the rows are built (doubling as the row -> contact map before) and in
-  // the solver's setup; then the Newton iterations' active weights s
+  // the solver's setup; then per Newton iteration the diagonal entry of the group's edge-weight
+  // matrix C (C_kk; a single row's active weight).  NC: C_nk, the row's coupling to its contact's
+  // normal row (0 for single and normal rows).
   float D[MMX_LDSEFC];
+  alignas(16) float NC[MMX_LDSEFC];
   float* ovf;  // this env's overflow rows (S.efc_ovf + i * MMX_OVF_F)
   int ncon, nefc, flags;
+  int nsingle;  // rows [0, nsingle): equality + limit rows (+ zero padding); contact groups after
+  int nefc_mj;  // MuJoCo's row count (pyramid edges + equality + limits), for the statistics
   int ncls[3];    // collision candidates per narrowphase class (plane, box-box, GJK)
   int tbase[11];  // rows are grouped by block-pair type: type t owns rows [tbase[t], tbase[t+1])
   int act_free;  // bit a: actuator a's force is inside its forcerange (its kv enters qDeriv)
@@ -118,12 +129,16 @@ DEV float* scr_of(EnvSh& E) { return &E.J[0][0]; }
 DEV float* obs_of(EnvSh& E) { return &E.J[0][0] + SCR_OBS; }
 DEV const float* obs_of(const EnvSh& E) { return &E.J[0][0] + SCR_OBS; }
 DEV float* lrow_of(EnvSh& E) { return &E.con[0][0]; }  // [27][27] Newton factor / staging tile
+// the rows' mu between the row build and the solver setup (E.con is dead once the rows exist)
+DEV float* mu_stage(EnvSh& E) { return &E.con[0][0]; }
+static_assert(MMX_MAXEFC <= MMX_MAXCON * CON_F, "row mu staging exceeds E.con");
 // Constraint row i: J in E.J[i] and D in E.D[i] for i < MMX_LDSEFC, else in the env's HBM
 // overflow block (J rows [OVFEFC][16], then D [OVFEFC]).  For a lane-owned row i = LANE + 64 q the
 // test folds at compile time (LANE's known bits), so the unrolled loops carry no branch.
 static_assert(MMX_LDSEFC % WG == 0 && MMX_LDSEFC <= MMX_MAXEFC, "LDS rows: whole lane slices");
 DEV float* ovf_j(const EnvSh& E, int i) { return E.ovf + 16 * (i - MMX_LDSEFC); }
 DEV float* ovf_d(const EnvSh& E, int i) { return E.ovf + 16 * MMX_OVFEFC + (i - MMX_LDSEFC); }
+DEV float* ovf_nc(const EnvSh& E, int i) { return E.ovf + 17 * MMX_OVFEFC + (i - MMX_LDSEFC); }
 DEV float4 jrow4(const EnvSh& E, int i, int q) {
   return i < MMX_LDSEFC ? reinterpret_cast<const float4*>(E.J[i])[q] : reinterpret_cast<const float4*>(ovf_j(E, i))[q];
 }
@@ -136,6 +151,11 @@ DEV float dget(const EnvSh& E, int i) { return i < MMX_LDSEFC ? E.D[i] : *ovf_d(
 DEV void dset(EnvSh& E, int i, float v) {
   if (i < MMX_LDSEFC) E.D[i] = v;
   else *ovf_d(E, i) = v;
+}
+DEV float ncget(const EnvSh& E, int i) { return i < MMX_LDSEFC ? E.NC[i] : *ovf_nc(E, i); }
+DEV void ncset(EnvSh& E, int i, float v) {
+  if (i < MMX_LDSEFC) E.NC[i] = v;
+  else *ovf_nc(E, i) = v;
 }
 // rows written by one lane and read by another: HBM rows need the wave's stores complete first
 // (workgroup scope = s_waitcnt vmcnt(0); the CU's L1 is shared by the wave).  Uniform branch.
@@ -904,26 +924,27 @@ DEV V3 contact_t1(V3 n) {  // mju_makeFrame's first tangent
   return normalize(y - n * dot(n, y));
 }
 
-// one pyramid row (rr) of contact c, built straight into block format: an arm block entry is
-// the motion subspace of dof d seen at the contact point, a cube block the free-body Jacobian
-DEV void contact_row(EnvSh& E, int row, int c, int rr) {
+// Basis row rr of contact c, built straight into block format: rr 0 = normal, 1 / 2 = tangents
+// t1 / t2 (mju_makeFrame), 3 = rotation about the normal (torsion, condim 4).  MuJoCo's pyramid
+// edges of the contact are J_n +/- mu_k J_k (k = t1, t2 with the sliding mu, torsion with the
+// torsional mu) and their aref = aref_n +/- mu_k aref_k with aref_k = -B J_k qvel (the position
+// term belongs to the normal); the solver forms them from these rows.  An arm block entry is the
+// motion subspace of dof d seen at the contact point, a cube block the free-body Jacobian.  Rows the
+// contact's condim does not use are zero rows with D = 0.  Returns the row's mu (-1: no edges).
+DEV float contact_row(EnvSh& E, int row, int c, int rr) {
   const float* cc = E.con[c];
   const V3 p = V3{cc[CON_POS], cc[CON_POS + 1], cc[CON_POS + 2]};
   const V3 n = V3{cc[CON_N], cc[CON_N + 1], cc[CON_N + 2]};
   const int dim = (int)cc[CON_DIM];
   const int b1 = (E.conkey[c] >> 16) & 255, b2 = (E.conkey[c] >> 24) & 255;
+  const bool used = rr == 0 || (rr < 3 && dim >= 3) || (rr == 3 && dim >= 4);
   const V3 t1 = contact_t1(n);
-  V3 u = n, w = V3{0.f, 0.f, 0.f};
+  const V3 u = rr == 0 ? n : (rr == 1 ? t1 : (rr == 2 ? cross(n, t1) : V3{0.f, 0.f, 0.f}));
+  const V3 w = rr == 3 ? n : V3{0.f, 0.f, 0.f};
+  // pyramidal cone: one R for every edge, the first edge's diagApprox (tran + mu0^2 tran) x
+  // 2 mu0^2 / impratio (impratio = 1; MuJoCo mj_makeImpedance, as in oracle/or_physics.c)
   float idiag = cc[CG_IT];  // impedance ratio x diagApprox
-  if (dim > 1) {  // pyramid edge J_n +/- mu_k J_k
-    const int k = rr >> 1;
-    const float mu = k < 2 ? cc[CON_MU0] : cc[CON_MU1];
-    const float sg = (rr & 1) ? -mu : mu;
-    if (k == 0) u = n + t1 * sg;
-    else if (k == 1) u = n + cross(n, t1) * sg;
-    else w = n * sg;
-    // pyramidal cone: one R for every edge, the first edge's diagApprox (tran + mu0^2 tran) x
-    // 2 mu0^2 / impratio (impratio = 1; MuJoCo mj_makeImpedance, as in oracle/or_physics.c)
+  if (dim > 1) {
     const float mu0 = cc[CON_MU0];
     idiag = 2.f * mu0 * mu0 * (cc[CG_IT] + mu0 * mu0 * cc[CG_IT]);
   }
@@ -980,23 +1001,28 @@ DEV void contact_row(EnvSh& E, int row, int c, int rr) {
     const float vc = j < 6 ? cubeA[j] : (j < 12 ? cubeB[j - 6] : 0.f);
     jv[j] = armrow ? va : vc;
   }
-  store_row(E, row, jv, rb0 | (rb1 << 4), vel, 1.f, cc[CG_KID], cc[CG_B], idiag);
+  store_row(E, row, jv, rb0 | (rb1 << 4), vel, 1.f, rr == 0 ? cc[CG_KID] : 0.f, cc[CG_B], idiag);
+  if (!used) dset(E, row, 0.f);  // (its J is zero as well: u = w = 0)
+  return !used || rr == 0 ? (rr == 0 ? 0.f : -1.f) : (rr < 3 ? cc[CON_MU0] : cc[CON_MU1]);
 }
 
 // Constraint rows in MuJoCo's order per lane scan: finger equality (lane 0), joint limits
-// (lanes 0..8), contact pyramids (lane c = contact c).  Equality and limit rows are written by
-// their lanes; contact rows are spread over all lanes through a row -> (contact, edge) map.
+// (lanes 0..8), contacts (lane c = contact c, 4 basis rows each).  Equality and limit rows are
+// written by their lanes; contact rows are spread over all lanes through a row -> (contact, basis
+// row) map.  Rows are grouped by block-pair type in aligned groups of 4 (type 0 starts with the
+// equality / limit rows, padded with zero rows to a multiple of 4); the rows' mu (the solver's
+// edge coefficients) are staged in E.con once every contact row is built.
 DEV void make_constraints_wave(EnvSh& E) {
   float* stats = E.stats;
   CLK_DECL;
   const float def_ref[2] = {0.02f, 1.0f};
   const float def_imp[5] = {0.9f, 0.95f, 0.001f, 0.5f, 2.0f};
   const int ncon = E.ncon;
-  // row -> (contact, pyramid edge) map, -1 for the equality / limit rows; it lives in the rows' D
-  // (dset / dget), so the equality / limit rows (whose store_row writes D) are stored after the
-  // contact rows
+  // row -> (contact, basis row) map, -1 for the equality / limit / padding rows; it lives in the
+  // rows' D (dset / dget), so the equality / limit rows (whose store_row writes D) are stored after
+  // the contact rows
   auto rowmap_set = [&](int r, int m) { dset(E, r, __int_as_float(m)); };
-  int nlim = 0, ncr = 0, dim = 0, tc = -1;
+  int nlim = 0, tc = -1, nedge = 0;
   bool lo_act = false, hi_act = false;
   if (LANE < 9) {
     const float q = E.qpos[LANE];
@@ -1005,8 +1031,8 @@ DEV void make_constraints_wave(EnvSh& E) {
     nlim = (int)lo_act + (int)hi_act;
   }
   if (LANE < ncon) {
-    dim = (int)E.con[LANE][CON_DIM];
-    ncr = dim == 1 ? 1 : 2 * (dim - 1);
+    const int dim = (int)E.con[LANE][CON_DIM];
+    nedge = dim == 1 ? 1 : 2 * (dim - 1);
     const int kb = E.conkey[LANE];
     const int k1 = body_block((kb >> 16) & 255), k2 = body_block((kb >> 24) & 255);
     int rb0 = k1 >= 0 ? k1 : k2, rb1 = (k1 >= 0 && k2 >= 0 && k2 != k1) ? k2 : BLK_NONE;
@@ -1017,19 +1043,21 @@ DEV void make_constraints_wave(EnvSh& E) {
     }
     tc = row_type(rb0, rb1);
   }
-  // rows grouped by block-pair type (type-major, lane order inside a type): equality + limits
-  // are arm-only rows (type 0) and come first in type 0
+  // single rows (equality + limits), then per type the contact groups
   const int acnt = (LANE == 0 ? 1 : 0) + nlim;
-  int arow = 0, brow = 0, base = 0;
-  // per-type prefix counts, three 10-bit fields per 32-bit scan (type totals <= MAXEFC < 1024)
+  const int aincl = wave_scan_incl(acnt);
+  const int nsingle_raw = __builtin_amdgcn_readlane(aincl, 63);
+  const int nsingle = (nsingle_raw + 3) & ~3;
+  const int arow = aincl - acnt;
+  int brow = 0, base = 0;
+  // per-type prefix counts of contact rows, three 10-bit fields per 32-bit scan (<= MAXEFC < 1024)
 #pragma unroll
   for (int t0 = 0; t0 < NTYPE; t0 += 3) {
     int packed = 0;
 #pragma unroll
     for (int f = 0; f < 3; f++) {
       const int t = t0 + f;
-      const int cnt = t < NTYPE ? (t == 0 ? acnt : 0) + (tc == t ? ncr : 0) : 0;
-      packed |= cnt << (10 * f);
+      packed |= (t < NTYPE && tc == t ? 4 : 0) << (10 * f);
     }
     const int incl = wave_scan_incl(packed);
     const int tot = __builtin_amdgcn_readlane(incl, 63);
@@ -1037,23 +1065,27 @@ DEV void make_constraints_wave(EnvSh& E) {
     for (int f = 0; f < 3; f++) {
       const int t = t0 + f;
       if (t >= NTYPE) break;
-      const int cnt = (t == 0 ? acnt : 0) + (tc == t ? ncr : 0);
+      const int cnt = tc == t ? 4 : 0;
       const int excl = ((incl >> (10 * f)) & 1023) - cnt;
-      if (t == 0) arow = base + excl;
-      if (tc == t) brow = base + excl + (t == 0 ? acnt : 0);
+      const int first = base + (t == 0 ? nsingle : 0);  // type 0: the single rows come first
+      if (tc == t) brow = first + excl;
       if (LANE == 0) E.tbase[t] = min(base, MMX_MAXEFC);
-      base += (tot >> (10 * f)) & 1023;
+      base = first + ((tot >> (10 * f)) & 1023);
     }
   }
   const int total = base;
   const int nefc = min(total, MMX_MAXEFC);
+  const int nefc_mj = nsingle_raw + (int)wave_sum((float)nedge);
   if (LANE == 0) {
     E.tbase[NTYPE] = nefc;
     E.nefc = nefc;
+    E.nefc_mj = nefc_mj;
+    E.nsingle = nsingle;
     if (total > MMX_MAXEFC) E.flags |= SHF_EFC_OVF;
   }
-  int row = arow;
   PROBE(3, stats, STAT_T_AUX0);
+  if (LANE < 4 && nsingle_raw + LANE < nsingle) rowmap_set(nsingle_raw + LANE, -1);  // padding
+  int row = arow;
   if (LANE == 0 && row < MMX_MAXEFC) rowmap_set(row++, -1);  // finger equality
   if (LANE < 9) {
 #pragma unroll
@@ -1076,14 +1108,23 @@ DEV void make_constraints_wave(EnvSh& E) {
     c[CG_IT] = impr * tran;  // (the pyramid's common R needs only the translational invweight)
     c[CG_KID] = kid;
     c[CG_B] = B;
-    for (int rr = 0; rr < ncr && brow + rr < MMX_MAXEFC; rr++) rowmap_set(brow + rr, LANE | (rr << 8));
+#pragma unroll
+    for (int rr = 0; rr < 4; rr++)
+      if (brow + rr < MMX_MAXEFC) rowmap_set(brow + rr, LANE | (rr << 8));
   }
   ovf_fence(nefc);
   SYNC();
   PROBE(3, stats, STAT_T_AUX3);
-  for (int r = LANE; r < nefc; r += WG) {
-    const int m = __float_as_int(dget(E, r));
-    if (m >= 0) contact_row(E, r, m & 255, m >> 8);
+  constexpr int RPB = (MMX_MAXEFC + WG - 1) / WG;
+  float mu[RPB];
+#pragma unroll
+  for (int q = 0; q < RPB; q++) {
+    const int r = LANE + WG * q;
+    mu[q] = 0.f;
+    if (r < nefc) {
+      const int m = __float_as_int(dget(E, r));
+      if (m >= 0) mu[q] = contact_row(E, r, m & 255, m >> 8);
+    }
   }
   row = arow;
   float jv[16];
@@ -1113,7 +1154,17 @@ DEV void make_constraints_wave(EnvSh& E) {
       }
     }
   }
+  if (LANE < 4 && nsingle_raw + LANE < nsingle) {  // zero padding rows (weight 0)
+#pragma unroll
+    for (int j = 0; j < 16; j++) jv[j] = 0.f;
+    store_row(E, nsingle_raw + LANE, jv, 0 | (BLK_NONE << 4), 0.f, 1.f, 0.f, 0.f, 1.f);
+    dset(E, nsingle_raw + LANE, 0.f);
+  }
   ovf_fence(nefc);
+  SYNC();  // every contact row is built: E.con is dead, the rows' mu go there for the solver setup
+#pragma unroll
+  for (int q = 0; q < RPB; q++)
+    if (LANE + WG * q < nefc) mu_stage(E)[LANE + WG * q] = mu[q];
   SYNC();
   PROBE(3, stats, STAT_T_AUX2);
 }
@@ -1173,11 +1224,42 @@ DEV float mass_mul_diff(const EnvSh& E, const float* xa, const float* xb) {
   return LANE < 27 ? E.Mc[LANE - 9] * (xa[LANE] - xb[LANE]) : 0.f;
 }
 
+// Pyramid edges from basis rows.  Lane l owns rows l + 64 q; rows are 4-aligned groups, so a
+// group's rows sit in one DPP quad (lanes 4m..4m+3).  A row's role: single (equality / limit /
+// padding row: one edge, itself), normal row of a contact (no edge of its own), basis row k >= 1 of
+// a contact (the two edges J_n +/- mu_k J_k; mu < 0: unused row, no edge).  Edge e of the lane's
+// row is a_e (normal row value) + b_e (own value), for residuals and for J p alike.
+struct EdgeCoef {
+  float a0, b0, a1, b1;  // edge 0: a0 n + b0 own, edge 1: a1 n + b1 own; all 0 for a missing edge
+};
+// (no boolean per edge: a missing edge has zero coefficients, so its value is 0 and never
+// active; only the finger equality, row 0 = lane 0 of slice 0, is active at any sign)
+DEV EdgeCoef edge_coef(int i, int nefc, int nsingle, float mu) {
+  EdgeCoef c;
+  const bool valid = i < nefc;
+  const bool single = valid && i < nsingle;
+  const bool krow = valid && !single && (i & 3) != 0 && mu >= 0.f;
+  c.a0 = krow ? 1.f : 0.f;
+  c.b0 = krow ? mu : (single ? 1.f : 0.f);
+  c.a1 = c.a0;
+  c.b1 = krow ? -mu : 0.f;
+  return c;
+}
+// the finger equality row (always active): row 0, owned by lane 0 in slice 0
+#define EQROW(q) ((q) == 0 && LANE == 0)
+// value held by the first lane of the caller's DPP quad (the group's normal row)
+DEV float quad_first(float v) { return dpp_f<0x00>(v); }  // quad_perm [0,0,0,0]
+DEV float quad_sum(float v) {
+  v += dpp_f<0xB1>(v);  // quad_perm [1,0,3,2]
+  return v + dpp_f<0x4E>(v);  // quad_perm [2,3,0,1]
+}
+
 // cost at two candidate points (warm start, qacc_smooth) in one pass; also returns, per lane,
-// the row residuals J x - aref of the rows it owns and (M (x - xs))_lane for both candidates, so
-// the Newton loop starts from them and then only updates them (r += a J p, M dx += a M p)
-DEV void cost2_wave(const EnvSh& E, const float* xa, const float* xb, float& ca, float& cb, float* va, float* vb,
-                    float& ma, float& mb) {
+// the basis-row residuals J x - aref of the rows it owns and (M (x - xs))_lane for both
+// candidates, so the Newton loop starts from them and then only updates them (r += a J p,
+// M dx += a M p).  Edge cost 0.5 D e^2 on active edges (e < 0, or the equality).
+DEV void cost2_wave(const EnvSh& E, const float* xa, const float* xb, const float* mu, const float* dd, float& ca,
+                    float& cb, float* va, float* vb, float& ma, float& mb) {
   float c0 = 0.f, c1 = 0.f;
   ma = 0.f;
   mb = 0.f;
@@ -1187,36 +1269,45 @@ DEV void cost2_wave(const EnvSh& E, const float* xa, const float* xb, float& ca,
     c0 = 0.5f * (xa[LANE] - E.qacc_s[LANE]) * ma;
     c1 = 0.5f * (xb[LANE] - E.qacc_s[LANE]) * mb;
   }
+  const int nefc = E.nefc, nsingle = E.nsingle;
 #pragma unroll
   for (int q = 0; q < RPL; q++) {
     const int i = LANE + WG * q;
     va[q] = 0.f;
     vb[q] = 0.f;
-    if (i < E.nefc) {
-      const bool eq = i == 0;  // row 0: the finger equality
+    if (WG * q >= nefc) continue;  // uniform: the slice holds no row
+    if (i < nefc) {
       const float aref = jget(E, i, 15);
       va[q] = row_dot16(E, i, xa) - aref;
       vb[q] = row_dot16(E, i, xb) - aref;
-      const float D = dget(E, i);
-      if (eq || va[q] < 0.f) c0 += 0.5f * D * va[q] * va[q];
-      if (eq || vb[q] < 0.f) c1 += 0.5f * D * vb[q] * vb[q];
     }
+    const float na = quad_first(va[q]), nb = quad_first(vb[q]);
+    const EdgeCoef ec = edge_coef(i, nefc, nsingle, mu[q]);
+    const float ea0 = fmaf(ec.a0, na, ec.b0 * va[q]), ea1 = fmaf(ec.a1, na, ec.b1 * va[q]);
+    const float eb0 = fmaf(ec.a0, nb, ec.b0 * vb[q]), eb1 = fmaf(ec.a1, nb, ec.b1 * vb[q]);
+    const float h = 0.5f * dd[q];
+    c0 += (EQROW(q) || ea0 < 0.f ? h * ea0 * ea0 : 0.f) + (ea1 < 0.f ? h * ea1 * ea1 : 0.f);
+    c1 += (EQROW(q) || eb0 < 0.f ? h * eb0 * eb0 : 0.f) + (eb1 < 0.f ? h * eb1 * eb1 : 0.f);
   }
   ca = wave_sum(c0);
   cb = wave_sum(c1);
 }
 
 // J'WJ and J'W r on the matrix cores, one block-pair row type at a time.  Rows of a type share
-// their slot -> dof map, so in slot space the type's contribution is a 16 x 16 tile
-// G = sum_k J_k' [w_k J_k | w_k r_k]: v_mfma_f32_16x16x4_f32 with A[slot i][row k] = J[k][i] and
-// B[row k][slot j] = w_k J[k][j], where slot 15 (always 0 in J) carries w_k r_k instead, so
-// G[:, 15] is the type's gradient.  Lane l supplies J[row + (l >> 4)][l & 15] for both operands:
-// a contiguous read of the block-format rows.  Each tile is staged in LDS and gathered by the
+// their slot -> dof map, so in slot space the type's contribution is a 16 x 16 tile.  Over the
+// pyramid edges J_e = c_e' B of a 4-row group B (c_e = e_n +/- mu_k e_k), sum_e w_e J_e' J_e =
+// B' C B with the group's 4 x 4 edge-weight matrix C = sum_e w_e c_e c_e' (an arrow: C_nn, C_nk,
+// C_kk), and sum_e w_e r_e J_e' = B' g.  So G = sum_groups B' [C B | g]:
+// v_mfma_f32_16x16x4_f32 with A[slot i][row k] = B[k][i] and B-operand[row k][slot j] =
+// (C B)[k][j] = C_kk B[k][j] + (k == n ? sum_m C_nm B[m][j] : C_nk B[n][j]), where slot 15
+// (always 0 in J) carries g_k instead, so G[:, 15] is the type's gradient.  Single rows form
+// groups with a diagonal C (their active weights).  Lane l supplies row (l >> 4) of the step's
+// group at slot l & 15: contiguous reads of the block-format rows.  Each tile is staged in LDS and gathered by the
 // dof lanes into their Hessian row (static columns) and gradient.  Returns, in lane j < 27,
 // row j of H = M + J'WJ in hrow[0..27) and g_j = (M (x - xs) + J'W r)_j.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 #ifndef MMX_HESS_U
-#define MMX_HESS_U 1  // measured: 1 step per trip +0.6 %, 4 steps -3.5 % vs 2 (C3)
+#define MMX_HESS_U 2  // groups (MFMA steps) per trip, their loads issued together
 #endif
 DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
   float* stats = E.stats;
@@ -1233,32 +1324,61 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
     const int r0 = E.tbase[t], r1 = E.tbase[t + 1];
     if (r1 <= r0) continue;
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-    // MMX_HESS_U MFMA steps (4 rows each) per trip, loads first; the steps alternate between the
-    // two accumulators, so each sums the same row groups in the same order for any MMX_HESS_U
-    for (int s0 = r0; s0 < r1; s0 += 4 * MMX_HESS_U) {
-      const bool all_lds = s0 + 4 * MMX_HESS_U <= MMX_LDSEFC;  // uniform: the trip's rows are all LDS rows
-      float jv[MMX_HESS_U], w[MMX_HESS_U];
-      bool valid[MMX_HESS_U];
+    // MMX_HESS_U MFMA steps (one 4-row group each) per trip, loads first; the steps alternate
+    // between the two accumulators, so each sums the same groups in the same order for any
+    // MMX_HESS_U.  Types span whole groups (tbase and MMX_LDSEFC are multiples of 4), so every step
+    // is full.  The LDS groups and the (rare) HBM overflow groups run in separate loops: one
+    // address space per loop, no generic (flat) loads in the hot one.
+    const float m_[4] = {rk == 0 ? 1.f : 0.f, rk == 1 ? 1.f : 0.f, rk == 2 ? 1.f : 0.f, rk == 3 ? 1.f : 0.f};
+    const float c15 = col == 15 ? 1.f : 0.f;  // slot 15 carries g, not C B
+    auto groups = [&](auto from_lds, int g_begin, int g_end) {
+      constexpr bool LDS = decltype(from_lds)::value;
+      for (int s0 = g_begin; s0 < g_end; s0 += 4 * MMX_HESS_U) {
+        float a[MMX_HESS_U], b[MMX_HESS_U];
+        float jg_[MMX_HESS_U][4], nc_[MMX_HESS_U][4], dr_[MMX_HESS_U];
 #pragma unroll
-      for (int u = 0; u < MMX_HESS_U; u++) {
-        const int r = s0 + 4 * u + rk;
-        valid[u] = r < r1;
-        const int rc = valid[u] ? r : r0;
-        if (all_lds) {
-          jv[u] = E.J[rc][col];  // slot 15 holds w r
-          w[u] = E.D[rc];        // active weight s
-        } else {
-          jv[u] = jget(E, rc, col);
-          w[u] = dget(E, rc);
+        for (int u = 0; u < MMX_HESS_U; u++) {
+          const int g0 = min(s0 + 4 * u, g_end - 4), r = g0 + rk;
+          if (LDS) {
+            const float4 n4 = *reinterpret_cast<const float4*>(&E.NC[g0]);  // one broadcast read
+            nc_[u][0] = n4.x; nc_[u][1] = n4.y; nc_[u][2] = n4.z; nc_[u][3] = n4.w;
+#pragma unroll
+            for (int m = 0; m < 4; m++) jg_[u][m] = E.J[g0 + m][col];  // slot 15 holds g
+            dr_[u] = E.D[r];
+          } else {
+#pragma unroll
+            for (int m = 0; m < 4; m++) {
+              jg_[u][m] = ovf_j(E, g0 + m)[col];
+              nc_[u][m] = *ovf_nc(E, g0 + m);
+            }
+            dr_[u] = *ovf_d(E, r);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < MMX_HESS_U; u++) {
+          // arithmetic selects over the lane's row rk (0 / 1 masks): no divergent branches
+          const float live = s0 + 4 * u < g_end ? 1.f : 0.f;  // uniform
+          const float* jg = jg_[u];
+          const float* nc = nc_[u];
+          const float own = fmaf(m_[0], jg[0], fmaf(m_[1], jg[1], fmaf(m_[2], jg[2], m_[3] * jg[3])));
+          const float ncr = fmaf(m_[1], nc[1], fmaf(m_[2], nc[2], m_[3] * nc[3]));  // C_nk of row rk (0 for n)
+          const float s123 = fmaf(nc[1], jg[1], fmaf(nc[2], jg[2], nc[3] * jg[3]));
+          const float cpl = fmaf(ncr, jg[0], m_[0] * s123);
+          a[u] = live * own;  // (slot 15 only feeds G's unused row 15)
+          b[u] = live * fmaf(c15, own - fmaf(dr_[u], own, cpl), fmaf(dr_[u], own, cpl));
+        }
+#pragma unroll
+        for (int u = 0; u < MMX_HESS_U; u++) {
+          if (u & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[u], acc1, 0, 0, 0);
+          else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[u], acc0, 0, 0, 0);
         }
       }
-#pragma unroll
-      for (int u = 0; u < MMX_HESS_U; u++) {
-        const float a = valid[u] ? jv[u] : 0.f;  // (slot 15 only feeds G's unused row 15)
-        const float b = valid[u] ? (col == 15 ? jv[u] : w[u] * jv[u]) : 0.f;
-        if (u & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc1, 0, 0, 0);
-        else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc0, 0, 0, 0);
-      }
+    };
+    const int split = min(max(r0, MMX_LDSEFC), r1);
+    groups(std::true_type{}, r0, split);
+    if (split < r1) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the overflow rows' stores (ovf_fence)
+      groups(std::false_type{}, split, r1);
     }
     PROBE(6, stats, STAT_T_AUX0);
     // stage: lane l holds G[4 (l >> 4) + q][l & 15]
@@ -1417,22 +1537,27 @@ DEV float chol_solve_arrow(EnvSh& E, const float* hrow, float v, int cpl) {
 DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
   float* stats = E.stats;
   CLK_DECL;
-  const int nefc = E.nefc;
+  const int nefc = E.nefc, nsingle = E.nsingle;
+  // per owned row: D (1/R; the contact's common pyramid R), mu (staged in E.con by the row build,
+  // read before the Hessian staging tile reuses E.con) and the edge coefficients
+  float dd[RPL], mu[RPL];
+#pragma unroll
+  for (int q = 0; q < RPL; q++) {
+    const int i = LANE + WG * q;
+    dd[q] = i < nefc ? dget(E, i) : 0.f;
+    mu[q] = i < nefc ? mu_stage(E)[i] : 0.f;
+  }
   // start from the cheaper of the warm start and qacc_smooth (as MuJoCo does)
   float c_ws, c_s, ra[RPL], rs[RPL], mws, ms;
-  cost2_wave(E, E.ws, E.qacc_s, c_ws, c_s, ra, rs, mws, ms);
+  cost2_wave(E, E.ws, E.qacc_s, mu, dd, c_ws, c_s, ra, rs, mws, ms);
   const bool from_ws = c_ws < c_s;
   if (LANE < 27) E.x[LANE] = from_ws ? E.ws[LANE] : E.qacc_s[LANE];
   float mdx = from_ws ? mws : ms;  // (M (x - xs))_lane, kept current through the iterations
   float scale = LANE < 27 ? E.qfrc[LANE] * E.qfrc[LANE] : 0.f;
   scale = sqrtf(wave_sum(scale)) + 1.f;
-  float rr[RPL], jp[RPL], dd[RPL];
-  bool eq[RPL];
+  float rr[RPL], jp[RPL];  // basis-row residuals J x - aref and J p
 #pragma unroll
   for (int q = 0; q < RPL; q++) {
-    const int i = LANE + WG * q;
-    dd[q] = i < nefc ? dget(E, i) : 0.f;
-    eq[q] = i == 0;  // row 0: the finger equality (always present)
     rr[q] = from_ws ? ra[q] : rs[q];
     jp[q] = 0.f;
   }
@@ -1445,15 +1570,28 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
   resid = 0.f;
   PROBE(1, stats, STAT_T_AUX3);
   for (; it < max_iter; it++) {
-    // active weights s and w r of the current residuals (LDS copies feed the MFMA pass)
+    // per group: the edge-weight matrix C (C_kk -> D, C_nk -> NC) and g = sum_e w_e r_e c_e
+    // (-> slot 15), from the active edges of the current residuals; a contact's normal row
+    // collects its edges' normal parts over the DPP quad
 #pragma unroll
     for (int q = 0; q < RPL; q++) {
+      if (WG * q >= nefc) break;  // uniform: no rows past this slice
       const int i = LANE + WG * q;
+      const EdgeCoef ec = edge_coef(i, nefc, nsingle, mu[q]);
+      const float rn = quad_first(rr[q]);
+      const float e0 = fmaf(ec.a0, rn, ec.b0 * rr[q]), e1 = fmaf(ec.a1, rn, ec.b1 * rr[q]);
+      const float w0 = EQROW(q) || e0 < 0.f ? dd[q] : 0.f;  // (missing edges: coefficients 0)
+      const float w1 = e1 < 0.f ? dd[q] : 0.f;
+      const float ckk = fmaf(w0 * ec.b0, ec.b0, w1 * ec.b1 * ec.b1);
+      const float cnk = fmaf(w0 * ec.a0, ec.b0, w1 * ec.a1 * ec.b1);
+      const float gk = fmaf(w0 * e0, ec.b0, w1 * e1 * ec.b1);
+      const float cnn = quad_sum(fmaf(w0 * ec.a0, ec.a0, w1 * ec.a1 * ec.a1));
+      const float gn = quad_sum(fmaf(w0 * e0, ec.a0, w1 * e1 * ec.a1));
+      const bool nrow = i >= nsingle && (i & 3) == 0;
       if (i < nefc) {
-        const float v = rr[q];
-        const float w = (eq[q] || v < 0.f) ? dd[q] : 0.f;
-        jset(E, i, 15, w * v);  // w r for the gradient (the row's aref slot is dead after the setup)
-        dset(E, i, w);          // s (D itself is in registers since the setup)
+        jset(E, i, 15, nrow ? gn : gk);  // g for the gradient (the row's aref slot is dead after the setup)
+        dset(E, i, nrow ? cnn : ckk);    // C diagonal (D itself is in registers since the setup)
+        ncset(E, i, nrow ? 0.f : cnk);
       }
     }
     ovf_fence(nefc);
@@ -1467,15 +1605,26 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
     const float pj = chol_solve_arrow(E, hrow, -g, cpl);
     if (LANE < 27) E.p[LANE] = pj;
     SYNC();
-    float hp = 0.f;  // (H p)_lane: the gradient's change per unit step while no row changes state
+    float hp = 0.f;  // (H p)_lane: the gradient's change per unit step while no edge changes state
 #pragma unroll
     for (int m = 0; m < 27; m++) hp = fmaf(hrow[m], E.p[m], hp);
     PROBE(1, stats, STAT_T_AUX2);
-    // exact line search on phi(a) = cost(x + a p): phi' is piecewise linear and increasing
+    // exact line search on phi(a) = cost(x + a p): phi' is piecewise linear and increasing; per
+    // owned row its (up to two) edges e(a) = e + a je
+    float e0[RPL], e1[RPL], j0[RPL], j1[RPL];
 #pragma unroll
     for (int q = 0; q < RPL; q++) {
+      e0[q] = e1[q] = j0[q] = j1[q] = 0.f;
+      jp[q] = 0.f;
+      if (WG * q >= nefc) continue;  // uniform: the slice holds no row
       const int i = LANE + WG * q;
       jp[q] = i < nefc ? row_dot16(E, i, E.p) : 0.f;
+      const EdgeCoef ec = edge_coef(i, nefc, nsingle, mu[q]);
+      const float rn = quad_first(rr[q]), pn = quad_first(jp[q]);
+      e0[q] = fmaf(ec.a0, rn, ec.b0 * rr[q]);
+      e1[q] = fmaf(ec.a1, rn, ec.b1 * rr[q]);
+      j0[q] = fmaf(ec.a0, pn, ec.b0 * jp[q]);
+      j1[q] = fmaf(ec.a1, pn, ec.b1 * jp[q]);
     }
     PROBE(10, stats, STAT_T_AUX0);
     float c0 = 0.f, c1 = 0.f, mp = 0.f;
@@ -1493,10 +1642,12 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
       float d1 = 0.f, d2 = 0.f;
 #pragma unroll
       for (int q = 0; q < RPL; q++) {
-        const float v = fmaf(alpha, jp[q], rr[q]);
-        const float dj = (eq[q] || v < 0.f) ? dd[q] * jp[q] : 0.f;
-        d1 = fmaf(dj, v, d1);
-        d2 = fmaf(dj, jp[q], d2);
+        if (WG * q >= nefc) break;  // uniform
+        const float a0 = fmaf(alpha, j0[q], e0[q]), a1 = fmaf(alpha, j1[q], e1[q]);
+        const float s0 = EQROW(q) || a0 < 0.f ? dd[q] * j0[q] : 0.f;
+        const float s1 = a1 < 0.f ? dd[q] * j1[q] : 0.f;
+        d1 = fmaf(s0, a0, fmaf(s1, a1, d1));
+        d2 = fmaf(s0, j0[q], fmaf(s1, j1[q], d2));
       }
       d1 = wave_sum(d1) + c0 + alpha * c1;
       d2 = wave_sum(d2) + c1;
@@ -1518,12 +1669,14 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
       stepn = alpha * alpha * pj * pj;
     }
     mdx = fmaf(alpha, mp, mdx);
-    bool flip = false;  // a row changed active state over the step
+    bool flip = false;  // an edge changed active state over the step
 #pragma unroll
     for (int q = 0; q < RPL; q++) {
-      const float v = fmaf(alpha, jp[q], rr[q]);
-      flip |= !eq[q] && ((v < 0.f) != (rr[q] < 0.f));
-      rr[q] = v;
+      if (WG * q >= nefc) break;  // uniform
+      const float a0 = fmaf(alpha, j0[q], e0[q]), a1 = fmaf(alpha, j1[q], e1[q]);
+      flip |= !EQROW(q) && ((a0 < 0.f) != (e0[q] < 0.f));
+      flip |= (a1 < 0.f) != (e1[q] < 0.f);
+      rr[q] = fmaf(alpha, jp[q], rr[q]);
     }
     SYNC();
     stepn = sqrtf(wave_sum(stepn));
@@ -1799,17 +1952,17 @@ DEV void mj_step_wave(int max_iter, float tol, EnvSh& E, float* con_dst) {
   integrate_wave(E);
   CLK(stats, STAT_T_INT);
   if (LANE == 0) {
-    stats[STAT_NEFC] += (float)E.nefc;
+    stats[STAT_NEFC] += (float)E.nefc_mj;  // MuJoCo's rows (pyramid edges), not the stored basis rows
     stats[STAT_NCON] += (float)E.ncon;
     stats[STAT_SOLVER_ITER] += (float)it;
     stats[STAT_SUBSTEPS] += 1.f;
     stats[STAT_RESID] = fmaxf(stats[STAT_RESID], resid);
 #ifdef MMX_PHASE_CLOCK
     if (MMX_PROBE == 12) {  // row / contact count distribution (sizes the LDS row capacity)
-      stats[STAT_T_AUX0] = fmaxf(stats[STAT_T_AUX0], (float)E.nefc);
+      stats[STAT_T_AUX0] = fmaxf(stats[STAT_T_AUX0], (float)E.nefc);  // stored (basis) rows
       stats[STAT_T_AUX1] = fmaxf(stats[STAT_T_AUX1], (float)E.ncon);
-      stats[STAT_T_AUX2] += E.nefc > 192 ? 1.f : 0.f;
-      stats[STAT_T_AUX3] += E.nefc > 224 ? 1.f : 0.f;
+      stats[STAT_T_AUX2] += E.nefc > MMX_LDSEFC ? 1.f : 0.f;
+      stats[STAT_T_AUX3] += E.nefc > 160 ? 1.f : 0.f;
     }
 #endif
   }
@@ -2202,6 +2355,7 @@ DEV void load_env(const MMXState& S, int i, EnvSh& E) {
     E.flags = 0;
     E.ncon = 0;
     E.nefc = 0;
+    E.nefc_mj = 0;
   }
   SYNC();
 }
@@ -2273,7 +2427,7 @@ DEV void step_end(const MMXState& S, int i, EnvSh& E) {
   // mj_forward position stage (gym_env.py:560): kinematics + contacts for the staged penalty
   if (LANE == 0) {
     EPI(EPI_NCON) = E.ncon;
-    EPI(EPI_NEFC) = E.nefc;
+    EPI(EPI_NEFC) = E.nefc_mj;
   }
   kinematics_wave(E);
   if (S.reward_type == 2) collide_wave(E, true);
@@ -2337,7 +2491,7 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_substep_kernel(MMXState S, 
       fold_flags(S, i, E);
       if (mode & SS_LAST) {
         EPI(EPI_NCON) = E.ncon;
-        EPI(EPI_NEFC) = E.nefc;
+        EPI(EPI_NEFC) = E.nefc_mj;
       }
     }
   }
@@ -2412,7 +2566,7 @@ __device__ __attribute__((MMX_SUBSTEP_ATTR)) void substep(int max_iter, float to
     integrate_wave(E);
     CLK(stats, STAT_T_INT);
     if (LANE == 0) {
-      stats[STAT_NEFC] += (float)E.nefc;
+      stats[STAT_NEFC] += (float)E.nefc_mj;
       stats[STAT_NCON] += (float)E.ncon;
       stats[STAT_SOLVER_ITER] += (float)it;
       stats[STAT_SUBSTEPS] += 1.f;

@@ -14,14 +14,15 @@
 #define MMX_NU_ 8
 #define MMX_NOBS 85
 #define MMX_MAXCON 64
-#define MMX_MAXEFC 384
+// constraint rows (basis rows: 4 per contact + equality / limits padded to 4; <= 64 x 4 + 20)
+#define MMX_MAXEFC 320
 // constraint rows [0, MMX_LDSEFC) live in the workgroup's LDS, rows [MMX_LDSEFC, MMX_MAXEFC) in the
 // env's HBM overflow block (efc_ovf); 192 rows keep the env's LDS under 20 KB (8 envs per CU)
 #ifndef MMX_LDSEFC
 #define MMX_LDSEFC 192
 #endif
 #define MMX_OVFEFC (MMX_MAXEFC - MMX_LDSEFC)
-#define MMX_OVF_F (MMX_OVFEFC * 17)  // floats per env: J rows [OVFEFC][16], then D [OVFEFC]
+#define MMX_OVF_F (MMX_OVFEFC * 18)  // floats per env: J rows [OVFEFC][16], then D, NC [OVFEFC]
 #define MMX_NSUBSTEP 16
 
 // stale kinematics cache read by the IK (controller.py:99-108 reads data.xpos / mj_jac
