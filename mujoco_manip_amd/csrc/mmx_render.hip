@@ -1,14 +1,17 @@
 // Batched camera renderer for gfx950: the overhead and wrist images of
 // PickPlaceGymEnv's observation (gym_env.py:295-339 via cameras.py:9-53, mujoco.Renderer).
 //
-// One workgroup (512 lanes) renders one horizontal band (8192 px) of one camera image of one env:
+// One workgroup (512 lanes) renders one horizontal band (up to 8192 px) of one camera image of one
+// env (two workgroups per CU: one shades while the other sets up):
 //   1. body poses of the env (stored by the step / reset / forward kernels in S.rpose) and the
 //      camera pose (overhead: fixed; wrist: on the hand, env.py:52-65) -> LDS;
 //   2. all render vertices (tools/compile_render.py: floor grid, table / bins / cubes as boxes
-//      and prisms, each Panda body as the hull of its visual meshes) to camera space -> LDS;
-//   3. triangles, one lane each: near cull, projection (MuJoCo pinhole, fovy, row 0 at the top),
-//      back-face cull, bounding box clipped to the band, into one of two LDS queues by box
-//      area.  Small boxes (<= 256 px) are scanned by 16-lane groups, one triangle per group
+//      and prisms, each Panda body as the hull of its visual meshes) to camera space and, once
+//      per vertex, to the screen (MuJoCo pinhole, fovy, row 0 at the top) -> LDS (screen x, y,
+//      1 / depth: the camera-space point is recovered from them where the shading needs it);
+//   3. triangles, one lane each: near cull, back-face cull, bounding box clipped to the band,
+//      into one of two LDS queues by box
+//      area.  Small boxes (<= 2048 px) are scanned by 16-lane groups, one triangle per group
 //      (every lane of a wave busy however the box sizes vary); large ones (floor tiles, table top)
 //      by the whole workgroup, pixel-parallel.  Depth test = one 32-bit LDS atomicMax per covered pixel on
 //      (inverse depth quantised over the camera's depth range : 20 bits | triangle : 12 bits);
@@ -38,21 +41,29 @@
 #define RNSLOT 14
 static_assert(MMR_NTRI <= 4096, "triangle index must fit the 12-bit depth-key field");
 #ifndef MMR_BAND_PX
-#define MMR_BAND_PX 8192
+#define MMR_BAND_PX 8192  // 32 KB z-buffer: LDS for two workgroups per CU
 #endif
 #ifndef MMR_SMALL_AREA
-#define MMR_SMALL_AREA 256
+#define MMR_SMALL_AREA 2048  // measured: 256 -> 2048 px boxes on 16-lane groups, -8 % render time (4096: +9 %)
 #endif
-static constexpr int kBandPx = MMR_BAND_PX;      // z-buffer pixels per band (32 KB of LDS)
+static constexpr int kBandPx = MMR_BAND_PX;      // z-buffer pixels per band
 static constexpr int kSmallArea = MMR_SMALL_AREA; // bounding boxes up to this many pixels: a 16-lane group
-static constexpr int kGroup = 16;                // lanes per small triangle
+#ifndef MMR_GROUP
+#define MMR_GROUP 16
+#endif
+static constexpr int kGroup = MMR_GROUP;         // lanes per small triangle
 static constexpr int kMaxBig = 1024;
 
-DEV int rend_band_rows(int S) { return kBandPx / S < S ? kBandPx / S : S; }
+// rows per band: the image split into the fewest bands that fit the z-buffer, balanced
+__host__ DEV int rend_band_rows(int S) {
+  const int nb = (S * S + kBandPx - 1) / kBandPx;
+  return (S + nb - 1) / nb;
+}
 
 struct RTri {  // screen-space setup of one triangle
   float x0, y0, x1, y1, x2, y2;  // pixel coordinates
   float iz0, iz1, iz2;           // 1 / depth
+  float inv;                     // 1 / (e0 + e1 + e2): the edge functions sum to twice the area
   int i0, i1, i2;                // vertex ids: shared edges are evaluated in one canonical order
   int bx0, by0, bx1, by1;        // pixel bbox (inclusive), clipped to the band
 };
@@ -68,28 +79,34 @@ DEV float rend_edge(float xa, float ya, int ia, float xb, float yb, int ib, floa
   return fwd ? e : -e;
 }
 
-// camera-space vertex -> screen; false if behind the near plane
-DEV bool rend_project(float4 c, float f, float half, float znear, float& sx, float& sy, float& iz) {
+// camera-space vertex -> screen (sx, sy, 1 / depth, 1) or (0, 0, 0, 0) behind the near plane
+DEV float4 rend_project(float4 c, float f, float half, float znear) {
   const float d = -c.z;
-  if (d < znear) return false;
-  iz = 1.f / d;
-  sx = half + f * c.x * iz;
-  sy = half - f * c.y * iz;
-  return true;
+  if (d < znear) return make_float4(0.f, 0.f, 0.f, 0.f);
+  const float iz = 1.f / d;
+  return make_float4(half + f * c.x * iz, half - f * c.y * iz, iz, 1.f);
 }
 
-DEV bool rend_setup(const float4* vc, int t, float f, float half, float znear, int S, int row0, int row1,
-                    RTri& T) {
+// the camera-space point of a projected vertex (inverse of rend_project)
+DEV float4 rend_unproject(float sx, float sy, float iz, float f, float half) {
+  const float d = 1.f / iz;
+  return make_float4((sx - half) * d / f, (half - sy) * d / f, -d, 0.f);
+}
+
+DEV bool rend_setup(const float4* vs, int t, int S, int row0, int row1, RTri& T) {
   const int a = MMR_tri[3 * t], b = MMR_tri[3 * t + 1], c = MMR_tri[3 * t + 2];
   T.i0 = a;
   T.i1 = b;
   T.i2 = c;
-  if (!rend_project(vc[a], f, half, znear, T.x0, T.y0, T.iz0)) return false;
-  if (!rend_project(vc[b], f, half, znear, T.x1, T.y1, T.iz1)) return false;
-  if (!rend_project(vc[c], f, half, znear, T.x2, T.y2, T.iz2)) return false;
+  const float4 pa = vs[a], pb = vs[b], pc = vs[c];
+  if (pa.w == 0.f || pb.w == 0.f || pc.w == 0.f) return false;  // a vertex behind the near plane
+  T.x0 = pa.x; T.y0 = pa.y; T.iz0 = pa.z;
+  T.x1 = pb.x; T.y1 = pb.y; T.iz1 = pb.z;
+  T.x2 = pc.x; T.y2 = pc.y; T.iz2 = pc.z;
   // screen y points down: a counter-clockwise (outward) face has negative signed area
   const float area = (T.x1 - T.x0) * (T.y2 - T.y0) - (T.x2 - T.x0) * (T.y1 - T.y0);
   if (!(area < -1e-12f)) return false;
+  T.inv = 1.f / area;
   const float mnx = fminf(T.x0, fminf(T.x1, T.x2)), mxx = fmaxf(T.x0, fmaxf(T.x1, T.x2));
   const float mny = fminf(T.y0, fminf(T.y1, T.y2)), mxy = fmaxf(T.y0, fmaxf(T.y1, T.y2));
   // pixel (i, j) has its centre at (i + 0.5, j + 0.5)
@@ -108,8 +125,7 @@ DEV uint32_t rend_cover(const RTri& T, int t, int px, int py, float iz_lo, float
   const float e1 = rend_edge(T.x2, T.y2, T.i2, T.x0, T.y0, T.i0, x, y);
   const float e2 = rend_edge(T.x0, T.y0, T.i0, T.x1, T.y1, T.i1, x, y);
   if (e0 > 0.f || e1 > 0.f || e2 > 0.f) return 0u;
-  const float inv = 1.f / (e0 + e1 + e2);
-  const float iz = (e0 * T.iz0 + e1 * T.iz1 + e2 * T.iz2) * inv;
+  const float iz = (e0 * T.iz0 + e1 * T.iz1 + e2 * T.iz2) * T.inv;
   const float q = fminf(fmaxf((iz - iz_lo) * iz_scale, 0.f), 1.f);
   const uint32_t d = 1u + (uint32_t)(q * 1048574.f);  // 1 .. 2^20 - 1 (0 = empty)
   return (d << 12) | (uint32_t)t;
@@ -117,8 +133,8 @@ DEV uint32_t rend_cover(const RTri& T, int t, int px, int py, float iz_lo, float
 
 extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, int env_base) {
   extern __shared__ __align__(16) unsigned char rsmem[];
-  float4* vc = reinterpret_cast<float4*>(rsmem);                                 // [MMR_NVERT]
-  float* bpose = reinterpret_cast<float*>(vc + MMR_NVERT);                        // [19][12]
+  float4* vs = reinterpret_cast<float4*>(rsmem);                                 // [MMR_NVERT] screen
+  float* bpose = reinterpret_cast<float*>(vs + MMR_NVERT);                        // [19][12]
   uint32_t* zb = reinterpret_cast<uint32_t*>(bpose + 19 * 12);                    // [kBandPx]
   unsigned short* bigq = reinterpret_cast<unsigned short*>(zb + kBandPx);         // [kMaxBig]
   int* nbig = reinterpret_cast<int*>(bigq + kMaxBig);
@@ -176,26 +192,26 @@ extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, 
   }
   __syncthreads();
 
-  // 2. vertices to camera space
+  // 2. vertices to camera space and to the screen
   M3 cR;
   for (int k = 0; k < 9; k++) cR.m[k] = cam[k];
   const V3 cx = V3{cam[9], cam[10], cam[11]};
-  for (int v = tid; v < MMR_NVERT; v += RWG) {
-    const float* o = bpose + 12 * MMR_vert_body[v];
-    M3 R;
-    for (int k = 0; k < 9; k++) R.m[k] = o[k];
-    const V3 w = V3{o[9], o[10], o[11]} + mul(R, V3{MMR_vert[3 * v], MMR_vert[3 * v + 1], MMR_vert[3 * v + 2]});
-    const V3 c = mulT(cR, w - cx);
-    vc[v] = make_float4(c.x, c.y, c.z, 0.f);
-  }
-  __syncthreads();
-
-  // 3. rasterise
   const int c = ci == 0 ? MMX_CAM_OVERHEAD : MMX_CAM_WRIST;
   const float half = 0.5f * Sz;
   const float f = half / tanf(MMX_cam_fovy[c] * (3.14159265358979f / 360.f));
   // depth range of the camera: overhead 2 m above the floor, wrist from 1 cm
   const float znear = ci == 0 ? 0.5f : 0.01f, zfar = ci == 0 ? 2.5f : 4.0f;
+  for (int v = tid; v < MMR_NVERT; v += RWG) {
+    const float* o = bpose + 12 * MMR_vert_body[v];
+    M3 R;
+    for (int k = 0; k < 9; k++) R.m[k] = o[k];
+    const V3 w = V3{o[9], o[10], o[11]} + mul(R, V3{MMR_vert[3 * v], MMR_vert[3 * v + 1], MMR_vert[3 * v + 2]});
+    const V3 cv = mulT(cR, w - cx);
+    vs[v] = rend_project(make_float4(cv.x, cv.y, cv.z, 0.f), f, half, znear);
+  }
+  __syncthreads();
+
+  // 3. rasterise
   const float iz_lo = 1.f / zfar, iz_scale = 1.f / (1.f / znear - 1.f / zfar);
   const V3 l_top = mulT(cR, V3{0.f, 0.f, 1.f});  // toward the directional light (dir 0 0 -1)
   const V3 lp_cam = mulT(cR, V3{0.5f, 0.5f, 1.5f} - cx);
@@ -203,9 +219,10 @@ extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, 
   // pixel no triangle covers shows the floor where its ray meets z = 0 inside the plane, else sky
   for (int t = MMR_FLOOR_TRIS + tid; t < MMR_NTRI; t += RWG) {
     RTri T;
-    if (!rend_setup(vc, t, f, half, znear, Sz, row0, row1, T)) continue;
+    if (!rend_setup(vs, t, Sz, row0, row1, T)) continue;
     {  // flat shading of the face, once: headlight + directional + point light (at the centroid)
-      const float4 a = vc[T.i0], b = vc[T.i1], cc = vc[T.i2];
+      const float4 a = rend_unproject(T.x0, T.y0, T.iz0, f, half), b = rend_unproject(T.x1, T.y1, T.iz1, f, half),
+                   cc = rend_unproject(T.x2, T.y2, T.iz2, f, half);
       const V3 n = normalize(cross(V3{b.x - a.x, b.y - a.y, b.z - a.z}, V3{cc.x - a.x, cc.y - a.y, cc.z - a.z}));
       const V3 pc = V3{(a.x + b.x + cc.x) * (1.f / 3.f), (a.y + b.y + cc.y) * (1.f / 3.f), (a.z + b.z + cc.z) * (1.f / 3.f)};
       const float light = 0.3f + 0.6f * fmaxf(n.z, 0.f) + 0.8f * fmaxf(dot(n, l_top), 0.f) +
@@ -227,10 +244,12 @@ extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, 
     for (int q = grp; q < ns; q += RWG / kGroup) {
       const int t = smallq[q];
       RTri T;
-      rend_setup(vc, t, f, half, znear, Sz, row0, row1, T);
+      rend_setup(vs, t, Sz, row0, row1, T);
       const int w = T.bx1 - T.bx0 + 1, area = w * (T.by1 - T.by0 + 1);
+      const float rw = 1.f / (float)w;
       for (int k = gl; k < area; k += kGroup) {
-        const int px = T.bx0 + k % w, py = T.by0 + k / w;
+        const int r = (int)(((float)k + 0.5f) * rw);  // k / w, exact for these sizes (no integer divide)
+        const int px = T.bx0 + k - r * w, py = T.by0 + r;
         const uint32_t key = rend_cover(T, t, px, py, iz_lo, iz_scale);
         if (key) atomicMax(&zb[(py - row0) * Sz + px], key);
       }
@@ -240,10 +259,12 @@ extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, 
   for (int q = 0; q < nb; q++) {  // large triangles: the workgroup scans the box pixel-parallel
     const int t = bigq[q];
     RTri T;
-    rend_setup(vc, t, f, half, znear, Sz, row0, row1, T);
+    rend_setup(vs, t, Sz, row0, row1, T);
     const int w = T.bx1 - T.bx0 + 1, area = w * (T.by1 - T.by0 + 1);
+    const float rw = 1.f / (float)w;
     for (int k = tid; k < area; k += RWG) {
-      const int px = T.bx0 + k % w, py = T.by0 + k / w;
+      const int r = (int)(((float)k + 0.5f) * rw);  // k / w, exact for these sizes (no integer divide)
+      const int px = T.bx0 + k - r * w, py = T.by0 + r;
       const uint32_t key = rend_cover(T, t, px, py, iz_lo, iz_scale);
       if (key) atomicMax(&zb[(py - row0) * Sz + px], key);
     }
@@ -310,7 +331,7 @@ extern "C" size_t mmx_render_lds_bytes() {
 
 extern "C" hipError_t mmx_launch_render(const MMXState* S, int base, int count, hipStream_t st) {
   if (count <= 0 || S->image_size <= 0) return hipSuccess;
-  const int rows = S->image_size < kBandPx / S->image_size ? S->image_size : kBandPx / S->image_size;
+  const int rows = rend_band_rows(S->image_size);
   const int bands = (S->image_size + rows - 1) / rows;
   hipLaunchKernelGGL(mmx_render_kernel, dim3(bands, 2, count), dim3(RWG), mmx_render_lds_bytes(), st, *S, base);
   return hipGetLastError();

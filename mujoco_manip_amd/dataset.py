@@ -17,8 +17,11 @@ MI355X instead of one after another:
   `meta/episodes/...parquet`, `meta/stats.json`) plus the reference's `metadata.json`
   (generation config + `episode_seeds`, :306-319).
 
-Camera images need the batched renderer, which this build does not have yet:
-the two image features are rejected with a ValueError rather than silently dropped.
+Camera images (observation.images.overhead / .wrist, features.py:11-20, 224 x 224 RGB) come from
+the batched HIP renderer (mmx_render.hip): the PRE-step images of every active
+slot are gathered on device each step, PNG-encoded on the host and stored the way LeRobot stores
+`dtype: image` features with use_videos=False (generate_dataset.py:250-260): a parquet struct
+column {bytes: PNG, path} per frame, per-channel image statistics in meta/stats.json.
 LeRobot itself is not importable here, so the on-disk layout follows LeRobot v3.0's documented
 format without a round-trip check against the library ("format unpinned"); the frame VALUES are
 pinned against the oracle running the reference loop (tests/test_dataset.py).
@@ -167,7 +170,7 @@ class Episode:
     obj: str
     bin: str
     seed: int | None
-    frames: dict = field(default_factory=dict)  # feature -> np.ndarray [T, ...] (strings: list)
+    frames: dict = field(default_factory=dict)  # feature -> np.ndarray [T, ...] (strings, PNG bytes: list)
     length: int = 0
 
 
@@ -195,11 +198,26 @@ def resolve_features(features=None, reward_type="staged"):
         feats = {k: FEATURES[k] for k in requested}
     if reward_type != "staged":
         feats.pop("next.reward", None)
-    imgs = [k for k in feats if k in IMAGE_KEYS]
-    if imgs:
-        raise ValueError(f"image features {imgs} need the batched camera renderer (SURVEY §8 f1), "
-                         "which this build does not provide yet; request the numeric features only")
     return feats
+
+
+def png_encode(img: np.ndarray) -> bytes:
+    """uint8 [H, W, 3] -> PNG bytes (what LeRobot embeds for an `image` feature)."""
+    import io
+
+    from PIL import Image
+
+    buf = io.BytesIO()
+    Image.fromarray(np.ascontiguousarray(img)).save(buf, format="PNG", compress_level=1)
+    return buf.getvalue()
+
+
+def png_decode(data: bytes) -> np.ndarray:
+    import io
+
+    from PIL import Image
+
+    return np.asarray(Image.open(io.BytesIO(data)).convert("RGB"))
 
 
 def episode_seeds(seed: int, num_episodes: int) -> list[int]:
@@ -211,10 +229,12 @@ def episode_seeds(seed: int, num_episodes: int) -> list[int]:
 
 def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type="staged", randomize_objects=False,
                      seed=0, spawn_x_range=(-0.20, 0.20), spawn_y_range=(0.30, 0.45), num_envs=1024, device=0,
-                     max_gym_steps=5000):
+                     max_gym_steps=5000, on_step=None):
     """Run `num_episodes` reference run_episode loops (generate_dataset.py:83-198) side by side.
 
-    Returns (episodes, seeds): a list of Episode with per-feature frame arrays in step order.
+    Returns (episodes, seeds): a list of Episode with per-feature frame arrays in step order
+    (image features: lists of PNG bytes).  on_step(slots, episode_ids, env), when given, sees the
+    env before each batched step (the state the step's frames were recorded from).
     """
     import torch
 
@@ -231,6 +251,7 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
     need_actions = bool(set(feature_keys) & set(ACTION_KEYS))
     need_reward = "next.reward" in feature_keys and reward_type == "staged"
     obs_feats = [(k, f) for k, f in OBS_TO_FEATURE.items() if f in feature_keys]
+    img_feats = [(cam, f) for cam, f in enumerate(IMAGE_KEYS) if f in feature_keys]
 
     eps = [Episode(e, *task_list[e % len(task_list)], seeds[e] if seeds else None) for e in range(E)]
     slot_ep = np.full(N, -1, np.int64)
@@ -279,6 +300,8 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
         for k, f in obs_feats:
             a, b, _ = OBS_SLICES[k]
             frame[f] = obs_pre[:, a:b]
+        for cam, f in img_feats:  # PRE-step images (rendered after the reset / previous step)
+            frame[f] = env._images[:, cam].index_select(0, idx)
         a_sel = action.index_select(0, idx)
         if need_actions:
             T = env.initial_ee_se3.index_select(0, idx)
@@ -287,6 +310,8 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
                 if k in feature_keys:
                     frame[k] = enc[k]
         fsm_after = fsm_view.index_select(0, idx).clone()
+        if on_step is not None:
+            on_step(act_slots, slot_ep[act_slots].copy(), env)
         env.step(action)
         if need_reward:
             frame["next.reward"] = env._rc.index_select(0, idx).clone()
@@ -299,6 +324,8 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
     host = []
     for r, (slots, ep_ids, frame, fsm) in enumerate(rec):
         hf = {k: v.cpu().numpy() for k, v in frame.items()}
+        for _, f in img_feats:
+            hf[f] = [png_encode(im) for im in hf[f]]
         host.append((hf, fsm.cpu().numpy()))
         for j, e in enumerate(ep_ids):
             per_ep_rows[e].append((r, j))
@@ -308,6 +335,8 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
         for k in feature_keys:
             if k == "observation.phase_description":
                 ep.frames[k] = [phase_description(host[r][1][j], ep.obj, ep.bin) for r, j in rows]
+            elif k in IMAGE_KEYS:
+                ep.frames[k] = [host[r][0][k][j] for r, j in rows]
             elif host and k in host[0][0]:
                 ep.frames[k] = np.stack([host[r][0][k][j] for r, j in rows]).astype(np.float32)
     env.close()
@@ -321,9 +350,21 @@ def _feature_stats(x: np.ndarray) -> dict:
             "std": x.std(0).tolist(), "count": [int(len(x))]}
 
 
+def _image_stats(pngs, max_frames=32) -> dict:
+    """Per-channel statistics of an image feature over a frame sample, pixels scaled to [0, 1],
+    shaped (3, 1, 1) as LeRobot keeps them for image / video features."""
+    idx = np.linspace(0, len(pngs) - 1, min(len(pngs), max_frames)).astype(int)
+    x = np.stack([png_decode(pngs[i]) for i in idx]).astype(np.float64) / 255.0  # [F, H, W, 3]
+    c = x.reshape(-1, 3)
+    shape = lambda v: [[[float(a)]] for a in v]  # noqa: E731
+    return {"min": shape(c.min(0)), "max": shape(c.max(0)), "mean": shape(c.mean(0)), "std": shape(c.std(0)),
+            "count": [int(len(pngs))]}
+
+
 def write_lerobot_v3(root: str, repo_id: str, episodes, features: dict, *, fps=CONTROL_FPS,
                      robot_type="franka_panda", chunks_size=1000, data_files_size_in_mb=100, extra_info=None):
-    """Write episodes in the LeRobot v3.0 layout (use_videos=False, no image features).
+    """Write episodes in the LeRobot v3.0 layout (use_videos=False: image features embedded as
+    parquet structs {bytes: PNG, path}).
 
     data/chunk-XXX/file-YYY.parquet  frames of consecutive episodes (features + timestamp,
                                      frame_index, episode_index, index, task_index)
@@ -341,6 +382,8 @@ def write_lerobot_v3(root: str, repo_id: str, episodes, features: dict, *, fps=C
     task_idx = {t: i for i, t in enumerate(tasks)}
     num_keys = [k for k, f in features.items() if f["dtype"] == "float32"]
     str_keys = [k for k, f in features.items() if f["dtype"] == "string"]
+    img_keys = [k for k, f in features.items() if f["dtype"] == "image"]
+    img_type = pa.struct([("bytes", pa.binary()), ("path", pa.string())])
 
     def ep_table(ep, start):
         n = ep.length
@@ -353,6 +396,10 @@ def write_lerobot_v3(root: str, repo_id: str, episodes, features: dict, *, fps=C
         for k in str_keys:
             cols[k] = pa.array(list(ep.frames[k]), pa.string())
             fields.append(pa.field(k, pa.string()))
+        for k in img_keys:  # LeRobot's embedded image layout (images/<key>/episode_<e>/frame_<i>.png)
+            cols[k] = pa.array([{"bytes": b, "path": f"images/{k}/episode_{ep.index:06d}/frame_{i:06d}.png"}
+                                for i, b in enumerate(ep.frames[k])], img_type)
+            fields.append(pa.field(k, img_type))
         fi = np.arange(n, dtype=np.int64)
         extra = {"timestamp": pa.array((fi / fps).astype(np.float32)), "frame_index": pa.array(fi),
                  "episode_index": pa.array(np.full(n, ep.index, np.int64)), "index": pa.array(start + fi),
@@ -389,6 +436,9 @@ def write_lerobot_v3(root: str, repo_id: str, episodes, features: dict, *, fps=C
         for k in num_keys:
             for s, v in _feature_stats(np.asarray(ep.frames[k])).items():
                 row[f"stats/{k}/{s}"] = v
+        for k in img_keys:
+            for s, v in _image_stats(ep.frames[k], 8).items():
+                row[f"stats/{k}/{s}"] = v
         ep_rows.append(row)
         cur.append(tab)
         cur_bytes += tab.nbytes
@@ -404,6 +454,8 @@ def write_lerobot_v3(root: str, repo_id: str, episodes, features: dict, *, fps=C
     for k in num_keys:
         allf = np.concatenate([np.asarray(ep.frames[k], np.float32).reshape(ep.length, -1) for ep in episodes])
         stats[k] = _feature_stats(allf)
+    for k in img_keys:
+        stats[k] = _image_stats([b for ep in episodes for b in ep.frames[k]])
     with open(os.path.join(meta, "stats.json"), "w") as f:
         json.dump(stats, f, indent=1)
     feats = {k: {"dtype": v["dtype"], "shape": list(v["shape"]), "names": v["names"]} for k, v in features.items()}
@@ -447,6 +499,8 @@ def read_lerobot_v3(root: str):
             col = tab.column(name).take(sel).combine_chunks()
             if pa.types.is_fixed_size_list(col.type):
                 fr[name] = np.asarray(col.flatten(), np.float32).reshape(len(sel), col.type.list_size)
+            elif pa.types.is_struct(col.type):  # embedded image: {bytes: PNG, path}
+                fr[name] = np.stack([png_decode(v["bytes"]) for v in col.to_pylist()]) if len(sel) else None
             elif pa.types.is_string(col.type):
                 fr[name] = col.to_pylist()
             else:
