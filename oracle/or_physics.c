@@ -664,3 +664,4 @@ void or_get_contact(or_env* e, int i, int* geom, double* dist, double* pos, doub
 void or_get_efc_force(or_env* e, double* f) { memcpy(f, e->efc_force, e->nefc * sizeof(double)); }
 double or_solver_residual(or_env* e) { return e->solver_res; }
 void or_get_qacc(or_env* e, double* qacc) { memcpy(qacc, e->qacc, sizeof(e->qacc)); }
+void or_get_mass_matrix(or_env* e, double* M) { memcpy(M, e->M, sizeof(e->M)); }

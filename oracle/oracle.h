@@ -71,6 +71,7 @@ void or_get_contact(or_env* e, int i, int* geom, double* dist, double* pos, doub
 void or_get_efc_force(or_env* e, double* f);
 double or_solver_residual(or_env* e);
 void or_get_qacc(or_env* e, double* qacc);
+void or_get_mass_matrix(or_env* e, double* M); /* qM (dense NV x NV, CRBA + armature) of the last forward */
 void or_get_obs(or_env* e, float* obs85);
 void or_get_initial_ee(or_env* e, double* T16);
 int or_step_count(or_env* e);

@@ -67,6 +67,7 @@ def lib():
         L.or_solver_residual.restype = C.c_double
         L.or_solver_residual.argtypes = [C.c_void_p]
         L.or_get_qacc.argtypes = [C.c_void_p, dp]
+        L.or_get_mass_matrix.argtypes = [C.c_void_p, dp]
         L.or_get_obs.argtypes = [C.c_void_p, fp]
         L.or_get_initial_ee.argtypes = [C.c_void_p, dp]
         L.or_step_count.restype = C.c_int
@@ -272,6 +273,12 @@ class OracleEnv:
         q = np.zeros(NV)
         lib().or_get_qacc(self.ptr, _d(q))
         return q
+
+    def mass_matrix(self):
+        """qM of the last forward (CRBA + armature), dense NV x NV."""
+        M = np.zeros(NV * NV)
+        lib().or_get_mass_matrix(self.ptr, _d(M))
+        return M.reshape(NV, NV)
 
     def obs(self):
         o = np.zeros(85, np.float32)
