@@ -29,7 +29,16 @@
 
 #define WG 64  // lanes of the wave that runs a phase
 // lane within the wave; WAVE_ID: which of the env-step kernel's two waves (0 or 1)
+#ifdef MMX_LANE_OPAQUE  // experiment: lane id re-materialised per use (nothing lane-indexed hoists)
+DEV int lane_opaque() {
+  int t = (int)threadIdx.x;
+  asm volatile("" : "+v"(t));
+  return t & 63;
+}
+#define LANE lane_opaque()
+#else
 #define LANE ((int)(threadIdx.x & 63))
+#endif
 #define WAVE_ID ((int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6))
 // SYNC: wave-local LDS ordering (a phase runs on ONE wave: its lanes exchange data through LDS,
 // whose operations a wave issues and completes in order, so no s_barrier / waitcnt is needed,
@@ -1426,6 +1435,81 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
   return LANE < 27 ? gacc + mdx : 0.f;
 }
 
+// Incremental form of hess_grad_mfma for the Newton iterations after the first.  Over a line
+// search only the edges whose active state flipped change their weight, so with Delta C the
+// groups' change of edge-weight matrix (nonzero only in groups holding a flipped edge):
+//   H_new = H_old + sum_groups B' dC B,   g_new = g_old + a H_old p + sum_groups B' dC r_new
+// (g = M (x - xs) + sum B' C r; B' C_old r_new = B' C_old r_old + a B' C_old B p).  E.D / E.NC /
+// slot 15 hold dC_kk, dC_nk and dC r_new (newton_wave's weight pass in delta mode); gm[q] bit 4m
+// marks group m of row slice q as changed (wave-uniform).  Only the changed groups' MFMA steps run,
+// and only the row types holding one are staged and gathered.  LDS rows only (the caller runs the
+// full pass when rows spill to HBM).  Adds into hrow; returns sum B' dC r in lane j < 27.
+#define HESS_LQ (MMX_LDSEFC / WG)  // row slices held in LDS
+#ifndef MMX_NEWTON_DELTA
+#define MMX_NEWTON_DELTA 1  // 0: full Hessian / gradient pass every Newton iteration (A/B switch)
+#endif
+DEV float hess_grad_delta(EnvSh& E, float* hrow, const unsigned long long* gm) {
+  float* G = lrow_of(E);
+  const int col = LANE & 15, rk = LANE >> 4;
+  const int d = min(LANE, 26);
+  const int bd = dof_blk(d), od = d - blk_d0(bd);
+  const float m_[4] = {rk == 0 ? 1.f : 0.f, rk == 1 ? 1.f : 0.f, rk == 2 ? 1.f : 0.f, rk == 3 ? 1.f : 0.f};
+  const float c15 = col == 15 ? 1.f : 0.f;
+  float gacc = 0.f;
+  for (int t = 0; t < NTYPE; t++) {
+    const int r0 = E.tbase[t], r1 = E.tbase[t + 1];
+    if (r1 <= r0) continue;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    bool any = false;
+#pragma unroll
+    for (int q = 0; q < HESS_LQ; q++) {
+      if (64 * q >= r1 || 64 * (q + 1) <= r0) continue;  // uniform
+      const int lo = max(r0 - 64 * q, 0), hi = min(r1 - 64 * q, 64);
+      unsigned long long m = gm[q] & (hi >= 64 ? ~0ull : ((1ull << hi) - 1ull)) & (~0ull << lo);
+      while (m) {  // uniform: the type's changed groups, one MFMA step each
+        const int g0 = 64 * q + __builtin_ctzll(m);
+        m &= m - 1ull;
+        any = true;
+        const float4 n4 = *reinterpret_cast<const float4*>(&E.NC[g0]);
+        float jg[4];
+#pragma unroll
+        for (int mm = 0; mm < 4; mm++) jg[mm] = E.J[g0 + mm][col];  // slot 15 holds dC r
+        const float dr = E.D[g0 + rk];
+        const float own = fmaf(m_[0], jg[0], fmaf(m_[1], jg[1], fmaf(m_[2], jg[2], m_[3] * jg[3])));
+        const float ncr = fmaf(m_[1], n4.y, fmaf(m_[2], n4.z, m_[3] * n4.w));
+        const float s123 = fmaf(n4.y, jg[1], fmaf(n4.z, jg[2], n4.w * jg[3]));
+        const float cpl = fmaf(ncr, jg[0], m_[0] * s123);
+        const float b = fmaf(c15, own - fmaf(dr, own, cpl), fmaf(dr, own, cpl));
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(own, b, acc, 0, 0, 0);
+      }
+    }
+    if (!any) continue;
+#pragma unroll
+    for (int q = 0; q < 4; q++) G[16 * (4 * rk + q) + col] = acc[q];
+    SYNC();
+    const int b0 = kTB0[t], b1 = kTB1[t];
+    const int n0 = blk_size(b0);
+    const int sd = bd == b0 ? od : (bd == b1 ? n0 + od : -1);
+    if (sd >= 0) {
+      const float* Gr = G + 16 * sd;
+#pragma unroll
+      for (int B = 0; B < 4; B++) {
+        const int nb = B == 0 ? 9 : 6, dB = B == 0 ? 0 : 9 + 6 * (B - 1);
+        if (B == b0) {
+#pragma unroll
+          for (int k = 0; k < nb; k++) hrow[dB + k] += Gr[k];
+        } else if (B == b1) {
+#pragma unroll
+          for (int k = 0; k < nb; k++) hrow[dB + k] += Gr[n0 + k];
+        }
+      }
+      gacc += Gr[15];
+    }
+    SYNC();
+  }
+  return LANE < 27 ? gacc : 0.f;
+}
+
 // The same contraction as ONE 32 x 32 tile in dof space (27 dofs + the gradient column 27) on
 // v_mfma_f32_32x32x2_f32, two rows of a group per MFMA step: lane l supplies A[dof i][row k] =
 // J[row k][slot of dof i] and B[row k][dof i] = (C B)[k][dof i], with i = l & 31 and k = l >> 5;
@@ -1667,11 +1751,23 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
   SYNC();
   int it = 0;
   resid = 0.f;
+  // Hessian rows and gradient persist across iterations: after the first full pass each later one
+  // adds only the groups whose edge weights changed (hess_grad_delta); act holds the lane's edge
+  // active bits (bit 2q: edge 0 of slice q, bit 2q + 1: edge 1) the current H was built from
+  float hrow[32];
+  float gpred = 0.f;  // g_old + a H_old p: the gradient at the new point before the weight change
+  int act = 0;
   PROBE(1, stats, STAT_T_AUX3);
   for (; it < max_iter; it++) {
     // per group: the edge-weight matrix C (C_kk -> D, C_nk -> NC) and g = sum_e w_e r_e c_e
     // (-> slot 15), from the active edges of the current residuals; a contact's normal row
-    // collects its edges' normal parts over the DPP quad
+    // collects its edges' normal parts over the DPP quad.  Delta mode: the same with the change
+    // of each edge's weight (+-D where its active state flipped, else 0), and a mask of the
+    // groups holding a flipped edge.
+    const bool delta = MMX_NEWTON_DELTA && it > 0 && nefc <= MMX_LDSEFC;  // uniform
+    unsigned long long gm[HESS_LQ];
+#pragma unroll
+    for (int q = 0; q < HESS_LQ; q++) gm[q] = 0ull;
 #pragma unroll
     for (int q = 0; q < RPL; q++) {
       if (WG * q >= nefc) break;  // uniform: no rows past this slice
@@ -1679,8 +1775,18 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
       const EdgeCoef ec = edge_coef(i, nefc, nsingle, mu[q]);
       const float rn = quad_first(rr[q]);
       const float e0 = fmaf(ec.a0, rn, ec.b0 * rr[q]), e1 = fmaf(ec.a1, rn, ec.b1 * rr[q]);
-      const float w0 = EQROW(q) || e0 < 0.f ? dd[q] : 0.f;  // (missing edges: coefficients 0)
-      const float w1 = e1 < 0.f ? dd[q] : 0.f;
+      const bool on0 = EQROW(q) || e0 < 0.f, on1 = e1 < 0.f;  // (missing edges: coefficients 0)
+      const bool was0 = (act >> (2 * q)) & 1, was1 = (act >> (2 * q + 1)) & 1;
+      act = (act & ~(3 << (2 * q))) | ((on0 ? 1 : 0) << (2 * q)) | ((on1 ? 2 : 0) << (2 * q));
+      float w0 = on0 ? dd[q] : 0.f, w1 = on1 ? dd[q] : 0.f;
+      if (delta) {
+        w0 = on0 == was0 ? 0.f : (on0 ? dd[q] : -dd[q]);
+        w1 = on1 == was1 ? 0.f : (on1 ? dd[q] : -dd[q]);
+        if (q < HESS_LQ) {
+          const unsigned long long bm = __ballot(w0 != 0.f || w1 != 0.f);
+          gm[q < HESS_LQ ? q : 0] = (bm | (bm >> 1) | (bm >> 2) | (bm >> 3)) & 0x1111111111111111ull;
+        }
+      }
       const float ckk = fmaf(w0 * ec.b0, ec.b0, w1 * ec.b1 * ec.b1);
       const float cnk = fmaf(w0 * ec.a0, ec.b0, w1 * ec.a1 * ec.b1);
       const float gk = fmaf(w0 * e0, ec.b0, w1 * e1 * ec.b1);
@@ -1696,12 +1802,16 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
     ovf_fence(nefc);
     SYNC();
     PROBE(1, stats, STAT_T_AUX0);
-    float hrow[32];
+    float g;
+    if (delta) {
+      g = gpred + hess_grad_delta(E, hrow, gm);
+    } else {
 #if MMX_HESS32
-    const float g = hess_grad_mfma32(E, nefc, hrow, mdx);
+      g = hess_grad_mfma32(E, nefc, hrow, mdx);
 #else
-    const float g = hess_grad_mfma(E, nefc, hrow, mdx);
+      g = hess_grad_mfma(E, nefc, hrow, mdx);
 #endif
+    }
     resid = sqrtf(wave_sum(g * g)) / scale;
     PROBE(1, stats, STAT_T_AUX1);
     if (resid < tol) break;
@@ -1787,11 +1897,11 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
       it++;
       break;
     }
+    gpred = LANE < 27 ? fmaf(alpha, hp, g) : 0.f;
     if (__ballot(flip) == 0ull) {
       // same active set: H is unchanged, so g(x + a p) = g + a H p exactly; when that already
       // meets the tolerance the confirming Hessian pass is skipped
-      const float gn = LANE < 27 ? fmaf(alpha, hp, g) : 0.f;
-      const float rn = sqrtf(wave_sum(gn * gn)) / scale;
+      const float rn = sqrtf(wave_sum(gpred * gpred)) / scale;
       if (rn < tol) {
         resid = rn;
         it++;
