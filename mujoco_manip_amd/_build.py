@@ -28,8 +28,13 @@ DEVICE_MATH = ["-Xarch_device", "-freciprocal-math", "-Xarch_device", "-fapprox-
 # occupancy-driven scheduler on the C3 bench (max-ilp +2 %, max-memory-clause +0 %).  The option
 # is an LLVM backend flag; the host compile accepts and ignores it.
 DEVICE_SCHED = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
+# no SLP vectorisation in device code: at -O3 it packs pairs of independent fp32 ops into
+# v_pk_fma_f32 / v_pk_mul_f32 on even-aligned register pairs (2,700 packed ops in the substep); the
+# pairing constraints raised the substep's register pressure into scratch spills (frame 480 -> 172 B)
+# and the packed ops bought no issue slots: C3 1.905M -> 2.100M env steps/s in the A/B
+DEVICE_NOSLP = ["-Xarch_device", "-fno-slp-vectorize"]
 # extra compiler flags (experiments only; the committed build uses none)
-FLAGS = DEVICE_MATH + DEVICE_SCHED + os.environ.get("MMX_EXTRA_FLAGS", "").split()
+FLAGS = DEVICE_MATH + DEVICE_SCHED + DEVICE_NOSLP + os.environ.get("MMX_EXTRA_FLAGS", "").split()
 
 
 def lib_path(profile: bool = False) -> str:

@@ -106,6 +106,7 @@ DEV void plane_box(Sink& cs, const Geom& P, const Geom& B, V3 hb) {
       cnt++;
     }
   }
+  const int base = cs.reserve(cnt < 4 ? cnt : 4);  // one slot reservation for the pair
 #pragma unroll
   for (int k = 0; k < 4; k++) {  // keep the 4 deepest corners
     if (k >= cnt) break;
@@ -129,7 +130,7 @@ DEV void plane_box(Sink& cs, const Geom& P, const Geom& B, V3 hb) {
         cd[m] = td;
         cp[m] = tp;
       }
-    cs.add(P.g, B.g, cd[k], cp[k], nz);
+    cs.put(base + k, P.g, B.g, cd[k], cp[k], nz);
   }
 }
 
@@ -279,11 +280,17 @@ DEV void box_box(Sink& cs, const Geom& G1, const Geom& G2, V3 hb1, V3 hb2, V3* p
                dot(qs[c], -ax1) - b3 <= 0.f;
     PROBEF(8, cs.E->stats, STAT_T_AUX1);
     if (inside) {
+      float dep[4];
+      int n = 0;
 #pragma unroll
       for (int c = 0; c < 4; c++) {
-        const float depth = -dot(qs[c] - cr, nref);
-        if (depth >= 0.f) cs.add(G1.g, G2.g, -depth, qs[c] + nref * (0.5f * depth), nout);
+        dep[c] = -dot(qs[c] - cr, nref);
+        n += dep[c] >= 0.f ? 1 : 0;
       }
+      int slot = cs.reserve(n);
+#pragma unroll
+      for (int c = 0; c < 4; c++)
+        if (dep[c] >= 0.f) cs.put(slot++, G1.g, G2.g, -dep[c], qs[c] + nref * (0.5f * dep[c]), nout);
       PROBEF(8, cs.E->stats, STAT_T_AUX2);
       return;
     }
@@ -298,9 +305,12 @@ DEV void box_box(Sink& cs, const Geom& G1, const Geom& G2, V3 hb1, V3 hb2, V3* p
   np = clip_poly(poly, np, tmp, ax1, dot(ax1, cr) + hrv);
   np = clip_poly(tmp, np, poly, -ax1, dot(-ax1, cr) + hrv);
   PROBEF(8, cs.E->stats, STAT_T_AUX3);
+  int n = 0;
+  for (int c = 0; c < np; c++) n += -dot(poly[c] - cr, nref) >= 0.f ? 1 : 0;
+  int slot = cs.reserve(n);
   for (int c = 0; c < np; c++) {
     const float depth = -dot(poly[c] - cr, nref);
-    if (depth >= 0.f) cs.add(G1.g, G2.g, -depth, poly[c] + nref * (0.5f * depth), nout);
+    if (depth >= 0.f) cs.put(slot++, G1.g, G2.g, -depth, poly[c] + nref * (0.5f * depth), nout);
   }
 }
 

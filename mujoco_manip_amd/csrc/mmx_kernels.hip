@@ -641,14 +641,20 @@ struct WaveSink {
     mu2 = fmaxf(MMX_geom_friction[3 * g1 + 2], MMX_geom_friction[3 * g2 + 2]);
     dim = (float)max(MMX_geom_condim[g1], MMX_geom_condim[g2]);
   }
-  DEV void add(int g1, int g2, float dist, V3 pos, V3 nrm) {
+  DEV void add(int g1, int g2, float dist, V3 pos, V3 nrm) { put(reserve(1), g1, g2, dist, pos, nrm); }
+  // n consecutive contact slots with one LDS atomic (a pair's corners / clipped points are
+  // counted first, then reserved together); returns the first slot, MMX_MAXCON when none is kept
+  DEV int reserve(int n) {
+    if (n <= 0) return MMX_MAXCON;
     if (ro) atomicOr(&E->flags, (int)SHF_ROBOT_OBST);
-    if (!store) return;
-    const int slot = atomicAdd(&E->ncon, 1);
-    if (slot >= MMX_MAXCON) {
-      atomicOr(&E->flags, (int)SHF_CON_OVF);
-      return;
-    }
+    if (!store) return MMX_MAXCON;
+    const int slot = atomicAdd(&E->ncon, n);
+    if (slot + n > MMX_MAXCON) atomicOr(&E->flags, (int)SHF_CON_OVF);
+    return slot;
+  }
+  // contact into a reserved slot (slots past the list are dropped); keys follow the call order
+  DEV void put(int slot, int g1, int g2, float dist, V3 pos, V3 nrm) {
+    if (slot >= MMX_MAXCON) return;
     nrm = normalize(nrm);
     float* c = E->con[slot];
     c[CON_DIST] = dist;
@@ -966,11 +972,13 @@ DEV float contact_row(EnvSh& E, int row, int c, int rr) {
   }
   float vel = 0.f;
   float arm[9];
+  // u . (v_d + w_d x p) + w . w_d = u . v_d + w_d . (p x u + w): one cross product per row
+  const V3 pu = cross(p, u) + w;
 #pragma unroll
   for (int d = 0; d < 9; d++) {  // body 2 counts +, body 1 counts -
     const float coef = (arm_anc(d, b2) ? 1.f : 0.f) - (arm_anc(d, b1) ? 1.f : 0.f);
     const SV sd = load_S(E, d);
-    arm[d] = coef * (dot(u, sd.v + cross(sd.w, p)) + dot(w, sd.w));
+    arm[d] = coef * (dot(u, sd.v) + dot(sd.w, pu));
     vel = fmaf(arm[d], E.qvel[d], vel);
   }
   float cubeA[6], cubeB[6];  // blocks rb0 (when a cube) and rb1
@@ -987,11 +995,9 @@ DEV float contact_row(EnvSh& E, int row, int c, int rr) {
       const V3 x = body_x(E, b);
       const M3 R = body_R(E, b);
       float cv[6] = {sg * u.x, sg * u.y, sg * u.z, 0.f, 0.f, 0.f};
+      const V3 ru = cross(p - x, u) + w;  // u . (r_k x (p - x)) + w . r_k = r_k . ((p - x) x u + w)
 #pragma unroll
-      for (int k = 0; k < 3; k++) {
-        const V3 rk = col(R, k);
-        cv[3 + k] = sg * (dot(u, cross(rk, p - x)) + dot(w, rk));
-      }
+      for (int k = 0; k < 3; k++) cv[3 + k] = sg * dot(col(R, k), ru);
       const int d0 = blk_d0(blk);
       const bool toA = blk == rb0;
 #pragma unroll
@@ -1184,11 +1190,39 @@ DEV void make_constraints_wave(EnvSh& E) {
 // Lane l owns constraint rows l + 64 q (q < RPL): their residual, search-direction projection,
 // D and equality flag stay in registers through the line search.  The Hessian and gradient come
 // from one MFMA pass (hess_grad_mfma) straight into registers; the Cholesky factorisation and
-// both triangular solves run in registers (chol_solve_reg): no LDS matrix, no barrier.
+// both triangular solves run in registers (chol_solve).
 #define RPL ((MMX_MAXEFC + WG - 1) / WG)
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 DEV float readlane_f(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+
+// Newton lane layout: the solver's dof-space values (Hessian rows, gradient, search direction,
+// M v) sit with arm dof d in lane d (DPP row 0 of the wave's four 16-lane rows) and cube b's dof k
+// in lane 16 b + k (row b), so each dof block owns one DPP row: the block Cholesky broadcasts a
+// pivot to its block with one row_newbcast.  Lanes 9..15, 16 b + 6..15 hold no dof (-1).
+DEV int newton_dof(int L) {
+  const int r = L >> 4, k = L & 15;
+  return r == 0 ? (k < 9 ? k : -1) : (k < 6 ? 9 + 6 * (r - 1) + k : -1);
+}
+__host__ __device__ constexpr int newton_lane(int d) { return d < 9 ? d : 16 * (1 + (d - 9) / 6) + (d - 9) % 6; }
+// DPP row_newbcast:K, the value of lane K of each 16-lane row in every lane of that row
+template <int K>
+DEV float row_bcast_t(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + K, 0xF, 0xF, false));
+}
+// k is a constant of a fully unrolled loop at every call: the switch folds to one DPP move
+DEV float row_bcast(float v, int k) {
+  switch (k) {
+    case 0: return row_bcast_t<0>(v);
+    case 1: return row_bcast_t<1>(v);
+    case 2: return row_bcast_t<2>(v);
+    case 3: return row_bcast_t<3>(v);
+    case 4: return row_bcast_t<4>(v);
+    case 5: return row_bcast_t<5>(v);
+    case 6: return row_bcast_t<6>(v);
+    case 7: return row_bcast_t<7>(v);
+    default: return row_bcast_t<8>(v);
+  }
+}
 
 // J_i . x for a block-format row (slots past the row's width hold zeros)
 DEV float row_dot16(const EnvSh& E, int i, const float* x) {
@@ -1212,25 +1246,27 @@ DEV float row_dot16(const EnvSh& E, int i, const float* x) {
   return s;
 }
 
-// (M v)_lane for lane < 27 (arm rows: the 9 x 9 block; cube rows: the diagonal)
+// (M v) of the lane's dof (Newton lane layout; arm rows: the 9 x 9 block; cube rows: the diagonal)
 DEV float mass_mul(const EnvSh& E, const float* v) {
+  const int nd = newton_dof(LANE);
   if (LANE < 9) {
     float m = 0.f;
 #pragma unroll
     for (int b = 0; b < 9; b++) m = fmaf(E.M9[LANE][b], v[b], m);
     return m;
   }
-  return LANE < 27 ? E.Mc[LANE - 9] * v[LANE] : 0.f;
+  return nd >= 0 ? E.Mc[nd - 9] * v[nd] : 0.f;
 }
-// (M (xa - xb))_lane, same layout
+// (M (xa - xb)) of the lane's dof, same layout
 DEV float mass_mul_diff(const EnvSh& E, const float* xa, const float* xb) {
+  const int nd = newton_dof(LANE);
   if (LANE < 9) {
     float m = 0.f;
 #pragma unroll
     for (int b = 0; b < 9; b++) m = fmaf(E.M9[LANE][b], xa[b] - xb[b], m);
     return m;
   }
-  return LANE < 27 ? E.Mc[LANE - 9] * (xa[LANE] - xb[LANE]) : 0.f;
+  return nd >= 0 ? E.Mc[nd - 9] * (xa[nd] - xb[nd]) : 0.f;
 }
 
 // Pyramid edges from basis rows.  Lane l owns rows l + 64 q; rows are 4-aligned groups, so a
@@ -1272,11 +1308,12 @@ DEV void cost2_wave(const EnvSh& E, const float* xa, const float* xb, const floa
   float c0 = 0.f, c1 = 0.f;
   ma = 0.f;
   mb = 0.f;
-  if (LANE < 27) {
+  const int nd = newton_dof(LANE);
+  if (nd >= 0) {
     ma = mass_mul_diff(E, xa, E.qacc_s);
     mb = mass_mul_diff(E, xb, E.qacc_s);
-    c0 = 0.5f * (xa[LANE] - E.qacc_s[LANE]) * ma;
-    c1 = 0.5f * (xb[LANE] - E.qacc_s[LANE]) * mb;
+    c0 = 0.5f * (xa[nd] - E.qacc_s[nd]) * ma;
+    c1 = 0.5f * (xb[nd] - E.qacc_s[nd]) * mb;
   }
   const int nefc = E.nefc, nsingle = E.nsingle;
 #pragma unroll
@@ -1326,8 +1363,9 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
   CLK_DECL;
   float* G = lrow_of(E);  // 16 x 16 staging tile (the factor's space is free until the Cholesky)
   const int col = LANE & 15, rk = LANE >> 4;
-  const int d = min(LANE, 26);
-  const int bd = dof_blk(d), od = d - blk_d0(bd);
+  // the lane's dof (Newton lane layout): block LANE >> 4, offset LANE & 15 in it
+  const int nd = newton_dof(LANE), d = max(nd, 0);
+  const int bd = nd >= 0 ? LANE >> 4 : -2, od = LANE & 15;
 #pragma unroll
   for (int i = 0; i < 27; i++) hrow[i] = d < 9 ? (i < 9 ? E.M9[d][i] : 0.f) : (i == d ? E.Mc[d - 9] : 0.f);
   float gacc = 0.f;
@@ -1432,7 +1470,7 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
     PROBE(6, stats, STAT_T_AUX1);
   }
   PROBE(6, stats, STAT_T_AUX2);
-  return LANE < 27 ? gacc + mdx : 0.f;
+  return nd >= 0 ? gacc + mdx : 0.f;
 }
 
 // Incremental form of hess_grad_mfma for the Newton iterations after the first.  Over a line
@@ -1451,8 +1489,8 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
 DEV float hess_grad_delta(EnvSh& E, float* hrow, const unsigned long long* gm) {
   float* G = lrow_of(E);
   const int col = LANE & 15, rk = LANE >> 4;
-  const int d = min(LANE, 26);
-  const int bd = dof_blk(d), od = d - blk_d0(bd);
+  const int nd = newton_dof(LANE);
+  const int bd = nd >= 0 ? LANE >> 4 : -2, od = LANE & 15;
   const float m_[4] = {rk == 0 ? 1.f : 0.f, rk == 1 ? 1.f : 0.f, rk == 2 ? 1.f : 0.f, rk == 3 ? 1.f : 0.f};
   const float c15 = col == 15 ? 1.f : 0.f;
   float gacc = 0.f;
@@ -1507,147 +1545,160 @@ DEV float hess_grad_delta(EnvSh& E, float* hrow, const unsigned long long* gm) {
     }
     SYNC();
   }
-  return LANE < 27 ? gacc : 0.f;
+  return nd >= 0 ? gacc : 0.f;
 }
 
-// The same contraction as ONE 32 x 32 tile in dof space (27 dofs + the gradient column 27) on
-// v_mfma_f32_32x32x2_f32, two rows of a group per MFMA step: lane l supplies A[dof i][row k] =
-// J[row k][slot of dof i] and B[row k][dof i] = (C B)[k][dof i], with i = l & 31 and k = l >> 5;
-// B's column 27 carries g_k, so column 27 of the tile is J' g.  No per-type staging / gather: the
-// group's header gives the dof -> slot map.  The tile is symmetric, so Hessian row j = column j,
-// which lanes j (rows = 0-3 mod 8) and j + 32 (rows = 4-7 mod 8) hold.
-#ifndef MMX_HESS32  // experiment switch; measured 1.63M vs 1.87M env steps/s for the per-type 16 x 16
-#define MMX_HESS32 0    // tiles: 4x the MFMA work (32 x 32 dof tile, 2 steps per group) on one chain
-#endif
-typedef float f32x16v __attribute__((ext_vector_type(16)));
-DEV float hess_grad_mfma32(EnvSh& E, int nefc, float* hrow, float mdx) {
-  float* stats = E.stats;
-  CLK_DECL;
-  const int i = LANE & 31, kk = LANE >> 5;
-  const int d = min(LANE, 26);
-  const float mk0 = kk == 0 ? 1.f : 0.f, mk1 = 1.f - mk0;
-  const float ci = i < 27 ? 1.f : 0.f, cg = i == 27 ? 1.f : 0.f;
-  f32x16v acc;
+// ---------------------------------------------------------------- Cholesky solves of H p = v
+// H is 27 x 27 and block-structured: the arm block (9 dofs) and three cube blocks (6 dofs each),
+// coupled only where a constraint row spans two blocks (cpl: 4 x 4 bit mask of block pairs).
+// Lanes hold rows in the Newton lane layout (hrow[i] = H[dof][i], columns in dof order); the
+// solution comes back in the same layout.
+
+// Block form (no cube-cube coupling): every cube block factors inside its own DPP row, pivots
+// broadcast with row_newbcast.  Without any coupling the four blocks factor in lockstep (9 pivot
+// steps for all of H; cube rows meet identity rows on their dummy lanes 6..8).  With arm-cube
+// coupling the arrow order holds: the three cube blocks first (6 lockstep steps), the arm lanes
+// forming their coupling columns L[arm][cube] and the Schur complement of the arm block as each
+// cube pivot passes (v_readlane of the cube rows' values), then the arm block (9 steps in row 0).
+// Each pivot lane collects the column of L that the transposed solve needs (c[m] = L[m][own],
+// block-relative; cx[i] = L[arm i][own] for a coupled cube lane) with one select per value it
+// reads anyway, so no LDS transpose.
+// block-relative row of the lane: its entries in its own block's columns (dummy lanes: identity)
+DEV void block_row(const float* hrow, float* hb) {
+  const int r = LANE >> 4, kk = LANE & 15;
+  const bool valid = r != 0 ? kk < 6 : kk < 9;
+  // 0/1 masks, not selects: a select chain over hrow[m + 6 r ...] is turned into a lane-indexed
+  // load, which moves hrow to scratch
+  const float m0 = r == 0 ? 1.f : 0.f, m1 = r == 1 ? 1.f : 0.f, m2 = r == 2 ? 1.f : 0.f, m3 = r == 3 ? 1.f : 0.f;
 #pragma unroll
-  for (int r = 0; r < 16; r++) acc[r] = 0.f;
-  PROBE(6, stats, STAT_T_AUX3);
-  auto groups = [&](auto from_lds, int g_begin, int g_end) {
-    constexpr bool LDS = decltype(from_lds)::value;
-    for (int g0 = g_begin; g0 < g_end; g0 += 4) {
-      const int h = E.hdr[g0];  // the group's rows share their blocks
-      const int slot = i < 27 ? row_slot(h, i) : (i == 27 ? 15 : -1);
-      const int sl = max(slot, 0);
-      const float valid = slot >= 0 ? 1.f : 0.f;
-      float jg[4];
-      float4 nc4, d4;
-      if (LDS) {
+  for (int m = 0; m < 9; m++) {
+    const float vv = m < 6 ? fmaf(m3, hrow[21 + m], fmaf(m2, hrow[15 + m], fmaf(m1, hrow[9 + m], m0 * hrow[m]))) : m0 * hrow[m];
+    hb[m] = valid ? vv : (m == kk ? 1.f : 0.f);
+  }
+}
+// no coupling at all: the four blocks factor in lockstep (9 pivot steps; cube rows meet identity
+// rows on their dummy lanes 6..8), forward solve riding along
+DEV float chol_block_free(const float* hrow, float v) {
+  const int r = LANE >> 4, kk = LANE & 15;
+  const bool valid = r != 0 ? kk < 6 : kk < 9;
+  float hb[9], c[9], dinv[9];
+  block_row(hrow, hb);
 #pragma unroll
-        for (int m = 0; m < 4; m++) jg[m] = E.J[g0 + m][sl];
-        nc4 = *reinterpret_cast<const float4*>(&E.NC[g0]);
-        d4 = *reinterpret_cast<const float4*>(&E.D[g0]);
-      } else {
+  for (int m = 0; m < 9; m++) c[m] = 0.f;
+  float y = valid ? v : 0.f;
 #pragma unroll
-        for (int m = 0; m < 4; m++) jg[m] = ovf_j(E, g0 + m)[sl];
-        nc4 = make_float4(*ovf_nc(E, g0), *ovf_nc(E, g0 + 1), *ovf_nc(E, g0 + 2), *ovf_nc(E, g0 + 3));
-        d4 = make_float4(*ovf_d(E, g0), *ovf_d(E, g0 + 1), *ovf_d(E, g0 + 2), *ovf_d(E, g0 + 3));
+  for (int k = 0; k < 9; k++) {
+    const float d = fmaxf(row_bcast(hb[k], k), 1e-20f);
+    const float inv = __builtin_amdgcn_rsqf(d), sd = d * inv;
+    dinv[k] = inv;
+    const float l = kk == k ? sd : hb[k] * inv;  // lanes after the pivot: L[own][k]
+    hb[k] = l;
+    const float yk = row_bcast(y, k) * inv;
+    y = kk == k ? yk : (kk > k ? fmaf(-l, yk, y) : y);
+#pragma unroll
+    for (int m = k + 1; m < 9; m++) {
+      const float lm = row_bcast(l, m);
+      hb[m] = fmaf(-lm, l, hb[m]);
+      c[m] = kk == k ? lm : c[m];
+    }
+  }
+#pragma unroll
+  for (int k = 8; k >= 0; k--) {  // L' z = y
+    const float zk = row_bcast(y, k) * dinv[k];
+    y = kk == k ? zk : (kk < k ? fmaf(-c[k], zk, y) : y);
+  }
+  return valid ? y : 0.f;
+}
+// arm-cube coupling (a grasp), no cube-cube coupling: arrow order, the three cube blocks first (6
+// lockstep steps) with the arm lanes forming their coupling columns L[arm][cube] and the arm
+// block's Schur complement as each cube pivot passes (v_readlane of the cube rows' values), then
+// the arm block (9 steps in row 0); the transposed solve in reverse order
+DEV float chol_block_arm(const float* hrow, float v, int cpla) {
+  const int L = LANE, r = L >> 4, kk = L & 15;
+  const bool cube = r != 0;
+  const bool valid = cube ? kk < 6 : kk < 9;
+  float hb[9], c[9], cx[9], dinv[9], hx[18];
+  block_row(hrow, hb);
+#pragma unroll
+  for (int m = 0; m < 9; m++) {
+    c[m] = 0.f;
+    cx[m] = 0.f;
+  }
+#pragma unroll
+  for (int m = 0; m < 18; m++) hx[m] = hrow[9 + m];  // arm lanes: the coupling columns
+  float y = valid ? v : 0.f;
+#pragma unroll
+  for (int k = 0; k < 6; k++) {  // the cube blocks (arm lanes: l = 0, untouched)
+    const float d = fmaxf(row_bcast(hb[k], k), 1e-20f);
+    const float inv = __builtin_amdgcn_rsqf(d), sd = d * inv;
+    dinv[k] = inv;
+    const float l = cube ? (kk == k ? sd : hb[k] * inv) : 0.f;
+    hb[k] = cube ? l : hb[k];
+    const float yk = row_bcast(y, k) * inv;
+    y = cube ? (kk == k ? yk : (kk > k ? fmaf(-l, yk, y) : y)) : y;
+#pragma unroll
+    for (int m = k + 1; m < 6; m++) {
+      const float lm = row_bcast(l, m);
+      hb[m] = fmaf(-lm, l, hb[m]);
+      c[m] = cube && kk == k ? lm : c[m];
+    }
+#pragma unroll
+    for (int b = 1; b < 4; b++) {
+      if (!((cpla >> b) & 1)) continue;  // uniform
+      const float invb = readlane_f(inv, 16 * b);
+      const float la = cube ? 0.f : hx[6 * (b - 1) + k] * invb;  // arm lane j: L[j][cube pivot]
+      hx[6 * (b - 1) + k] = la;
+#pragma unroll
+      for (int m = k + 1; m < 6; m++) hx[6 * (b - 1) + m] = fmaf(-readlane_f(l, 16 * b + m), la, hx[6 * (b - 1) + m]);
+#pragma unroll
+      for (int i = 0; i < 9; i++) {  // Schur complement of the arm block
+        const float li = readlane_f(la, i);
+        hb[i] = fmaf(-li, la, hb[i]);
+        cx[i] = L == 16 * b + k ? li : cx[i];
       }
+      y = fmaf(-la, readlane_f(y, 16 * b + k), y);  // the cube pivot's y is final
+    }
+  }
+  if (!cube) {
 #pragma unroll
-      for (int m = 0; m < 4; m++) jg[m] *= valid;
-      const float s123 = fmaf(nc4.y, jg[1], fmaf(nc4.z, jg[2], nc4.w * jg[3]));  // normal row's coupling
+    for (int k = 0; k < 9; k++) {  // the arm block, row 0
+      const float d = fmaxf(row_bcast(hb[k], k), 1e-20f);
+      const float inv = __builtin_amdgcn_rsqf(d), sd = d * inv;
+      dinv[k] = inv;
+      const float l = kk == k ? sd : hb[k] * inv;
+      hb[k] = l;
+      const float yk = row_bcast(y, k) * inv;
+      y = kk == k ? yk : (kk > k ? fmaf(-l, yk, y) : y);
 #pragma unroll
-      for (int st = 0; st < 2; st++) {  // rows 2 st + kk of the group
-        const float own = st == 0 ? fmaf(mk0, jg[0], mk1 * jg[1]) : fmaf(mk0, jg[2], mk1 * jg[3]);
-        const float dr = st == 0 ? fmaf(mk0, d4.x, mk1 * d4.y) : fmaf(mk0, d4.z, mk1 * d4.w);
-        const float ncr = st == 0 ? mk1 * nc4.y : fmaf(mk0, nc4.z, mk1 * nc4.w);  // C_nk (0 for the normal row)
-        const float cpl = st == 0 ? fmaf(ncr, jg[0], mk0 * s123) : ncr * jg[0];
-        const float a = ci * own;
-        const float b = fmaf(ci, fmaf(dr, own, cpl), cg * own);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+      for (int m = k + 1; m < 9; m++) {
+        const float lm = row_bcast(l, m);
+        hb[m] = fmaf(-lm, l, hb[m]);
+        c[m] = kk == k ? lm : c[m];
       }
     }
-  };
-  const int split = min(nefc, MMX_LDSEFC);
-  groups(std::true_type{}, 0, split);
-  if (split < nefc) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the overflow rows' stores (ovf_fence)
-    groups(std::false_type{}, split, nefc);
-  }
-  PROBE(6, stats, STAT_T_AUX0);
-  // column 27 (the gradient) through LDS; the other half of each column from lane l ^ 32
-  float* G = lrow_of(E);
-  if (i == 27) {
 #pragma unroll
-    for (int r = 0; r < 16; r++) G[(r >> 2) * 8 + 4 * kk + (r & 3)] = acc[r];
+    for (int k = 8; k >= 0; k--) {  // L' z = y: the arm block (eliminated last) first
+      const float zk = row_bcast(y, k) * dinv[k];
+      y = kk == k ? zk : (kk < k ? fmaf(-c[k], zk, y) : y);
+    }
   }
-  float oth[16];
 #pragma unroll
-  for (int r = 0; r < 16; r++) oth[r] = __shfl_xor(acc[r], 32);
+  for (int i = 0; i < 9; i++) y = fmaf(-cx[i], readlane_f(y, i), y);  // (cx = 0 off the coupled cubes)
 #pragma unroll
-  for (int m = 0; m < 27; m++) {
-    const int r = (m >> 3) * 4 + (m & 3);
-    const float tile = ((m >> 2) & 1) ? oth[r] : acc[r];
-    hrow[m] = tile + (d < 9 ? (m < 9 ? E.M9[d][m] : 0.f) : (m == d ? E.Mc[d - 9] : 0.f));
+  for (int k = 5; k >= 0; k--) {
+    const float zk = row_bcast(y, k) * dinv[k];
+    y = cube ? (kk == k ? zk : (kk < k ? fmaf(-c[k], zk, y) : y)) : y;
   }
-  SYNC();
-  const float g = LANE < 27 ? G[LANE] + mdx : 0.f;
-  SYNC();
-  PROBE(6, stats, STAT_T_AUX1);
-  return g;
+  return valid ? y : 0.f;
 }
 
-// Returns (H^{-1} v)_j in lane j for H given by rows hrow (lane j = row j, j < 27) and v_j.  The
-// factor stays in registers: lane j holds row j of L (h[m] = L[j][m], m <= j) and column j of L
-// (c[i] = L[i][j], i >= j); cross-lane values move with v_readlane.
-DEV float chol_solve_reg(EnvSh& E, const float* hrow, float v) {
-  const int j = LANE;
-  float h[27], dinv[27];
-#pragma unroll
-  for (int i = 0; i < 27; i++) h[i] = hrow[i];
-#pragma unroll
-  for (int k = 0; k < 27; k++) {
-    const float d = fmaxf(readlane_f(h[k], k), 1e-20f);
-    const float sd = __builtin_amdgcn_sqrtf(d), inv = __builtin_amdgcn_rcpf(sd);
-    dinv[k] = inv;
-    const float l = j == k ? sd : h[k] * inv;  // lane j >= k: L[j][k]
-    h[k] = l;
-#pragma unroll
-    for (int i = k + 1; i < 27; i++) h[i] = fmaf(-readlane_f(l, i), l, h[i]);
-  }
-  float y = j < 27 ? v : 0.f;
-#pragma unroll
-  for (int k = 0; k < 27; k++) {  // L y = v
-    const float yk = readlane_f(y, k) * dinv[k];
-    y = j == k ? yk : (j > k ? fmaf(-h[k], yk, y) : y);
-  }
-  // columns of L for the transposed solve: rows out to LDS, columns back in
-  const int jc = min(j, 26);
-  if (j < 27) {
-#pragma unroll
-    for (int m = 0; m < 27; m++) lrow_of(E)[27 * j + m] = h[m];
-  }
-  SYNC();
-  float c[27];
-#pragma unroll
-  for (int k = 0; k < 27; k++) c[k] = lrow_of(E)[27 * k + jc];  // L[k][j]
-#pragma unroll
-  for (int k = 26; k >= 0; k--) {  // L' z = y
-    const float zk = readlane_f(y, k) * dinv[k];
-    y = j == k ? zk : (j < k ? fmaf(-c[k], zk, y) : y);
-  }
-  SYNC();
-  return y;
-}
-
-// Arrow-ordered register Cholesky solve: pivots in the order cube 1, cube 2, cube 3, arm, and a
-// pivot only updates the blocks it is coupled to (cpl: 4 x 4 bit mask of block pairs sharing a
-// constraint row, plus the fill-in eliminating a block creates among the blocks after it).
-// Uncoupled cubes cost a 6 x 6 factorisation each instead of touching all 27 rows; a grasped cube
-// adds its 6 x 9 coupling to the arm.  Same layout as chol_solve_reg: lane j = dof j.
+// General arrow-ordered register Cholesky (any coupling, incl. cube-cube): pivots in the order
+// cube 1, cube 2, cube 3, arm, and a pivot only updates the blocks it is coupled to (cpl plus the
+// fill-in eliminating a block creates among the blocks after it); cross-lane values by
+// v_readlane from the dof's lane, columns of L for the transposed solve through an LDS transpose.
 DEV float chol_solve_arrow(EnvSh& E, const float* hrow, float v, int cpl) {
-  float* stats = E.stats;
-  CLK_DECL;
-  const int j = LANE;
-  const int pj = j < 9 ? j + 18 : (j < 27 ? j - 9 : 1000);  // elimination position of dof j
+  const int j = newton_dof(LANE);
+  const int pj = j < 0 ? 1000 : (j < 9 ? j + 18 : j - 9);  // elimination position of dof j
   float h[27], dinv[27];
 #pragma unroll
   for (int i = 0; i < 27; i++) h[i] = hrow[i];
@@ -1655,7 +1706,7 @@ DEV float chol_solve_arrow(EnvSh& E, const float* hrow, float v, int cpl) {
   for (int pi = 0; pi < 27; pi++) {
     const int p = pi < 18 ? pi + 9 : pi - 18;
     const int bp = p < 9 ? 0 : 1 + (p - 9) / 6;
-    const float d = fmaxf(readlane_f(h[p], p), 1e-20f);
+    const float d = fmaxf(readlane_f(h[p], newton_lane(p)), 1e-20f);
     const float inv = __builtin_amdgcn_rsqf(d), sd = d * inv;  // one transcendental per pivot
     dinv[p] = inv;
     const float l = j == p ? sd : h[p] * inv;  // lanes after p: L[j][p]
@@ -1670,7 +1721,7 @@ DEV float chol_solve_arrow(EnvSh& E, const float* hrow, float v, int cpl) {
         for (int k = 0; k < nB; k++) {
           const int i = dB + k;
           const int qi = i < 9 ? i + 18 : i - 9;
-          if (qi > pi) h[i] = fmaf(-readlane_f(l, i), l, h[i]);
+          if (qi > pi) h[i] = fmaf(-readlane_f(l, newton_lane(i)), l, h[i]);
         }
       }
     }
@@ -1679,25 +1730,23 @@ DEV float chol_solve_arrow(EnvSh& E, const float* hrow, float v, int cpl) {
 #pragma unroll
       for (int x = 0; x < 4; x++)
 #pragma unroll
-        for (int y = 0; y < 4; y++) {
-          const bool later_x = x == 0 || x > bp, later_y = y == 0 || y > bp;
-          if (x != y && later_x && later_y && x != bp && y != bp && ((cpl >> (4 * bp + x)) & 1) &&
-              ((cpl >> (4 * bp + y)) & 1))
-            cpl |= 1 << (4 * x + y);
+        for (int yb = 0; yb < 4; yb++) {
+          const bool later_x = x == 0 || x > bp, later_y = yb == 0 || yb > bp;
+          if (x != yb && later_x && later_y && x != bp && yb != bp && ((cpl >> (4 * bp + x)) & 1) &&
+              ((cpl >> (4 * bp + yb)) & 1))
+            cpl |= 1 << (4 * x + yb);
         }
     }
   }
-  PROBE(9, stats, STAT_T_AUX0);
-  float y = j < 27 ? v : 0.f;
+  float y = j >= 0 ? v : 0.f;
 #pragma unroll
   for (int pi = 0; pi < 27; pi++) {  // L y = v in elimination order
     const int p = pi < 18 ? pi + 9 : pi - 18;
-    const float yk = readlane_f(y, p) * dinv[p];
+    const float yk = readlane_f(y, newton_lane(p)) * dinv[p];
     y = j == p ? yk : (pj > pi ? fmaf(-h[p], yk, y) : y);
   }
-  PROBE(9, stats, STAT_T_AUX1);
-  const int jc = min(j, 26);
-  if (j < 27) {
+  const int jc = max(j, 0);
+  if (j >= 0) {
 #pragma unroll
     for (int m = 0; m < 27; m++) lrow_of(E)[27 * j + m] = h[m];
   }
@@ -1705,15 +1754,30 @@ DEV float chol_solve_arrow(EnvSh& E, const float* hrow, float v, int cpl) {
   float c[27];
 #pragma unroll
   for (int k = 0; k < 27; k++) c[k] = lrow_of(E)[27 * k + jc];  // L[k][j]
-  PROBE(9, stats, STAT_T_AUX2);
 #pragma unroll
   for (int pi = 26; pi >= 0; pi--) {  // L' z = y
     const int p = pi < 18 ? pi + 9 : pi - 18;
-    const float zk = readlane_f(y, p) * dinv[p];
+    const float zk = readlane_f(y, newton_lane(p)) * dinv[p];
     y = j == p ? zk : (pj < pi ? fmaf(-c[p], zk, y) : y);
   }
   SYNC();
-  PROBE(9, stats, STAT_T_AUX3);
+  return j >= 0 ? y : 0.f;
+}
+
+#ifndef MMX_CHOL_BLOCK
+#define MMX_CHOL_BLOCK 1  // 0: the arrow form for every solve (A/B switch)
+#endif
+// H^{-1} v: the block form unless two cubes are coupled (a cube resting on or pushing another)
+DEV float chol_solve(EnvSh& E, const float* hrow, float v, int cpl) {
+  float* stats = E.stats;
+  CLK_DECL;
+  const bool cube_cube = !MMX_CHOL_BLOCK || (cpl & 0x6AC0) != 0;  // bits 4 x + y with x, y in 1..3, x != y
+  const float y = cube_cube ? chol_solve_arrow(E, hrow, v, cpl)
+                            : ((cpl & 0xE) ? chol_block_arm(hrow, v, cpl & 0xE) : chol_block_free(hrow, v));
+  // probe set 9: cycles of the uncoupled / arm-coupled / cube-cube solves; AUX3 counts the
+  // arm-coupled solves + 1000 x the cube-cube ones
+  PROBE(9, stats, cube_cube ? STAT_T_AUX1 : ((cpl & 0xE) ? STAT_T_AUX2 : STAT_T_AUX0));
+  if (MMX_PROBE == 9 && LANE == 0) stats[STAT_T_AUX3] += cube_cube ? 1000.f : ((cpl & 0xE) ? 1.f : 0.f);
   return y;
 }
 
@@ -1734,9 +1798,10 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
   float c_ws, c_s, ra[RPL], rs[RPL], mws, ms;
   cost2_wave(E, E.ws, E.qacc_s, mu, dd, c_ws, c_s, ra, rs, mws, ms);
   const bool from_ws = c_ws < c_s;
-  if (LANE < 27) E.x[LANE] = from_ws ? E.ws[LANE] : E.qacc_s[LANE];
+  const int nd = newton_dof(LANE);  // the lane's dof in the Newton lane layout (-1: none)
+  if (nd >= 0) E.x[nd] = from_ws ? E.ws[nd] : E.qacc_s[nd];
   float mdx = from_ws ? mws : ms;  // (M (x - xs))_lane, kept current through the iterations
-  float scale = LANE < 27 ? E.qfrc[LANE] * E.qfrc[LANE] : 0.f;
+  float scale = nd >= 0 ? E.qfrc[nd] * E.qfrc[nd] : 0.f;
   scale = sqrtf(wave_sum(scale)) + 1.f;
   float rr[RPL], jp[RPL];  // basis-row residuals J x - aref and J p
 #pragma unroll
@@ -1806,17 +1871,13 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
     if (delta) {
       g = gpred + hess_grad_delta(E, hrow, gm);
     } else {
-#if MMX_HESS32
-      g = hess_grad_mfma32(E, nefc, hrow, mdx);
-#else
       g = hess_grad_mfma(E, nefc, hrow, mdx);
-#endif
     }
     resid = sqrtf(wave_sum(g * g)) / scale;
     PROBE(1, stats, STAT_T_AUX1);
     if (resid < tol) break;
-    const float pj = chol_solve_arrow(E, hrow, -g, cpl);
-    if (LANE < 27) E.p[LANE] = pj;
+    const float pj = chol_solve(E, hrow, -g, cpl);
+    if (nd >= 0) E.p[nd] = pj;
     SYNC();
     float hp = 0.f;  // (H p)_lane: the gradient's change per unit step while no edge changes state
 #pragma unroll
@@ -1841,9 +1902,9 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
     }
     PROBE(10, stats, STAT_T_AUX0);
     float c0 = 0.f, c1 = 0.f, mp = 0.f;
-    if (LANE < 27) {
+    if (nd >= 0) {
       mp = mass_mul(E, E.p);
-      c0 = mp * (E.x[LANE] - E.qacc_s[LANE]);
+      c0 = mp * (E.x[nd] - E.qacc_s[nd]);
       c1 = mp * pj;
     }
     c0 = wave_sum(c0);
@@ -1877,8 +1938,8 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
     PROBE(1, stats, STAT_T_AUX3);
     PROBE(10, stats, STAT_T_AUX2);
     float stepn = 0.f;
-    if (LANE < 27) {
-      E.x[LANE] += alpha * pj;
+    if (nd >= 0) {
+      E.x[nd] += alpha * pj;
       stepn = alpha * alpha * pj * pj;
     }
     mdx = fmaf(alpha, mp, mdx);
@@ -1897,7 +1958,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
       it++;
       break;
     }
-    gpred = LANE < 27 ? fmaf(alpha, hp, g) : 0.f;
+    gpred = nd >= 0 ? fmaf(alpha, hp, g) : 0.f;
     if (__ballot(flip) == 0ull) {
       // same active set: H is unchanged, so g(x + a p) = g + a H p exactly; when that already
       // meets the tolerance the confirming Hessian pass is skipped
