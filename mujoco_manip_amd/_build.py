@@ -27,7 +27,9 @@ DEVICE_MATH = ["-Xarch_device", "-freciprocal-math", "-Xarch_device", "-fapprox-
 # budget the 2-waves-per-SIMD occupancy allows) measured +6.4 % env steps/s over the default
 # occupancy-driven scheduler on the C3 bench (max-ilp +2 %, max-memory-clause +0 %).  The option
 # is an LLVM backend flag; the host compile accepts and ignores it.
-DEVICE_SCHED = ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"]
+DEVICE_SCHED = ["-mllvm", "-amdgpu-sched-strategy=" + os.environ.get("MMX_SCHED", "iterative-ilp")]
+if os.environ.get("MMX_SCHED") == "default":  # experiments: the backend's default scheduler
+    DEVICE_SCHED = []
 # no SLP vectorisation in device code: at -O3 it packs pairs of independent fp32 ops into
 # v_pk_fma_f32 / v_pk_mul_f32 on even-aligned register pairs (2,700 packed ops in the substep); the
 # pairing constraints raised the substep's register pressure into scratch spills (frame 480 -> 172 B)

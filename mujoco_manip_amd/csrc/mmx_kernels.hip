@@ -431,13 +431,25 @@ DEV RI ri_load(const float* d) {
 
 #define LT(r, c) ((r) * ((r) + 1) / 2 + (c))
 
-// RNE bias of the arm + composite inertias (for CRBA), one lane per moving arm body (2..11).  A body's velocity and
-// acceleration are running sums over the joints on its root path (arm_anc), its force is local;
-// subtree sums of force and inertia (the backward pass and the composite inertia) are gathers
-// over descendants.  Scratch at SCR_DYN: per body frc (6) + inertia (10), then subtree force (6).
+// RNE bias of the arm + composite inertias (for CRBA), one lane per moving arm body (2..11).  A
+// body's velocity and acceleration are running sums over the joints on its root path (arm_anc),
+// its force is local.  Lane l < 10 holds body b = 11 - l (the fingers 11, 10, then the chain 9..2),
+// so a body's subtree (bodies >= b for b <= 9, itself for a finger) is an inclusive prefix over
+// lanes 0..l: the backward pass and the composite inertias are 16 DPP row_shr scans in registers.
+// Scratch at SCR_DYN: subtree force (6) per body at 16 * 12, composite inertias at SCR_IC.
+DEV float shr_add_scan(float v) {  // inclusive prefix sum over the lanes of each 16-lane row
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xF, 0xF, false));  // row_shr:1
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x112, 0xF, 0xF, false));  // row_shr:2
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x114, 0xF, 0xF, false));  // row_shr:4
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x118, 0xF, 0xF, false));  // row_shr:8
+  return v;
+}
 DEV void rne_wave(EnvSh& E) {
   float* F = scr_of(E) + SCR_DYN;
-  const int b = LANE + 2;
+  const int b = 11 - LANE;
+  float fi[16];  // the body's force (6), then its inertia (m, h, J: 10)
+#pragma unroll
+  for (int m = 0; m < 16; m++) fi[m] = 0.f;
   if (LANE < 10) {
     const RI Ib = body_inertia(E, b);
     SV vel = SV{V3{0.f, 0.f, 0.f}, V3{0.f, 0.f, 0.f}};
@@ -451,29 +463,20 @@ DEV void rne_wave(EnvSh& E) {
       }
     }
     const SV f = rimul(Ib, acc) + cross_force(vel, rimul(Ib, vel));
-    float* o = F + 16 * b;
-    o[0] = f.w.x; o[1] = f.w.y; o[2] = f.w.z; o[3] = f.v.x; o[4] = f.v.y; o[5] = f.v.z;
-    ri_store(o + 6, Ib);
+    fi[0] = f.w.x; fi[1] = f.w.y; fi[2] = f.w.z; fi[3] = f.v.x; fi[4] = f.v.y; fi[5] = f.v.z;
+    ri_store(fi + 6, Ib);
   }
-  SYNC();
-  if (LANE < 10) {  // subtree sums: b is an ancestor-or-self of k
-    float fs[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, is[10];
 #pragma unroll
-    for (int m = 0; m < 10; m++) is[m] = 0.f;
+  for (int m = 0; m < 16; m++) {  // subtree sums (lanes >= 10 hold zeros and come after)
+    const float sm = shr_add_scan(fi[m]);
+    fi[m] = LANE == 1 ? fi[m] : sm;  // finger 10: its own subtree only (finger 11 sits before it)
+  }
+  if (LANE < 10) {
 #pragma unroll
-    for (int k = 11; k >= 2; k--) {
-      const bool in = b <= 9 ? k >= b : k == b;
-      const float* o = F + 16 * k;
-#pragma unroll
-      for (int m = 0; m < 6; m++) fs[m] += in ? o[m] : 0.f;
-#pragma unroll
-      for (int m = 0; m < 10; m++) is[m] += in ? o[6 + m] : 0.f;
-    }
-#pragma unroll
-    for (int m = 0; m < 10; m++) (scr_of(E) + SCR_IC)[10 * b + m] = is[m];
+    for (int m = 0; m < 10; m++) (scr_of(E) + SCR_IC)[10 * b + m] = fi[6 + m];
     float* o = F + 16 * 12 + 6 * b;
 #pragma unroll
-    for (int m = 0; m < 6; m++) o[m] = fs[m];
+    for (int m = 0; m < 6; m++) o[m] = fi[m];
   }
   SYNC();
   if (LANE < 9) {
@@ -482,7 +485,6 @@ DEV void rne_wave(EnvSh& E) {
   }
   SYNC();
 }
-
 
 // (A^{-1} v)_j in lane j for a small SPD A given by rows (lane j holds row j in arow[0..N)).
 // Right-looking Cholesky with v_readlane broadcasts; lane k keeps column k of L (selects) for
