@@ -56,6 +56,17 @@ static constexpr float kHome[7] = {1.5708f, -0.2f, 0.0f, -2.1f, 0.0f, 1.8f, 0.78
 static constexpr int kBinBody[3] = {MMX_BODY_BIN_RED, MMX_BODY_BIN_GREEN, MMX_BODY_BIN_BLUE};
 
 #define NSLOT 14  // arm bodies 1..11 -> slots 0..10, cubes 16..18 -> slots 11..13
+#ifdef MMX_TWO_WAVE
+static constexpr bool kTwoWave = true;
+#else
+static constexpr bool kTwoWave = false;
+#endif
+#ifndef MMX_CAND_CAP
+#define MMX_CAND_CAP 160      // persistent broadphase list entries (pair indices)
+#endif
+#ifndef MMX_CAND_MARGIN
+#define MMX_CAND_MARGIN 0.08f  // m: the list's inflation of the sphere / plane test (A/B: 0.04 +0.2 %, 0.08 +0.8 %, 0.15 -0.6 %)
+#endif
 #define LD 28     // padded row stride for 27-wide rows
 
 // ============================================================================ per-env LDS
@@ -96,6 +107,14 @@ struct EnvSh {
   int tbase[11];  // rows are grouped by block-pair type: type t owns rows [tbase[t], tbase[t+1])
   int act_free;  // bit a: actuator a's force is inside its forcerange (its kv enters qDeriv)
   float stats[STAT_N];  // lane 0 accumulates; loaded / stored with the env record
+  // persistent broadphase list (collide_prune): the pairs within MMX_CAND_MARGIN of contact when it
+  // was built, in pair order; valid while the bodies' accumulated displacement bound stays under
+  // half the margin.  ncand < 0: no valid list (every record load invalidates it).
+  float cdisp;     // bound on any geom's displacement since the build (x 2: a pair's relative one)
+  float crad;      // max over moving geoms of |geom centre - body origin| + bounding radius
+  float cva, cwa;  // this substep's max arm-body origin speed and angular speed (from the RNE)
+  int ncand;
+  unsigned short cand[MMX_CAND_CAP];
 };
 // The workgroup's env lives in one file-scope LDS object: the non-inlined substep function below
 // reaches it by symbol (LDS address space), not through a generic pointer.
@@ -244,6 +263,16 @@ DEV float wave_sum(float v) {
           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16))) +
          (__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)) +
           __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48)));
+}
+DEV float readlane_max0(float v) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)); }
+DEV float wave_max(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  v = fmaxf(v, dpp_f<0x140>(v));
+  return fmaxf(fmaxf(readlane_max0(v), __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16))),
+               fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)),
+                     __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48))));
 }
 // wave64 inclusive prefix sum: DPP row_shr butterflies inside each row of 16 lanes, then the
 // row totals (v_readlane) are added to the rows above
@@ -450,6 +479,7 @@ DEV void rne_wave(EnvSh& E) {
   float fi[16];  // the body's force (6), then its inertia (m, h, J: 10)
 #pragma unroll
   for (int m = 0; m < 16; m++) fi[m] = 0.f;
+  float vmax = 0.f, wmax = 0.f;  // for collide_prune's displacement bound
   if (LANE < 10) {
     const RI Ib = body_inertia(E, b);
     SV vel = SV{V3{0.f, 0.f, 0.f}, V3{0.f, 0.f, 0.f}};
@@ -463,6 +493,8 @@ DEV void rne_wave(EnvSh& E) {
       }
     }
     const SV f = rimul(Ib, acc) + cross_force(vel, rimul(Ib, vel));
+    vmax = norm(vel.v + cross(vel.w, body_x(E, b)));  // speed of the body origin
+    wmax = norm(vel.w);
     fi[0] = f.w.x; fi[1] = f.w.y; fi[2] = f.w.z; fi[3] = f.v.x; fi[4] = f.v.y; fi[5] = f.v.z;
     ri_store(fi + 6, Ib);
   }
@@ -482,6 +514,12 @@ DEV void rne_wave(EnvSh& E) {
   if (LANE < 9) {
     const float* o = F + 16 * 12 + 6 * MMX_jnt_body[LANE];
     (scr_of(E) + SCR_BIAS)[LANE] = sdot(load_S(E, LANE), SV{V3{o[0], o[1], o[2]}, V3{o[3], o[4], o[5]}});
+  }
+  vmax = wave_max(vmax);
+  wmax = wave_max(wmax);
+  if (LANE == 0) {
+    E.cva = vmax;
+    E.cwa = wmax;
   }
   SYNC();
 }
@@ -723,6 +761,27 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
   float* scr = &E.J[0][0];
   float* gx = scr + COL_GX;
   int* cand = reinterpret_cast<int*>(scr + COL_CAND);
+  // (2) runs over the persistent list when it is still valid: its pairs were within
+  // MMX_CAND_MARGIN of contact at the build, and no pair has since closed by more than the bound
+  // cdisp = sum over substeps of 2 dt (max body-origin speed + max angular speed x crad) (x 1.25
+  // for the integrators' second-order terms).  The list is in pair order, so the exact test below
+  // keeps the same candidates, in the same order, as the all-pairs pass.
+  bool use_list = false;
+  if (!kTwoWave && !only_ro && E.ncand >= 0) {  // (the two-wave step runs the RNE beside this)
+    float vc = 0.f;
+    if (LANE < 3) {
+      const int da = 9 + 6 * LANE;
+      vc = norm(V3{E.qvel[da], E.qvel[da + 1], E.qvel[da + 2]}) +
+           norm(V3{E.qvel[da + 3], E.qvel[da + 4], E.qvel[da + 5]}) * E.crad;
+    }
+    vc = fmaxf(fmaxf(readlane_max0(vc), __int_as_float(__builtin_amdgcn_readlane(__float_as_int(vc), 1))),
+               __int_as_float(__builtin_amdgcn_readlane(__float_as_int(vc), 2)));
+    const float inc = 1.25f * 2.f * kDt * fmaxf(fmaf(E.cwa, E.crad, E.cva), vc) + 1e-5f;
+    use_list = E.cdisp + inc < 0.5f * MMX_CAND_MARGIN;
+    SYNC();
+    if (LANE == 0) E.cdisp = use_list ? E.cdisp + inc : E.cdisp;
+  }
+  const bool rebuild = !kTwoWave && !only_ro && !use_list;
   if (LANE < MMX_NGEOM) {
     const Geom G = geom_pose(E, LANE);
     float* o = gx + GXS * LANE;
@@ -735,9 +794,40 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
     o[17] = MMX_geom_aabb[3 * LANE + 1];
     o[18] = MMX_geom_aabb[3 * LANE + 2];
   }
+  if (rebuild) {  // uniform: the moving geoms' extent about their body origins (rigid: any pose)
+    float ext = 0.f;
+    if (LANE < MMX_NGEOM) {
+      const int b = MMX_geom_body[LANE];
+      if (!MMX_body_static[b]) ext = norm(V3{gx[GXS * LANE], gx[GXS * LANE + 1], gx[GXS * LANE + 2]} - body_x(E, b)) +
+                                     MMX_geom_rbound[LANE];
+    }
+    ext = wave_max(ext);
+    if (LANE == 0) E.crad = ext;
+  }
   SYNC();
   PROBE(2, stats, STAT_T_AUX0);
-  // (2) sphere / plane-distance prune of all pairs: unrolled so the pair-table loads issue together
+  // (2) sphere / plane-distance prune
+  auto sphere_test = [&](int p, int pk, float infl) {
+    const int g1 = pk & 255, g2 = pk >> 8;
+    if (only_ro && !robot_obstacle(g1, g2)) return false;
+    const float* o1 = gx + GXS * g1;
+    const float* o2 = gx + GXS * g2;
+    const V3 d = V3{o2[0] - o1[0], o2[1] - o1[1], o2[2] - o1[2]};
+    if (__float_as_int(o1[13]) == GT_PLANE) return d.x * o1[5] + d.y * o1[8] + d.z * o1[11] <= o2[12] + infl;
+    const float rb = o1[12] + o2[12] + infl;
+    return dot(d, d) <= rb * rb;
+  };
+  int nc = 0;
+  if (use_list) {  // uniform: the list's pairs only (<= MMX_CAND_CAP, pair order)
+    const int n = E.ncand;
+    for (int k0 = 0; k0 < n; k0 += WG) {
+      const int k = k0 + LANE;
+      const int p = k < n ? (int)E.cand[k] : 0;
+      const bool keep = k < n && sphere_test(p, MMX_pair_packed[p], 0.f);
+      nc = wave_compact(keep, cand, nc, p);
+    }
+  } else {
+  // all pairs: unrolled so the pair-table loads issue together
   constexpr int NPASS = (MMX_NPAIR + WG - 1) / WG;
   int pg[NPASS];  // all pair-table loads in flight at once
 #pragma unroll
@@ -747,28 +837,14 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
   }
   // all tests first (ballot masks in SGPRs), compaction stores after: no LDS store between the
   // passes' gathers, so the compiler may keep several passes' loads in flight
-  unsigned long long km[NPASS];
+  unsigned long long km[NPASS], ki[NPASS];
 #pragma unroll
   for (int q = 0; q < NPASS; q++) {
     const int p = q * WG + LANE;
-    bool keep = false;
-    if (p < MMX_NPAIR) {
-      const int g1 = pg[q] & 255, g2 = pg[q] >> 8;
-      if (!only_ro || robot_obstacle(g1, g2)) {
-        const float* o1 = gx + GXS * g1;
-        const float* o2 = gx + GXS * g2;
-        const V3 d = V3{o2[0] - o1[0], o2[1] - o1[1], o2[2] - o1[2]};
-        if (__float_as_int(o1[13]) == GT_PLANE) {
-          keep = d.x * o1[5] + d.y * o1[8] + d.z * o1[11] <= o2[12];  // distance above the plane
-        } else {
-          const float rb = o1[12] + o2[12];
-          keep = dot(d, d) <= rb * rb;
-        }
-      }
-    }
-    km[q] = __ballot(keep);
+    km[q] = __ballot(p < MMX_NPAIR && sphere_test(p, pg[q], 0.f));
+    ki[q] = rebuild ? __ballot(p < MMX_NPAIR && sphere_test(p, pg[q], MMX_CAND_MARGIN)) : 0ull;
   }
-  int nc = 0;
+  int ni = 0;
 #pragma unroll
   for (int q = 0; q < NPASS; q++) {
     const unsigned long long m = km[q];
@@ -777,6 +853,17 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
       cand[nc + pos] = q * WG + LANE;
     }
     nc += __popcll(m);
+    if (rebuild) {  // the inflated set -> the persistent list (pair order)
+      const unsigned long long mi = ki[q];
+      const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(mi >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mi, 0u));
+      if (((mi >> LANE) & 1ull) && ni + pos < MMX_CAND_CAP) E.cand[ni + pos] = (unsigned short)(q * WG + LANE);
+      ni += __popcll(mi);
+    }
+  }
+  if (rebuild && LANE == 0) {
+    E.ncand = ni <= MMX_CAND_CAP ? ni : -1;
+    E.cdisp = 0.f;
+  }
   }
   SYNC();
   PROBE(2, stats, STAT_T_AUX1);
@@ -2632,6 +2719,9 @@ DEV void load_env(const MMXState& S, int i, EnvSh& E) {
     E.ncon = 0;
     E.nefc = 0;
     E.nefc_mj = 0;
+    E.ncand = -1;  // positions come from the record: rebuild the broadphase list
+    E.cva = 3e38f;
+    E.cwa = 3e38f;
   }
   SYNC();
 }
