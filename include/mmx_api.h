@@ -54,7 +54,7 @@ typedef struct {
   int8_t task_bin[9];
   int32_t fixed_task_obj;       /* -1: sample from the pool (gym_env.py:511-517) */
   int32_t fixed_task_bin;
-  int32_t image_size;           /* camera image side (multiple of 4, <= 1024); 0 = no rendering */
+  int32_t image_size;           /* camera image side (multiple of 16, <= 1024); 0 = no rendering */
   int32_t autoreset;            /* same-step autoreset on terminated/truncated/FSM done */
   int32_t solver_iterations;    /* Newton iteration cap (default 30) */
   float solver_tolerance;       /* relative gradient-norm tolerance (default 1e-6) */

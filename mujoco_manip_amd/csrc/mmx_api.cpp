@@ -181,7 +181,7 @@ void mmx_config_default(mmx_config* c) {
 int mmx_create(const mmx_config* cfg, mmx_sim** out) {
   if (!cfg || !out) return MMX_EINVAL;
   *out = nullptr;
-  if (cfg->image_size < 0 || cfg->image_size % 4 != 0 || cfg->image_size > 1024) return MMX_EINVAL;
+  if (cfg->image_size < 0 || cfg->image_size % 16 != 0 || cfg->image_size > 1024) return MMX_EINVAL;
   if (cfg->num_envs <= 0 || cfg->action_mode < 0 || cfg->action_mode > 4 || cfg->reward_type < 0 ||
       cfg->reward_type > 2 || cfg->n_tasks < 1 || cfg->n_tasks > 9)
     return MMX_EINVAL;

@@ -53,6 +53,10 @@ static constexpr int kSmallArea = MMR_SMALL_AREA; // bounding boxes up to this m
 #endif
 static constexpr int kGroup = MMR_GROUP;         // lanes per small triangle
 static constexpr int kMaxBig = 1024;
+#ifndef MMR_TPW
+#define MMR_TPW 2
+#endif
+static constexpr int kTPW = MMR_TPW;  // 16 x 16 tiles per wave and pass of the large-triangle queue
 
 // rows per band: the image split into the fewest bands that fit the z-buffer, balanced
 __host__ DEV int rend_band_rows(int S) {
@@ -129,6 +133,58 @@ DEV uint32_t rend_cover(const RTri& T, int t, int px, int py, float iz_lo, float
   const float q = fminf(fmaxf((iz - iz_lo) * iz_scale, 0.f), 1.f);
   const uint32_t d = 1u + (uint32_t)(q * 1048574.f);  // 1 .. 2^20 - 1 (0 = empty)
   return (d << 12) | (uint32_t)t;
+}
+
+// shading of 4 horizontally adjacent pixels (px .. px + 3, py) from their depth keys: flat face
+// light and material from tinfo / mrgb, the floor's checker where no triangle covers the pixel and
+// its ray meets the floor, the sky gradient elsewhere; RGB u8 (3 dwords) and segment ids (1 dword)
+DEV void shade4(const uint32_t* keys, int px0, int py, int Sz, float half, float f, const M3& cR, const V3& cx,
+                const V3& l_top, const V3& lp_cam, const uint32_t* tinfo, const float* mrgb, uint32_t* rgb_out,
+                uint32_t* seg_out) {
+  {
+    uint32_t rgbw[3] = {0u, 0u, 0u}, segw = 0u;
+    for (int u = 0; u < 4; u++) {
+      const int px = px0 + u;
+      const uint32_t key = keys[u];
+      const V3 dw = mul(cR, V3{(px + 0.5f - half) / f, -(py + 0.5f - half) / f, -1.f});  // world ray
+      float col[3];
+      int sid = 0;
+      const float s0 = -cx.z / dw.z;  // ray parameter at the floor plane z = 0
+      const float fx = cx.x + s0 * dw.x, fy = cx.y + s0 * dw.y;
+      if (key == 0u && dw.z < 0.f && fabsf(fx) <= MMR_FLOOR_HALF && fabsf(fy) <= MMR_FLOOR_HALF) {
+        // floor: checker (0.1 m squares) under the same lights as a face, evaluated per pixel
+        const float* mt = mrgb + 8 * MMR_FLOOR_MAT;
+        const V3 pc = mulT(cR, V3{fx, fy, 0.f} - cx);  // camera frame; the normal is l_top
+        const float light = fminf(0.3f + 0.6f * fmaxf(l_top.z, 0.f) + 0.8f +
+                                  0.4f * fmaxf(dot(l_top, normalize(lp_cam - pc)), 0.f), 3.99f);
+        sid = (int)mt[7];
+        const bool alt = ((int)floorf(fx / mt[6]) + (int)floorf(fy / mt[6])) & 1;
+        for (int k = 0; k < 3; k++) col[k] = fminf((alt ? mt[3 + k] : mt[k]) * light, 1.f);
+      } else if (key == 0u) {  // skybox gradient (rgb1 top -> rgb2 bottom, scene.xml:17-18)
+        const float sky = 0.5f * (dw.z * rsqrtf(dot(dw, dw)) + 1.f);
+        col[0] = 0.3f * sky; col[1] = 0.5f * sky; col[2] = 0.7f * sky;
+      } else {
+        const uint32_t ti = tinfo[key & 4095];
+        const float* mt = mrgb + 8 * (ti & 255);
+        const float light = (float)(ti >> 16) * (1.f / 16384.f);
+        sid = (int)mt[7];
+        bool alt = false;
+        if (mt[6] > 0.f) {  // floor checker: the ray meets the plane z = 0
+          const float s0 = -cx.z / dw.z;
+          alt = ((int)floorf((cx.x + s0 * dw.x) / mt[6]) + (int)floorf((cx.y + s0 * dw.y) / mt[6])) & 1;
+        }
+        for (int k = 0; k < 3; k++) col[k] = fminf((alt ? mt[3 + k] : mt[k]) * light, 1.f);
+      }
+      for (int k = 0; k < 3; k++) {
+        const uint32_t v8 = (uint32_t)(col[k] * 255.f + 0.5f);
+        const int byte = 3 * u + k;
+        rgbw[byte >> 2] |= v8 << (8 * (byte & 3));
+      }
+      segw |= (uint32_t)sid << (8 * u);
+    }
+    rgb_out[0] = rgbw[0]; rgb_out[1] = rgbw[1]; rgb_out[2] = rgbw[2];
+    seg_out[0] = segw;
+  }
 }
 
 extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, int env_base) {
@@ -255,71 +311,60 @@ extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, 
       }
     }
   }
-  const int nb = (MMR_SKIP & 2) ? 0 : min(nbig[0], kMaxBig);
-  for (int q = 0; q < nb; q++) {  // large triangles: the workgroup scans the box pixel-parallel
-    const int t = bigq[q];
-    RTri T;
-    rend_setup(vs, t, Sz, row0, row1, T);
-    const int w = T.bx1 - T.bx0 + 1, area = w * (T.by1 - T.by0 + 1);
-    const float rw = 1.f / (float)w;
-    for (int k = tid; k < area; k += RWG) {
-      const int r = (int)(((float)k + 0.5f) * rw);  // k / w, exact for these sizes (no integer divide)
-      const int px = T.bx0 + k - r * w, py = T.by0 + r;
-      const uint32_t key = rend_cover(T, t, px, py, iz_lo, iz_scale);
-      if (key) atomicMax(&zb[(py - row0) * Sz + px], key);
-    }
-  }
   __syncthreads();
 
-  // 4. shade, 4 pixels per lane (S is a multiple of 4): everything from LDS
-  const int npx = (row1 - row0) * Sz;
-  unsigned char* img = S.images + ((size_t)i * 2 + ci) * Sz * Sz * 3 + (size_t)row0 * Sz * 3;
-  unsigned char* seg = S.seg + ((size_t)i * 2 + ci) * Sz * Sz + (size_t)row0 * Sz;
-  for (int g = tid; g < ((MMR_SKIP & 4) ? 0 : npx / 4); g += RWG) {
-    uint32_t rgbw[3] = {0u, 0u, 0u}, segw = 0u;
-    for (int u = 0; u < 4; u++) {
-      const int p = 4 * g + u;
-      const int px = p % Sz, py = row0 + p / Sz;
-      const uint32_t key = zb[p];
-      const V3 dw = mul(cR, V3{(px + 0.5f - half) / f, -(py + 0.5f - half) / f, -1.f});  // world ray
-      float col[3];
-      int sid = 0;
-      const float s0 = -cx.z / dw.z;  // ray parameter at the floor plane z = 0
-      const float fx = cx.x + s0 * dw.x, fy = cx.y + s0 * dw.y;
-      if (key == 0u && dw.z < 0.f && fabsf(fx) <= MMR_FLOOR_HALF && fabsf(fy) <= MMR_FLOOR_HALF) {
-        // floor: checker (0.1 m squares) under the same lights as a face, evaluated per pixel
-        const float* mt = mrgb + 8 * MMR_FLOOR_MAT;
-        const V3 pc = mulT(cR, V3{fx, fy, 0.f} - cx);  // camera frame; the normal is l_top
-        const float light = fminf(0.3f + 0.6f * fmaxf(l_top.z, 0.f) + 0.8f +
-                                  0.4f * fmaxf(dot(l_top, normalize(lp_cam - pc)), 0.f), 3.99f);
-        sid = (int)mt[7];
-        const bool alt = ((int)floorf(fx / mt[6]) + (int)floorf(fy / mt[6])) & 1;
-        for (int k = 0; k < 3; k++) col[k] = fminf((alt ? mt[3 + k] : mt[k]) * light, 1.f);
-      } else if (key == 0u) {  // skybox gradient (rgb1 top -> rgb2 bottom, scene.xml:17-18)
-        const float sky = 0.5f * (dw.z * rsqrtf(dot(dw, dw)) + 1.f);
-        col[0] = 0.3f * sky; col[1] = 0.5f * sky; col[2] = 0.7f * sky;
-      } else {
-        const uint32_t ti = tinfo[key & 4095];
-        const float* mt = mrgb + 8 * (ti & 255);
-        const float light = (float)(ti >> 16) * (1.f / 16384.f);
-        sid = (int)mt[7];
-        bool alt = false;
-        if (mt[6] > 0.f) {  // floor checker: the ray meets the plane z = 0
-          const float s0 = -cx.z / dw.z;
-          alt = ((int)floorf((cx.x + s0 * dw.x) / mt[6]) + (int)floorf((cx.y + s0 * dw.y) / mt[6])) & 1;
-        }
-        for (int k = 0; k < 3; k++) col[k] = fminf((alt ? mt[3 + k] : mt[k]) * light, 1.f);
-      }
-      for (int k = 0; k < 3; k++) {
-        const uint32_t v8 = (uint32_t)(col[k] * 255.f + 0.5f);
-        const int byte = 3 * u + k;
-        rgbw[byte >> 2] |= v8 << (8 * (byte & 3));
-      }
-      segw |= (uint32_t)sid << (8 * u);
+  // 4. large triangles + shading, fused, per 16 x 16 tile (S is a multiple of 16): each wave owns
+  // kTPW tiles at a time, lane l the 4 pixels (4 (l & 3) .. +3, l >> 2) of each.  A lane starts from
+  // the small triangles' depth keys in zb, walks the large-triangle queue once per tile batch (the
+  // setup uniform per wave: scalar table loads, LDS broadcasts), skips tiles outside a triangle's
+  // box or wholly outside one of its edges (12 corner tests, one per lane, one ballot), keeps the
+  // nearest key in registers and shades its pixels straight away: no depth atomics, no zb write
+  // back, no barrier between the large-triangle raster and the shading.
+  const int nb = (MMR_SKIP & 2) ? 0 : min(nbig[0], kMaxBig);
+  const int tcols = Sz >> 4, ntiles = tcols * ((row1 - row0 + 15) >> 4);
+  const int lane = tid & 63, lx = 4 * (lane & 3), ly = lane >> 2;
+  unsigned char* img = S.images + ((size_t)i * 2 + ci) * Sz * Sz * 3;
+  unsigned char* seg = S.seg + ((size_t)i * 2 + ci) * Sz * Sz;
+  for (int tb = (tid >> 6) * kTPW; tb < ((MMR_SKIP & 4) ? 0 : ntiles); tb += (RWG / 64) * kTPW) {
+    int tx[kTPW], ty[kTPW];
+    uint32_t best[kTPW][4];
+    for (int j = 0; j < kTPW; j++) {
+      const int tile = min(tb + j, ntiles - 1);  // a batch's spare tiles repeat the last one (not stored)
+      const int trow = tile / tcols;
+      tx[j] = (tile - trow * tcols) * 16;
+      ty[j] = row0 + trow * 16;
+      const int py = ty[j] + ly;
+      for (int u = 0; u < 4; u++) best[j][u] = py < row1 ? zb[(py - row0) * Sz + tx[j] + lx + u] : 0u;
     }
-    uint32_t* o = reinterpret_cast<uint32_t*>(img + 12 * (size_t)g);
-    o[0] = rgbw[0]; o[1] = rgbw[1]; o[2] = rgbw[2];
-    reinterpret_cast<uint32_t*>(seg)[g] = segw;
+    for (int q = 0; q < nb; q++) {
+      const int t = __builtin_amdgcn_readfirstlane((int)bigq[q]);
+      RTri T;
+      rend_setup(vs, t, Sz, row0, row1, T);
+      for (int j = 0; j < kTPW; j++) {
+        if (T.bx1 < tx[j] || T.bx0 > tx[j] + 15 || T.by1 < ty[j] || T.by0 > ty[j] + 15) continue;
+        {  // lane 4e + c: edge e at tile corner c; a tile whose 4 corners all lie outside one edge
+           // lies wholly outside the triangle (pixel centres of the tile's corner pixels)
+          const int e = min(lane >> 2, 2), c = lane & 3;
+          const float cx0 = tx[j] + ((c & 1) ? 15.5f : 0.5f), cy0 = ty[j] + ((c & 2) ? 15.5f : 0.5f);
+          const float xa = e == 0 ? T.x1 : (e == 1 ? T.x2 : T.x0), ya = e == 0 ? T.y1 : (e == 1 ? T.y2 : T.y0);
+          const float xb = e == 0 ? T.x2 : (e == 1 ? T.x0 : T.x1), yb = e == 0 ? T.y2 : (e == 1 ? T.y0 : T.y1);
+          const int ia = e == 0 ? T.i1 : (e == 1 ? T.i2 : T.i0), ib = e == 0 ? T.i2 : (e == 1 ? T.i0 : T.i1);
+          const uint64_t out = __ballot(lane < 12 && rend_edge(xa, ya, ia, xb, yb, ib, cx0, cy0) > 0.f);
+          if ((out & 0xFull) == 0xFull || (out & 0xF0ull) == 0xF0ull || (out & 0xF00ull) == 0xF00ull) continue;
+        }
+        for (int u = 0; u < 4; u++) {
+          const uint32_t key = rend_cover(T, t, tx[j] + lx + u, ty[j] + ly, iz_lo, iz_scale);
+          best[j][u] = max(best[j][u], key);
+        }
+      }
+    }
+    for (int j = 0; j < kTPW; j++) {
+      const int py = ty[j] + ly;
+      if (tb + j >= ntiles || py >= row1) continue;
+      const size_t p0 = (size_t)py * Sz + tx[j] + lx;  // image pixel of the lane's first pixel
+      shade4(best[j], tx[j] + lx, py, Sz, half, f, cR, cx, l_top, lp_cam, tinfo, mrgb,
+             reinterpret_cast<uint32_t*>(img + 3 * p0), reinterpret_cast<uint32_t*>(seg + p0));
+    }
   }
 }
 

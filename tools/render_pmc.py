@@ -1,0 +1,45 @@
+"""Condense tools/render_pmc.sh output: mean SQ counters per mmx_render_kernel dispatch (the last
+`--last` dispatches) and per workgroup / per pixel -> profiles/<round>_render_pmc.json.  Diagnostic."""
+import argparse
+import csv
+import glob
+import json
+import os
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--round", default="r02")
+    ap.add_argument("--prof", default=os.path.join(REPO, "gpurun_out", "rpmc"))
+    ap.add_argument("--last", type=int, default=32)
+    ap.add_argument("--wg-per-dispatch", type=int, default=2048 * 2 * 2)  # envs x cameras x bands (128^2)
+    ap.add_argument("--px-per-dispatch", type=int, default=2048 * 2 * 128 * 128)
+    a = ap.parse_args()
+    per = {}
+    for f in glob.glob(os.path.join(a.prof, "**", "*counter_collection.csv"), recursive=True):
+        pas = os.path.relpath(f, a.prof).split(os.sep)[0]
+        for r in csv.DictReader(open(f, newline="")):
+            if "mmx_render_kernel" not in r.get("Kernel_Name", ""):
+                continue
+            d = (pas, int(r.get("Dispatch_Id") or r.get("Correlation_Id")))
+            per.setdefault(d, {}).setdefault(r["Counter_Name"], 0.0)
+            per[d][r["Counter_Name"]] += float(r["Counter_Value"])
+    out = {}
+    for pas in sorted({p for p, _ in per}):
+        ds = sorted(d for d in per if d[0] == pas)[-a.last:]
+        for k in per[ds[0]]:
+            out[k] = sum(per[d][k] for d in ds) / len(ds)
+    res = {"kernel": "mmx_render_kernel", "source": "tools/render_pmc.sh (C5, 128^2, 2048 envs per dispatch)",
+           "per_dispatch": out,
+           "per_workgroup": {k: v / a.wg_per_dispatch for k, v in out.items()},
+           "valu_issue_per_wave_cycle": out.get("SQ_ACTIVE_INST_VALU", 0) / max(out.get("SQ_WAVE_CYCLES", 1), 1),
+           "valu_insts_per_px": out.get("SQ_INSTS_VALU", 0) * 64 / a.px_per_dispatch}
+    dst = os.path.join(REPO, "profiles", f"{a.round}_render_pmc.json")
+    json.dump(res, open(dst, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
