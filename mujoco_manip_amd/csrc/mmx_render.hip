@@ -52,7 +52,15 @@ static constexpr int kSmallArea = MMR_SMALL_AREA; // bounding boxes up to this m
 #define MMR_GROUP 16
 #endif
 static constexpr int kGroup = MMR_GROUP;         // lanes per small triangle
-static constexpr int kMaxBig = 1024;
+static constexpr int kMaxBig = 512;  // per band; a full queue sends further large triangles to the small path
+#ifndef MMR_PF
+#define MMR_PF 1  // small raster: vertex ids of the next triangle prefetched
+#endif
+#ifndef MMR_BPW
+#define MMR_BPW 2
+#endif
+static constexpr int kBPW = MMR_BPW;  // bands per workgroup: vertex and triangle setup shared by them
+static_assert(kBPW >= 1 && kBPW <= 4, "nbig holds 2 counters per band");
 #ifndef MMR_TPW
 #define MMR_TPW 2
 #endif
@@ -97,8 +105,7 @@ DEV float4 rend_unproject(float sx, float sy, float iz, float f, float half) {
   return make_float4((sx - half) * d / f, (half - sy) * d / f, -d, 0.f);
 }
 
-DEV bool rend_setup(const float4* vs, int t, int S, int row0, int row1, RTri& T) {
-  const int a = MMR_tri[3 * t], b = MMR_tri[3 * t + 1], c = MMR_tri[3 * t + 2];
+DEV bool rend_setup_abc(const float4* vs, int a, int b, int c, int S, int row0, int row1, RTri& T) {
   T.i0 = a;
   T.i1 = b;
   T.i2 = c;
@@ -119,6 +126,9 @@ DEV bool rend_setup(const float4* vs, int t, int S, int row0, int row1, RTri& T)
   T.by0 = max(row0, (int)ceilf(mny - 0.5f));
   T.by1 = min(row1 - 1, (int)floorf(mxy - 0.5f));
   return T.bx0 <= T.bx1 && T.by0 <= T.by1;
+}
+DEV bool rend_setup(const float4* vs, int t, int S, int row0, int row1, RTri& T) {
+  return rend_setup_abc(vs, MMR_tri[3 * t], MMR_tri[3 * t + 1], MMR_tri[3 * t + 2], S, row0, row1, T);
 }
 
 // coverage + depth key of pixel (px, py) for triangle t; 0 = not covered
@@ -187,25 +197,26 @@ DEV void shade4(const uint32_t* keys, int px0, int py, int Sz, float half, float
   }
 }
 
-extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, int env_base) {
+extern "C" __global__ void __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(2 * RWG / 256, 2 * RWG / 256)))
+mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), registers to match
   extern __shared__ __align__(16) unsigned char rsmem[];
   float4* vs = reinterpret_cast<float4*>(rsmem);                                 // [MMR_NVERT] screen
   float* bpose = reinterpret_cast<float*>(vs + MMR_NVERT);                        // [19][12]
   uint32_t* zb = reinterpret_cast<uint32_t*>(bpose + 19 * 12);                    // [kBandPx]
-  unsigned short* bigq = reinterpret_cast<unsigned short*>(zb + kBandPx);         // [kMaxBig]
-  int* nbig = reinterpret_cast<int*>(bigq + kMaxBig);
-  float* cam = reinterpret_cast<float*>(nbig + 4);                                // R (9), p (3)
+  unsigned short* bigq = reinterpret_cast<unsigned short*>(zb + kBandPx);         // [kBPW][kMaxBig]
+  int* nbig = reinterpret_cast<int*>(bigq + kBPW * kMaxBig);                      // [8]: large, small per band
+  float* cam = reinterpret_cast<float*>(nbig + 8);                                // R (9), p (3)
   uint32_t* tinfo = reinterpret_cast<uint32_t*>(cam + 12);                        // [MMR_NTRI]
   float* mrgb = reinterpret_cast<float*>(tinfo + MMR_NTRI);                       // [MMR_NMAT][8]
-  unsigned short* smallq = reinterpret_cast<unsigned short*>(mrgb + 8 * MMR_NMAT); // [MMR_NTRI]
+  unsigned short* smallq = reinterpret_cast<unsigned short*>(mrgb + 8 * MMR_NMAT); // [kBPW][MMR_NTRI]
 
   const int tid = threadIdx.x;
   const int Sz = S.image_size;
   const int rows = rend_band_rows(Sz);
-  const int row0 = blockIdx.x * rows, row1 = min(Sz, row0 + rows);
+  const int rowA = blockIdx.x * kBPW * rows, rowB = min(Sz, rowA + kBPW * rows);  // the workgroup's bands
   const int ci = blockIdx.y;  // 0 overhead, 1 wrist
   const int i = env_base + blockIdx.z;
-  if (i >= S.N || row0 >= Sz) return;
+  if (i >= S.N || rowA >= Sz) return;
   const float* rp = S.rpose + (size_t)i * RNSLOT * 12;
 
   // 1. body poses (world, static scene bodies, moving bodies) and the camera
@@ -222,9 +233,8 @@ extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, 
       for (int k = 0; k < 3; k++) o[9 + k] = b == 0 ? 0.f : MMX_body_pos[3 * b + k];
     }
   }
+  if (tid < 8) nbig[tid] = 0;
   if (tid == 32) {
-    nbig[0] = 0;
-    nbig[1] = 0;
     const int c = ci == 0 ? MMX_CAM_OVERHEAD : MMX_CAM_WRIST;
     const M3 lq = qmat(Q4{MMX_cam_quat[4 * c], MMX_cam_quat[4 * c + 1], MMX_cam_quat[4 * c + 2], MMX_cam_quat[4 * c + 3]});
     const V3 lp = V3{MMX_cam_pos[3 * c], MMX_cam_pos[3 * c + 1], MMX_cam_pos[3 * c + 2]};
@@ -241,7 +251,7 @@ extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, 
     for (int k = 0; k < 9; k++) cam[k] = R.m[k];
     cam[9] = p.x; cam[10] = p.y; cam[11] = p.z;
   }
-  for (int k = tid; k < (row1 - row0) * Sz; k += RWG) zb[k] = 0u;
+  for (int k = tid; k < min(rows, rowB - rowA) * Sz; k += RWG) zb[k] = 0u;  // the first band's z-buffer
   if (tid < MMR_NMAT * 8) {  // rgb1, rgb2, checker square, segment id
     const int m = tid >> 3, k = tid & 7;
     mrgb[tid] = k < 6 ? MMR_mat_rgb[6 * m + k] : (k == 6 ? MMR_mat_checker[m] : (float)MMR_mat_seg[m]);
@@ -273,9 +283,11 @@ extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, 
   const V3 lp_cam = mulT(cR, V3{0.5f, 0.5f, 1.5f} - cx);
   // the floor's triangles [0, MMR_FLOOR_TRIS) are not rasterised: it lies below everything, so a
   // pixel no triangle covers shows the floor where its ray meets z = 0 inside the plane, else sky
+  // Each triangle is set up once for the workgroup's rows (cull, box, face light) and queued per
+  // band its box meets.
   for (int t = MMR_FLOOR_TRIS + tid; t < MMR_NTRI; t += RWG) {
     RTri T;
-    if (!rend_setup(vs, t, Sz, row0, row1, T)) continue;
+    if (!rend_setup(vs, t, Sz, rowA, rowB, T)) continue;
     {  // flat shading of the face, once: headlight + directional + point light (at the centroid)
       const float4 a = rend_unproject(T.x0, T.y0, T.iz0, f, half), b = rend_unproject(T.x1, T.y1, T.iz1, f, half),
                    cc = rend_unproject(T.x2, T.y2, T.iz2, f, half);
@@ -285,22 +297,45 @@ extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, 
                           0.4f * fmaxf(dot(n, normalize(lp_cam - pc)), 0.f);
       tinfo[t] = ((uint32_t)(fminf(light, 3.99f) * 16384.f) << 16) | MMR_tri_mat[t];
     }
-    const int area = (T.bx1 - T.bx0 + 1) * (T.by1 - T.by0 + 1);
-    if (area > kSmallArea) {
-      const int k = atomicAdd(nbig, 1);
-      if (k < kMaxBig) bigq[k] = (unsigned short)t;
-    } else {
-      smallq[atomicAdd(nbig + 1, 1)] = (unsigned short)t;
+    for (int kb = 0; kb < kBPW; kb++) {
+      const int r0 = rowA + kb * rows;
+      const int by0 = max(T.by0, r0), by1 = min(T.by1, r0 + rows - 1);
+      if (by0 > by1) continue;
+      const int area = (T.bx1 - T.bx0 + 1) * (by1 - by0 + 1);
+      int k = area > kSmallArea ? atomicAdd(nbig + 2 * kb, 1) : kMaxBig;
+      if (k < kMaxBig) bigq[kb * kMaxBig + k] = (unsigned short)t;
+      else smallq[kb * MMR_NTRI + atomicAdd(nbig + 2 * kb + 1, 1)] = (unsigned short)t;
     }
+  }
+  const int tcols = Sz >> 4;
+  const int lane = tid & 63, lx = 4 * (lane & 3), ly = lane >> 2;
+  unsigned char* img = S.images + ((size_t)i * 2 + ci) * Sz * Sz * 3;
+  unsigned char* seg = S.seg + ((size_t)i * 2 + ci) * Sz * Sz;
+  for (int kb = 0; kb < kBPW; kb++) {  // the bands one after the other through the one z-buffer
+  const int row0 = rowA + kb * rows, row1 = min(Sz, row0 + rows);
+  if (row0 >= Sz) break;
+  if (kb) {
+    __syncthreads();  // the previous band's tiles have read zb
+    for (int k = tid; k < (row1 - row0) * Sz; k += RWG) zb[k] = 0u;
   }
   __syncthreads();
   {  // small triangles: one per 16-lane group, the group's lanes stride over the box
-    const int ns = (MMR_SKIP & 1) ? 0 : nbig[1];
+    const int ns = (MMR_SKIP & 1) ? 0 : nbig[2 * kb + 1];
     const int grp = tid / kGroup, gl = tid % kGroup;
+    // one triangle ahead: the next triangle's vertex ids (table loads) are in flight while this
+    // one is scanned
+    int tn = grp < ns ? smallq[kb * MMR_NTRI + grp] : MMR_FLOOR_TRIS;
+    int an = MMR_tri[3 * tn], bn = MMR_tri[3 * tn + 1], cn = MMR_tri[3 * tn + 2];
     for (int q = grp; q < ns; q += RWG / kGroup) {
-      const int t = smallq[q];
+      int t = tn;
+      const int a = an, b = bn, c = cn;
+      if (MMR_PF && q + RWG / kGroup < ns) {
+        tn = smallq[kb * MMR_NTRI + q + RWG / kGroup];
+        an = MMR_tri[3 * tn]; bn = MMR_tri[3 * tn + 1]; cn = MMR_tri[3 * tn + 2];
+      }
       RTri T;
-      rend_setup(vs, t, Sz, row0, row1, T);
+      if (MMR_PF) rend_setup_abc(vs, a, b, c, Sz, row0, row1, T);
+      else rend_setup(vs, t = smallq[kb * MMR_NTRI + q], Sz, row0, row1, T);
       const int w = T.bx1 - T.bx0 + 1, area = w * (T.by1 - T.by0 + 1);
       const float rw = 1.f / (float)w;
       for (int k = gl; k < area; k += kGroup) {
@@ -320,11 +355,8 @@ extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, 
   // box or wholly outside one of its edges (12 corner tests, one per lane, one ballot), keeps the
   // nearest key in registers and shades its pixels straight away: no depth atomics, no zb write
   // back, no barrier between the large-triangle raster and the shading.
-  const int nb = (MMR_SKIP & 2) ? 0 : min(nbig[0], kMaxBig);
-  const int tcols = Sz >> 4, ntiles = tcols * ((row1 - row0 + 15) >> 4);
-  const int lane = tid & 63, lx = 4 * (lane & 3), ly = lane >> 2;
-  unsigned char* img = S.images + ((size_t)i * 2 + ci) * Sz * Sz * 3;
-  unsigned char* seg = S.seg + ((size_t)i * 2 + ci) * Sz * Sz;
+  const int nb = (MMR_SKIP & 2) ? 0 : min(nbig[2 * kb], kMaxBig);
+  const int ntiles = tcols * ((row1 - row0 + 15) >> 4);
   for (int tb = (tid >> 6) * kTPW; tb < ((MMR_SKIP & 4) ? 0 : ntiles); tb += (RWG / 64) * kTPW) {
     int tx[kTPW], ty[kTPW];
     uint32_t best[kTPW][4];
@@ -337,7 +369,7 @@ extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, 
       for (int u = 0; u < 4; u++) best[j][u] = py < row1 ? zb[(py - row0) * Sz + tx[j] + lx + u] : 0u;
     }
     for (int q = 0; q < nb; q++) {
-      const int t = __builtin_amdgcn_readfirstlane((int)bigq[q]);
+      const int t = __builtin_amdgcn_readfirstlane((int)bigq[kb * kMaxBig + q]);
       RTri T;
       rend_setup(vs, t, Sz, row0, row1, T);
       for (int j = 0; j < kTPW; j++) {
@@ -366,18 +398,19 @@ extern "C" __global__ void __launch_bounds__(RWG) mmx_render_kernel(MMXState S, 
              reinterpret_cast<uint32_t*>(img + 3 * p0), reinterpret_cast<uint32_t*>(seg + p0));
     }
   }
+  }  // bands
 }
 
 extern "C" size_t mmx_render_lds_bytes() {
   return sizeof(float4) * MMR_NVERT + sizeof(float) * 19 * 12 + sizeof(uint32_t) * kBandPx +
-         sizeof(unsigned short) * kMaxBig + 4 * sizeof(int) + 12 * sizeof(float) + sizeof(uint32_t) * MMR_NTRI +
-         sizeof(float) * 8 * MMR_NMAT + sizeof(unsigned short) * MMR_NTRI;
+         sizeof(unsigned short) * kBPW * kMaxBig + 8 * sizeof(int) + 12 * sizeof(float) + sizeof(uint32_t) * MMR_NTRI +
+         sizeof(float) * 8 * MMR_NMAT + sizeof(unsigned short) * kBPW * MMR_NTRI;
 }
 
 extern "C" hipError_t mmx_launch_render(const MMXState* S, int base, int count, hipStream_t st) {
   if (count <= 0 || S->image_size <= 0) return hipSuccess;
   const int rows = rend_band_rows(S->image_size);
   const int bands = (S->image_size + rows - 1) / rows;
-  hipLaunchKernelGGL(mmx_render_kernel, dim3(bands, 2, count), dim3(RWG), mmx_render_lds_bytes(), st, *S, base);
+  hipLaunchKernelGGL(mmx_render_kernel, dim3((bands + kBPW - 1) / kBPW, 2, count), dim3(RWG), mmx_render_lds_bytes(), st, *S, base);
   return hipGetLastError();
 }
