@@ -73,23 +73,26 @@ __host__ DEV int rend_band_rows(int S) {
 }
 
 struct RTri {  // screen-space setup of one triangle
-  float x0, y0, x1, y1, x2, y2;  // pixel coordinates
-  float iz0, iz1, iz2;           // 1 / depth
-  float inv;                     // 1 / (e0 + e1 + e2): the edge functions sum to twice the area
-  int i0, i1, i2;                // vertex ids: shared edges are evaluated in one canonical order
-  int bx0, by0, bx1, by1;        // pixel bbox (inclusive), clipped to the band
+  float A[3], B[3], C[3];  // edge k (opposite vertex k) as the plane e_k(x, y) = A x + B y + C
+  float w[3];              // depth-key weights: q = sum_k e_k w_k + q0 (1 / depth, scaled to [0, 1])
+  int bx0, by0, bx1, by1;  // pixel bbox (inclusive), clipped to the rows asked for
 };
 
-// Edge function of a -> b at p, evaluated from the lower vertex id to the higher one and negated
-// when the triangle walks the edge the other way: the two triangles of a shared edge get exactly
-// opposite values, so no pixel centre on the edge is missed by both (no FMA contraction either).
-DEV float rend_edge(float xa, float ya, int ia, float xb, float yb, int ib, float px, float py) {
-#pragma clang fp contract(off)
+// Edge function of a -> b as a plane, formed from the lower vertex id to the higher one and negated
+// when the triangle walks the edge the other way: the two triangles of a shared edge hold exactly
+// opposite coefficients and evaluate them with the same fused ops, so their values at a pixel
+// centre are exact negatives and no centre on the edge is missed by both.  (The constant term
+// cancels only to the rounding of x0 y1: ~1e-7 of the vertices' pixel coordinates, far below a
+// pixel's distance resolution for any edge on screen.)
+DEV void rend_edge_plane(float xa, float ya, int ia, float xb, float yb, int ib, float& A, float& B, float& C) {
   const bool fwd = ia < ib;
   const float x0 = fwd ? xa : xb, y0 = fwd ? ya : yb, x1 = fwd ? xb : xa, y1 = fwd ? yb : ya;
-  const float e = __fsub_rn(__fmul_rn(x0 - px, y1 - py), __fmul_rn(x1 - px, y0 - py));
-  return fwd ? e : -e;
+  const float sg = fwd ? 1.f : -1.f;
+  A = sg * (y0 - y1);
+  B = sg * (x1 - x0);
+  C = sg * __fsub_rn(__fmul_rn(x0, y1), __fmul_rn(x1, y0));
 }
+DEV float rend_edge_at(const RTri& T, int k, float x, float y) { return fmaf(T.A[k], x, fmaf(T.B[k], y, T.C[k])); }
 
 // camera-space vertex -> screen (sx, sy, 1 / depth, 1) or (0, 0, 0, 0) behind the near plane
 DEV float4 rend_project(float4 c, float f, float half, float znear) {
@@ -105,42 +108,41 @@ DEV float4 rend_unproject(float sx, float sy, float iz, float f, float half) {
   return make_float4((sx - half) * d / f, (half - sy) * d / f, -d, 0.f);
 }
 
-DEV bool rend_setup_abc(const float4* vs, int a, int b, int c, int S, int row0, int row1, RTri& T) {
-  T.i0 = a;
-  T.i1 = b;
-  T.i2 = c;
+// setup of triangle (a, b, c) for rows [row0, row1); false = culled (near plane, back face, no
+// pixel centre in its box).  iz_scale: depth-key scale (1 / depth range).
+DEV bool rend_setup_abc(const float4* vs, int a, int b, int c, int S, int row0, int row1, float iz_scale, RTri& T) {
   const float4 pa = vs[a], pb = vs[b], pc = vs[c];
   if (pa.w == 0.f || pb.w == 0.f || pc.w == 0.f) return false;  // a vertex behind the near plane
-  T.x0 = pa.x; T.y0 = pa.y; T.iz0 = pa.z;
-  T.x1 = pb.x; T.y1 = pb.y; T.iz1 = pb.z;
-  T.x2 = pc.x; T.y2 = pc.y; T.iz2 = pc.z;
   // screen y points down: a counter-clockwise (outward) face has negative signed area
-  const float area = (T.x1 - T.x0) * (T.y2 - T.y0) - (T.x2 - T.x0) * (T.y1 - T.y0);
+  const float area = (pb.x - pa.x) * (pc.y - pa.y) - (pc.x - pa.x) * (pb.y - pa.y);
   if (!(area < -1e-12f)) return false;
-  T.inv = 1.f / area;
-  const float mnx = fminf(T.x0, fminf(T.x1, T.x2)), mxx = fmaxf(T.x0, fmaxf(T.x1, T.x2));
-  const float mny = fminf(T.y0, fminf(T.y1, T.y2)), mxy = fmaxf(T.y0, fmaxf(T.y1, T.y2));
+  const float mnx = fminf(pa.x, fminf(pb.x, pc.x)), mxx = fmaxf(pa.x, fmaxf(pb.x, pc.x));
+  const float mny = fminf(pa.y, fminf(pb.y, pc.y)), mxy = fmaxf(pa.y, fmaxf(pb.y, pc.y));
   // pixel (i, j) has its centre at (i + 0.5, j + 0.5)
   T.bx0 = max(0, (int)ceilf(mnx - 0.5f));
   T.bx1 = min(S - 1, (int)floorf(mxx - 0.5f));
   T.by0 = max(row0, (int)ceilf(mny - 0.5f));
   T.by1 = min(row1 - 1, (int)floorf(mxy - 0.5f));
+  rend_edge_plane(pb.x, pb.y, b, pc.x, pc.y, c, T.A[0], T.B[0], T.C[0]);
+  rend_edge_plane(pc.x, pc.y, c, pa.x, pa.y, a, T.A[1], T.B[1], T.C[1]);
+  rend_edge_plane(pa.x, pa.y, a, pb.x, pb.y, b, T.A[2], T.B[2], T.C[2]);
+  const float s = iz_scale / area;  // barycentric e_k / area, times the key scale
+  T.w[0] = pa.z * s;
+  T.w[1] = pb.z * s;
+  T.w[2] = pc.z * s;
   return T.bx0 <= T.bx1 && T.by0 <= T.by1;
 }
-DEV bool rend_setup(const float4* vs, int t, int S, int row0, int row1, RTri& T) {
-  return rend_setup_abc(vs, MMR_tri[3 * t], MMR_tri[3 * t + 1], MMR_tri[3 * t + 2], S, row0, row1, T);
+DEV bool rend_setup(const float4* vs, int t, int S, int row0, int row1, float iz_scale, RTri& T) {
+  return rend_setup_abc(vs, MMR_tri[3 * t], MMR_tri[3 * t + 1], MMR_tri[3 * t + 2], S, row0, row1, iz_scale, T);
 }
 
-// coverage + depth key of pixel (px, py) for triangle t; 0 = not covered
-DEV uint32_t rend_cover(const RTri& T, int t, int px, int py, float iz_lo, float iz_scale) {
+// coverage + depth key of pixel (px, py) for triangle t; 0 = not covered.  q0 = -iz_lo * iz_scale.
+DEV uint32_t rend_cover(const RTri& T, int t, int px, int py, float q0) {
   const float x = px + 0.5f, y = py + 0.5f;
   // front faces have negative screen area: inside = every edge function <= 0
-  const float e0 = rend_edge(T.x1, T.y1, T.i1, T.x2, T.y2, T.i2, x, y);
-  const float e1 = rend_edge(T.x2, T.y2, T.i2, T.x0, T.y0, T.i0, x, y);
-  const float e2 = rend_edge(T.x0, T.y0, T.i0, T.x1, T.y1, T.i1, x, y);
-  if (e0 > 0.f || e1 > 0.f || e2 > 0.f) return 0u;
-  const float iz = (e0 * T.iz0 + e1 * T.iz1 + e2 * T.iz2) * T.inv;
-  const float q = fminf(fmaxf((iz - iz_lo) * iz_scale, 0.f), 1.f);
+  const float e0 = rend_edge_at(T, 0, x, y), e1 = rend_edge_at(T, 1, x, y), e2 = rend_edge_at(T, 2, x, y);
+  if (fmaxf(e0, fmaxf(e1, e2)) > 0.f) return 0u;
+  const float q = fminf(fmaxf(fmaf(e0, T.w[0], fmaf(e1, T.w[1], fmaf(e2, T.w[2], q0))), 0.f), 1.f);
   const uint32_t d = 1u + (uint32_t)(q * 1048574.f);  // 1 .. 2^20 - 1 (0 = empty)
   return (d << 12) | (uint32_t)t;
 }
@@ -278,7 +280,7 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
   __syncthreads();
 
   // 3. rasterise
-  const float iz_lo = 1.f / zfar, iz_scale = 1.f / (1.f / znear - 1.f / zfar);
+  const float iz_lo = 1.f / zfar, iz_scale = 1.f / (1.f / znear - 1.f / zfar), q0 = -iz_lo * iz_scale;
   const V3 l_top = mulT(cR, V3{0.f, 0.f, 1.f});  // toward the directional light (dir 0 0 -1)
   const V3 lp_cam = mulT(cR, V3{0.5f, 0.5f, 1.5f} - cx);
   // the floor's triangles [0, MMR_FLOOR_TRIS) are not rasterised: it lies below everything, so a
@@ -287,10 +289,12 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
   // band its box meets.
   for (int t = MMR_FLOOR_TRIS + tid; t < MMR_NTRI; t += RWG) {
     RTri T;
-    if (!rend_setup(vs, t, Sz, rowA, rowB, T)) continue;
+    const int ta = MMR_tri[3 * t], tb = MMR_tri[3 * t + 1], tc = MMR_tri[3 * t + 2];
+    if (!rend_setup_abc(vs, ta, tb, tc, Sz, rowA, rowB, iz_scale, T)) continue;
     {  // flat shading of the face, once: headlight + directional + point light (at the centroid)
-      const float4 a = rend_unproject(T.x0, T.y0, T.iz0, f, half), b = rend_unproject(T.x1, T.y1, T.iz1, f, half),
-                   cc = rend_unproject(T.x2, T.y2, T.iz2, f, half);
+      const float4 pa = vs[ta], pb = vs[tb], pcv = vs[tc];
+      const float4 a = rend_unproject(pa.x, pa.y, pa.z, f, half), b = rend_unproject(pb.x, pb.y, pb.z, f, half),
+                   cc = rend_unproject(pcv.x, pcv.y, pcv.z, f, half);
       const V3 n = normalize(cross(V3{b.x - a.x, b.y - a.y, b.z - a.z}, V3{cc.x - a.x, cc.y - a.y, cc.z - a.z}));
       const V3 pc = V3{(a.x + b.x + cc.x) * (1.f / 3.f), (a.y + b.y + cc.y) * (1.f / 3.f), (a.z + b.z + cc.z) * (1.f / 3.f)};
       const float light = 0.3f + 0.6f * fmaxf(n.z, 0.f) + 0.8f * fmaxf(dot(n, l_top), 0.f) +
@@ -334,14 +338,14 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
         an = MMR_tri[3 * tn]; bn = MMR_tri[3 * tn + 1]; cn = MMR_tri[3 * tn + 2];
       }
       RTri T;
-      if (MMR_PF) rend_setup_abc(vs, a, b, c, Sz, row0, row1, T);
-      else rend_setup(vs, t = smallq[kb * MMR_NTRI + q], Sz, row0, row1, T);
+      if (MMR_PF) rend_setup_abc(vs, a, b, c, Sz, row0, row1, iz_scale, T);
+      else rend_setup(vs, t = smallq[kb * MMR_NTRI + q], Sz, row0, row1, iz_scale, T);
       const int w = T.bx1 - T.bx0 + 1, area = w * (T.by1 - T.by0 + 1);
       const float rw = 1.f / (float)w;
       for (int k = gl; k < area; k += kGroup) {
         const int r = (int)(((float)k + 0.5f) * rw);  // k / w, exact for these sizes (no integer divide)
         const int px = T.bx0 + k - r * w, py = T.by0 + r;
-        const uint32_t key = rend_cover(T, t, px, py, iz_lo, iz_scale);
+        const uint32_t key = rend_cover(T, t, px, py, q0);
         if (key) atomicMax(&zb[(py - row0) * Sz + px], key);
       }
     }
@@ -371,21 +375,20 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
     for (int q = 0; q < nb; q++) {
       const int t = __builtin_amdgcn_readfirstlane((int)bigq[kb * kMaxBig + q]);
       RTri T;
-      rend_setup(vs, t, Sz, row0, row1, T);
+      rend_setup(vs, t, Sz, row0, row1, iz_scale, T);
       for (int j = 0; j < kTPW; j++) {
         if (T.bx1 < tx[j] || T.bx0 > tx[j] + 15 || T.by1 < ty[j] || T.by0 > ty[j] + 15) continue;
         {  // lane 4e + c: edge e at tile corner c; a tile whose 4 corners all lie outside one edge
            // lies wholly outside the triangle (pixel centres of the tile's corner pixels)
           const int e = min(lane >> 2, 2), c = lane & 3;
           const float cx0 = tx[j] + ((c & 1) ? 15.5f : 0.5f), cy0 = ty[j] + ((c & 2) ? 15.5f : 0.5f);
-          const float xa = e == 0 ? T.x1 : (e == 1 ? T.x2 : T.x0), ya = e == 0 ? T.y1 : (e == 1 ? T.y2 : T.y0);
-          const float xb = e == 0 ? T.x2 : (e == 1 ? T.x0 : T.x1), yb = e == 0 ? T.y2 : (e == 1 ? T.y0 : T.y1);
-          const int ia = e == 0 ? T.i1 : (e == 1 ? T.i2 : T.i0), ib = e == 0 ? T.i2 : (e == 1 ? T.i0 : T.i1);
-          const uint64_t out = __ballot(lane < 12 && rend_edge(xa, ya, ia, xb, yb, ib, cx0, cy0) > 0.f);
+          const float A = e == 0 ? T.A[0] : (e == 1 ? T.A[1] : T.A[2]), B = e == 0 ? T.B[0] : (e == 1 ? T.B[1] : T.B[2]);
+          const float C = e == 0 ? T.C[0] : (e == 1 ? T.C[1] : T.C[2]);
+          const uint64_t out = __ballot(lane < 12 && fmaf(A, cx0, fmaf(B, cy0, C)) > 0.f);
           if ((out & 0xFull) == 0xFull || (out & 0xF0ull) == 0xF0ull || (out & 0xF00ull) == 0xF00ull) continue;
         }
         for (int u = 0; u < 4; u++) {
-          const uint32_t key = rend_cover(T, t, tx[j] + lx + u, ty[j] + ly, iz_lo, iz_scale);
+          const uint32_t key = rend_cover(T, t, tx[j] + lx + u, ty[j] + ly, q0);
           best[j][u] = max(best[j][u], key);
         }
       }
