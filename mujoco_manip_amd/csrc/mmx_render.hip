@@ -47,6 +47,10 @@ static_assert(MMR_NTRI <= 4096, "triangle index must fit the 12-bit depth-key fi
 #define MMR_SMALL_AREA 2048  // measured: 256 -> 2048 px boxes on 16-lane groups, -8 % render time (4096: +9 %)
 #endif
 static constexpr int kBandPx = MMR_BAND_PX;      // z-buffer pixels per band
+#ifndef MMR_ZPAD
+#define MMR_ZPAD 1  // z-buffer row stride S + 1: a column walk's rows fall on different LDS banks
+#endif
+static constexpr int kZbWords = kBandPx + 128 * MMR_ZPAD;  // a band has at most 128 rows of <= S + 1
 static constexpr int kSmallArea = MMR_SMALL_AREA; // bounding boxes up to this many pixels: a 16-lane group
 #ifndef MMR_GROUP
 #define MMR_GROUP 16
@@ -56,6 +60,9 @@ static constexpr int kMaxBig = 512;  // per band; a full queue sends further lar
 #ifndef MMR_PF
 #define MMR_PF 1  // small raster: vertex ids of the next triangle prefetched
 #endif
+#ifndef MMR_COLS
+#define MMR_COLS 1  // small raster as column walks (0: row-major 16-pixel chunks)
+#endif
 #ifndef MMR_BPW
 #define MMR_BPW 2
 #endif
@@ -64,7 +71,20 @@ static_assert(kBPW >= 1 && kBPW <= 4, "nbig holds 2 counters per band");
 #ifndef MMR_TPW
 #define MMR_TPW 2
 #endif
-static constexpr int kTPW = MMR_TPW;  // 16 x 16 tiles per wave and pass of the large-triangle queue
+static constexpr int kTPW = MMR_TPW;
+// MMR_CLOCK (diagnostic builds only): wave 0 of each workgroup adds its wall-clock ticks (100 MHz)
+// per stage into g_rclk: 0 poses / camera / clear, 1 vertices, 2 triangle setup + queues, 3 small
+// raster, 4 large triangles + shading, 5 workgroups; read by mmx_render_clock (tools/render_clock.py)
+#ifdef MMR_CLOCK
+__device__ unsigned long long g_rclk[8];
+#define RCLK_DECL unsigned long long rclk_t = wall_clock64(), rclk_acc[5] = {0, 0, 0, 0, 0};
+#define RCLK(k) do { const unsigned long long n_ = wall_clock64(); rclk_acc[k] += n_ - rclk_t; rclk_t = n_; } while (0)
+#define RCLK_END if (tid == 0) { for (int k_ = 0; k_ < 5; k_++) atomicAdd(&g_rclk[k_], rclk_acc[k_]); atomicAdd(&g_rclk[5], 1ull); }
+#else
+#define RCLK_DECL
+#define RCLK(k)
+#define RCLK_END
+#endif  // 16 x 16 tiles per wave and pass of the large-triangle queue
 
 // rows per band: the image split into the fewest bands that fit the z-buffer, balanced
 __host__ DEV int rend_band_rows(int S) {
@@ -92,7 +112,16 @@ DEV void rend_edge_plane(float xa, float ya, int ia, float xb, float yb, int ib,
   B = sg * (x1 - x0);
   C = sg * __fsub_rn(__fmul_rn(x0, y1), __fmul_rn(x1, y0));
 }
-DEV float rend_edge_at(const RTri& T, int k, float x, float y) { return fmaf(T.A[k], x, fmaf(T.B[k], y, T.C[k])); }
+// e_k(x, y) = B y + (A x + C): every path evaluates it in this one order (the x part can be hoisted
+// out of a column walk without changing a bit)
+DEV float rend_edge_x(const RTri& T, int k, float x) { return fmaf(T.A[k], x, T.C[k]); }
+DEV float rend_edge_at(const RTri& T, int k, float x, float y) { return fmaf(T.B[k], y, rend_edge_x(T, k, x)); }
+// depth key from the edge values of a covered pixel
+DEV uint32_t rend_key(const RTri& T, int t, float e0, float e1, float e2, float q0) {
+  const float q = fminf(fmaxf(fmaf(e0, T.w[0], fmaf(e1, T.w[1], fmaf(e2, T.w[2], q0))), 0.f), 1.f);
+  const uint32_t d = 1u + (uint32_t)(q * 1048574.f);  // 1 .. 2^20 - 1 (0 = empty)
+  return (d << 12) | (uint32_t)t;
+}
 
 // camera-space vertex -> screen (sx, sy, 1 / depth, 1) or (0, 0, 0, 0) behind the near plane
 DEV float4 rend_project(float4 c, float f, float half, float znear) {
@@ -142,9 +171,7 @@ DEV uint32_t rend_cover(const RTri& T, int t, int px, int py, float q0) {
   // front faces have negative screen area: inside = every edge function <= 0
   const float e0 = rend_edge_at(T, 0, x, y), e1 = rend_edge_at(T, 1, x, y), e2 = rend_edge_at(T, 2, x, y);
   if (fmaxf(e0, fmaxf(e1, e2)) > 0.f) return 0u;
-  const float q = fminf(fmaxf(fmaf(e0, T.w[0], fmaf(e1, T.w[1], fmaf(e2, T.w[2], q0))), 0.f), 1.f);
-  const uint32_t d = 1u + (uint32_t)(q * 1048574.f);  // 1 .. 2^20 - 1 (0 = empty)
-  return (d << 12) | (uint32_t)t;
+  return rend_key(T, t, e0, e1, e2, q0);
 }
 
 // shading of 4 horizontally adjacent pixels (px .. px + 3, py) from their depth keys: flat face
@@ -204,8 +231,8 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
   extern __shared__ __align__(16) unsigned char rsmem[];
   float4* vs = reinterpret_cast<float4*>(rsmem);                                 // [MMR_NVERT] screen
   float* bpose = reinterpret_cast<float*>(vs + MMR_NVERT);                        // [19][12]
-  uint32_t* zb = reinterpret_cast<uint32_t*>(bpose + 19 * 12);                    // [kBandPx]
-  unsigned short* bigq = reinterpret_cast<unsigned short*>(zb + kBandPx);         // [kBPW][kMaxBig]
+  uint32_t* zb = reinterpret_cast<uint32_t*>(bpose + 19 * 12);                    // [rows][Zs]
+  unsigned short* bigq = reinterpret_cast<unsigned short*>(zb + kZbWords);        // [kBPW][kMaxBig]
   int* nbig = reinterpret_cast<int*>(bigq + kBPW * kMaxBig);                      // [8]: large, small per band
   float* cam = reinterpret_cast<float*>(nbig + 8);                                // R (9), p (3)
   uint32_t* tinfo = reinterpret_cast<uint32_t*>(cam + 12);                        // [MMR_NTRI]
@@ -215,11 +242,13 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
   const int tid = threadIdx.x;
   const int Sz = S.image_size;
   const int rows = rend_band_rows(Sz);
+  const int Zs = Sz + MMR_ZPAD;  // z-buffer row stride
   const int rowA = blockIdx.x * kBPW * rows, rowB = min(Sz, rowA + kBPW * rows);  // the workgroup's bands
   const int ci = blockIdx.y;  // 0 overhead, 1 wrist
   const int i = env_base + blockIdx.z;
   if (i >= S.N || rowA >= Sz) return;
   const float* rp = S.rpose + (size_t)i * RNSLOT * 12;
+  RCLK_DECL
 
   // 1. body poses (world, static scene bodies, moving bodies) and the camera
   if (tid < 19) {
@@ -253,12 +282,13 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
     for (int k = 0; k < 9; k++) cam[k] = R.m[k];
     cam[9] = p.x; cam[10] = p.y; cam[11] = p.z;
   }
-  for (int k = tid; k < min(rows, rowB - rowA) * Sz; k += RWG) zb[k] = 0u;  // the first band's z-buffer
+  for (int k = tid; k < min(rows, rowB - rowA) * Zs; k += RWG) zb[k] = 0u;  // the first band's z-buffer
   if (tid < MMR_NMAT * 8) {  // rgb1, rgb2, checker square, segment id
     const int m = tid >> 3, k = tid & 7;
     mrgb[tid] = k < 6 ? MMR_mat_rgb[6 * m + k] : (k == 6 ? MMR_mat_checker[m] : (float)MMR_mat_seg[m]);
   }
   __syncthreads();
+  RCLK(0);
 
   // 2. vertices to camera space and to the screen
   M3 cR;
@@ -278,6 +308,7 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
     vs[v] = rend_project(make_float4(cv.x, cv.y, cv.z, 0.f), f, half, znear);
   }
   __syncthreads();
+  RCLK(1);
 
   // 3. rasterise
   const float iz_lo = 1.f / zfar, iz_scale = 1.f / (1.f / znear - 1.f / zfar), q0 = -iz_lo * iz_scale;
@@ -320,9 +351,11 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
   if (row0 >= Sz) break;
   if (kb) {
     __syncthreads();  // the previous band's tiles have read zb
-    for (int k = tid; k < (row1 - row0) * Sz; k += RWG) zb[k] = 0u;
+    RCLK(4);
+    for (int k = tid; k < (row1 - row0) * Zs; k += RWG) zb[k] = 0u;
   }
   __syncthreads();
+  if (kb) RCLK(3); else RCLK(2);
   {  // small triangles: one per 16-lane group, the group's lanes stride over the box
     const int ns = (MMR_SKIP & 1) ? 0 : nbig[2 * kb + 1];
     const int grp = tid / kGroup, gl = tid % kGroup;
@@ -340,17 +373,47 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
       RTri T;
       if (MMR_PF) rend_setup_abc(vs, a, b, c, Sz, row0, row1, iz_scale, T);
       else rend_setup(vs, t = smallq[kb * MMR_NTRI + q], Sz, row0, row1, iz_scale, T);
-      const int w = T.bx1 - T.bx0 + 1, area = w * (T.by1 - T.by0 + 1);
+      const int w = T.bx1 - T.bx0 + 1;
       const float rw = 1.f / (float)w;
+#ifdef MMR_CLOCK
+      if (gl == 0) {
+        atomicAdd(&g_rclk[6], 1ull);
+        atomicAdd(&g_rclk[7], (unsigned long long)(w * (T.by1 - T.by0 + 1)));
+      }
+#endif
+#if MMR_COLS
+      // column walk: a box up to 16 wide gives each lane one column and a row phase (16 / w lanes
+      // per column, rows strided by that), a wider one 16 columns per pass, rows one by one; the
+      // edges' x parts are formed once per column, a pixel then costs 3 FMAs and a max
+      const bool narrow = w <= kGroup;
+      const int rstep = narrow ? (int)(((float)kGroup + 0.5f) * rw) : 1;  // kGroup / w (exact)
+      const int rph = narrow ? (int)(((float)gl + 0.5f) * rw) : 0;        // gl / w
+      if (rph < rstep) {
+        for (int col = narrow ? gl - rph * w : gl; col < w; col += kGroup) {
+          const int px = T.bx0 + col;
+          const float x = px + 0.5f;
+          const float ex0 = rend_edge_x(T, 0, x), ex1 = rend_edge_x(T, 1, x), ex2 = rend_edge_x(T, 2, x);
+          uint32_t* zc = zb + (T.by0 + rph - row0) * Zs + px;
+          for (int py = T.by0 + rph; py <= T.by1; py += rstep, zc += rstep * Zs) {
+            const float y = py + 0.5f;
+            const float e0 = fmaf(T.B[0], y, ex0), e1 = fmaf(T.B[1], y, ex1), e2 = fmaf(T.B[2], y, ex2);
+            if (fmaxf(e0, fmaxf(e1, e2)) <= 0.f) atomicMax(zc, rend_key(T, t, e0, e1, e2, q0));
+          }
+        }
+      }
+#else
+      const int area = w * (T.by1 - T.by0 + 1);
       for (int k = gl; k < area; k += kGroup) {
         const int r = (int)(((float)k + 0.5f) * rw);  // k / w, exact for these sizes (no integer divide)
         const int px = T.bx0 + k - r * w, py = T.by0 + r;
         const uint32_t key = rend_cover(T, t, px, py, q0);
-        if (key) atomicMax(&zb[(py - row0) * Sz + px], key);
+        if (key) atomicMax(&zb[(py - row0) * Zs + px], key);
       }
+#endif
     }
   }
   __syncthreads();
+  RCLK(3);
 
   // 4. large triangles + shading, fused, per 16 x 16 tile (S is a multiple of 16): each wave owns
   // kTPW tiles at a time, lane l the 4 pixels (4 (l & 3) .. +3, l >> 2) of each.  A lane starts from
@@ -370,7 +433,7 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
       tx[j] = (tile - trow * tcols) * 16;
       ty[j] = row0 + trow * 16;
       const int py = ty[j] + ly;
-      for (int u = 0; u < 4; u++) best[j][u] = py < row1 ? zb[(py - row0) * Sz + tx[j] + lx + u] : 0u;
+      for (int u = 0; u < 4; u++) best[j][u] = py < row1 ? zb[(py - row0) * Zs + tx[j] + lx + u] : 0u;
     }
     for (int q = 0; q < nb; q++) {
       const int t = __builtin_amdgcn_readfirstlane((int)bigq[kb * kMaxBig + q]);
@@ -384,7 +447,7 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
           const float cx0 = tx[j] + ((c & 1) ? 15.5f : 0.5f), cy0 = ty[j] + ((c & 2) ? 15.5f : 0.5f);
           const float A = e == 0 ? T.A[0] : (e == 1 ? T.A[1] : T.A[2]), B = e == 0 ? T.B[0] : (e == 1 ? T.B[1] : T.B[2]);
           const float C = e == 0 ? T.C[0] : (e == 1 ? T.C[1] : T.C[2]);
-          const uint64_t out = __ballot(lane < 12 && fmaf(A, cx0, fmaf(B, cy0, C)) > 0.f);
+          const uint64_t out = __ballot(lane < 12 && fmaf(B, cy0, fmaf(A, cx0, C)) > 0.f);
           if ((out & 0xFull) == 0xFull || (out & 0xF0ull) == 0xF0ull || (out & 0xF00ull) == 0xF00ull) continue;
         }
         for (int u = 0; u < 4; u++) {
@@ -402,10 +465,22 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
     }
   }
   }  // bands
+  RCLK(4);
+  RCLK_END
 }
+#ifdef MMR_CLOCK
+extern "C" hipError_t mmx_render_clock(unsigned long long* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rclk), sizeof(unsigned long long) * 8);
+  if (e == hipSuccess && reset) {
+    const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_rclk), z, sizeof(z));
+  }
+  return e;
+}
+#endif
 
 extern "C" size_t mmx_render_lds_bytes() {
-  return sizeof(float4) * MMR_NVERT + sizeof(float) * 19 * 12 + sizeof(uint32_t) * kBandPx +
+  return sizeof(float4) * MMR_NVERT + sizeof(float) * 19 * 12 + sizeof(uint32_t) * kZbWords +
          sizeof(unsigned short) * kBPW * kMaxBig + 8 * sizeof(int) + 12 * sizeof(float) + sizeof(uint32_t) * MMR_NTRI +
          sizeof(float) * 8 * MMR_NMAT + sizeof(unsigned short) * kBPW * MMR_NTRI;
 }
