@@ -1,24 +1,25 @@
 // Batched camera renderer for gfx950: the overhead and wrist images of
 // PickPlaceGymEnv's observation (gym_env.py:295-339 via cameras.py:9-53, mujoco.Renderer).
 //
-// One workgroup (512 lanes) renders one horizontal band (up to 8192 px) of one camera image of one
-// env (two workgroups per CU: one shades while the other sets up):
+// One workgroup (512 lanes) renders two horizontal bands (up to 8192 px each) of one camera image
+// of one env (two workgroups per CU: one rasterises while the other sets up); the bands share the
+// setup and take turns in one LDS z-buffer:
 //   1. body poses of the env (stored by the step / reset / forward kernels in S.rpose) and the
 //      camera pose (overhead: fixed; wrist: on the hand, env.py:52-65) -> LDS;
 //   2. all render vertices (tools/compile_render.py: floor grid, table / bins / cubes as boxes
 //      and prisms, each Panda body as the hull of its visual meshes) to camera space and, once
 //      per vertex, to the screen (MuJoCo pinhole, fovy, row 0 at the top) -> LDS (screen x, y,
 //      1 / depth: the camera-space point is recovered from them where the shading needs it);
-//   3. triangles, one lane each: near cull, back-face cull, bounding box clipped to the band,
-//      into one of two LDS queues by box
-//      area.  Small boxes (<= 2048 px) are scanned by 16-lane groups, one triangle per group
-//      (every lane of a wave busy however the box sizes vary); large ones (floor tiles, table top)
-//      by the whole workgroup, pixel-parallel.  Depth test = one 32-bit LDS atomicMax per covered pixel on
-//      (inverse depth quantised over the camera's depth range : 20 bits | triangle : 12 bits);
-//   4. shading, 4 pixels per lane: flat per-face light (computed once per triangle in pass 3), MuJoCo's
-//      headlight (ambient 0.3, diffuse 0.6) + the scene's directional (0.8) and point (0.4)
-//      lights (pick_and_place_scene.xml:6-9,33-36), the floor checker (0.1 m squares), sky
-//      gradient elsewhere; RGB u8 and the segment id written as packed dwords.
+//   3. triangles, one lane each: near cull, back-face cull, bounding box, flat face light, then
+//      per band into one of two LDS queues by box area;
+//   4. small boxes (<= 2048 px): one triangle per 8-lane group, walked column by column (edge
+//      functions as planes, 3 FMAs per pixel); depth test = one 32-bit LDS atomicMax per covered
+//      pixel on (inverse depth quantised over the camera's depth range : 20 bits | triangle : 12 bits);
+//   5. large boxes (table top, bin walls, close-up links) and shading, fused per 16 x 16 tile: the
+//      wave walks the large queue with its depth keys in registers, then shades 4 pixels per lane:
+//      flat per-face light, MuJoCo's headlight (ambient 0.3, diffuse 0.6) + the scene's directional
+//      (0.8) and point (0.4) lights (pick_and_place_scene.xml:6-9,33-36), the floor checker (0.1 m
+//      squares), sky gradient elsewhere; RGB u8 and the segment id written as packed dwords.
 // Not modelled (documented in DESIGN.md): shadows, specular, reflectance, bin transparency
 // (alpha 0.4 -> opaque), visual-mesh detail beyond each body's convex hull.
 #include <hip/hip_runtime.h>
@@ -53,7 +54,7 @@ static constexpr int kBandPx = MMR_BAND_PX;      // z-buffer pixels per band
 static constexpr int kZbWords = kBandPx + 128 * MMR_ZPAD;  // a band has at most 128 rows of <= S + 1
 static constexpr int kSmallArea = MMR_SMALL_AREA; // bounding boxes up to this many pixels: a 16-lane group
 #ifndef MMR_GROUP
-#define MMR_GROUP 16
+#define MMR_GROUP 8  // measured with the column walk: 8 lanes per triangle -3 % render time vs 16
 #endif
 static constexpr int kGroup = MMR_GROUP;         // lanes per small triangle
 static constexpr int kMaxBig = 512;  // per band; a full queue sends further large triangles to the small path
@@ -375,7 +376,7 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
       else rend_setup(vs, t = smallq[kb * MMR_NTRI + q], Sz, row0, row1, iz_scale, T);
       const int w = T.bx1 - T.bx0 + 1;
       const float rw = 1.f / (float)w;
-#ifdef MMR_CLOCK
+#ifdef MMR_CLOCK_STATS  // (global atomics: distorts the MMR_CLOCK times)
       if (gl == 0) {
         atomicAdd(&g_rclk[6], 1ull);
         atomicAdd(&g_rclk[7], (unsigned long long)(w * (T.by1 - T.by0 + 1)));
