@@ -14,7 +14,7 @@ def main():
     ap.add_argument("--round", default="r02")
     ap.add_argument("--prof", default=os.path.join(REPO, "gpurun_out", "rpmc"))
     ap.add_argument("--last", type=int, default=32)
-    ap.add_argument("--wg-per-dispatch", type=int, default=2048 * 2 * 2)  # envs x cameras x bands (128^2)
+    ap.add_argument("--wg-per-dispatch", type=int, default=2048 * 2)  # envs x cameras (128^2: both bands in one workgroup)
     ap.add_argument("--px-per-dispatch", type=int, default=2048 * 2 * 128 * 128)
     a = ap.parse_args()
     per = {}
