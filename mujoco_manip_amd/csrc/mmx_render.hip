@@ -64,6 +64,9 @@ static constexpr int kMaxBig = 512;  // per band; a full queue sends further lar
 #ifndef MMR_COLS
 #define MMR_COLS 1  // small raster as column walks (0: row-major 16-pixel chunks)
 #endif
+#ifndef MMR_SPAN
+#define MMR_SPAN 1  // column walk restricted to the column's span inside the triangle
+#endif
 #ifndef MMR_BPW
 #define MMR_BPW 2
 #endif
@@ -389,13 +392,34 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
       const bool narrow = w <= kGroup;
       const int rstep = narrow ? (int)(((float)kGroup + 0.5f) * rw) : 1;  // kGroup / w (exact)
       const int rph = narrow ? (int)(((float)gl + 0.5f) * rw) : 0;        // gl / w
+#if MMR_SPAN
+      const float rB[3] = {1.f / T.B[0], 1.f / T.B[1], 1.f / T.B[2]};  // (unused where B_k = 0)
+#endif
       if (rph < rstep) {
         for (int col = narrow ? gl - rph * w : gl; col < w; col += kGroup) {
           const int px = T.bx0 + col;
           const float x = px + 0.5f;
           const float ex0 = rend_edge_x(T, 0, x), ex1 = rend_edge_x(T, 1, x), ex2 = rend_edge_x(T, 2, x);
-          uint32_t* zc = zb + (T.by0 + rph - row0) * Zs + px;
-          for (int py = T.by0 + rph; py <= T.by1; py += rstep, zc += rstep * Zs) {
+#if MMR_SPAN
+          // the column's span inside the triangle: edge k bounds the row centres y = py + 0.5 from
+          // above (B_k > 0: y <= -ex_k / B_k) or below (B_k < 0); widened by a row on each side, it
+          // only narrows the walk, every pixel still takes the exact edge test
+          float lo = (float)T.by0, hi = (float)T.by1;
+          {
+            const float ex[3] = {ex0, ex1, ex2};
+            for (int k = 0; k < 3; k++) {
+              const float yb = -ex[k] * rB[k] - 0.5f;  // the boundary in row-index units
+              hi = T.B[k] > 0.f ? fminf(hi, yb + 1.f) : hi;
+              lo = T.B[k] < 0.f ? fmaxf(lo, yb - 1.f) : lo;
+            }
+          }
+          // (kept inside [by0, by1 + 1] / [by0 - 1, by1] before the integer conversion)
+          const int pylo = (int)ceilf(fminf(lo, (float)(T.by1 + 1))), pyhi = (int)floorf(fmaxf(hi, (float)(T.by0 - 1)));
+#else
+          const int pylo = T.by0, pyhi = T.by1;
+#endif
+          uint32_t* zc = zb + (pylo + rph - row0) * Zs + px;
+          for (int py = pylo + rph; py <= pyhi; py += rstep, zc += rstep * Zs) {
             const float y = py + 0.5f;
             const float e0 = fmaf(T.B[0], y, ex0), e1 = fmaf(T.B[1], y, ex1), e2 = fmaf(T.B[2], y, ex2);
             if (fmaxf(e0, fmaxf(e1, e2)) <= 0.f) atomicMax(zc, rend_key(T, t, e0, e1, e2, q0));
