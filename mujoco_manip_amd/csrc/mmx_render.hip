@@ -57,7 +57,11 @@ static constexpr int kSmallArea = MMR_SMALL_AREA; // bounding boxes up to this m
 #define MMR_GROUP 8  // measured with the column walk: 8 lanes per triangle -3 % render time vs 16
 #endif
 static constexpr int kGroup = MMR_GROUP;         // lanes per small triangle
-static constexpr int kMaxBig = 512;  // per band; a full queue sends further large triangles to the small path
+static constexpr int kMaxBig = 512;
+#ifndef MMR_BIG_CACHE
+#define MMR_BIG_CACHE 40  // large-triangle setups kept in LDS per band (what fits beside two workgroups per CU)
+#endif
+static constexpr int kBigCache = MMR_BIG_CACHE;  // per band; a full queue sends further large triangles to the small path
 #ifndef MMR_PF
 #define MMR_PF 1  // small raster: vertex ids of the next triangle prefetched
 #endif
@@ -242,6 +246,7 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
   uint32_t* tinfo = reinterpret_cast<uint32_t*>(cam + 12);                        // [MMR_NTRI]
   float* mrgb = reinterpret_cast<float*>(tinfo + MMR_NTRI);                       // [MMR_NMAT][8]
   unsigned short* smallq = reinterpret_cast<unsigned short*>(mrgb + 8 * MMR_NMAT); // [kBPW][MMR_NTRI]
+  RTri* bigs = reinterpret_cast<RTri*>(smallq + kBPW * MMR_NTRI);                 // [kBigCache] setups
 
   const int tid = threadIdx.x;
   const int Sz = S.image_size;
@@ -360,7 +365,10 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
   }
   __syncthreads();
   if (kb) RCLK(3); else RCLK(2);
-  {  // small triangles: one per 16-lane group, the group's lanes stride over the box
+  // the band's first kBigCache large triangles set up once for every wave's tile walk
+  for (int q = tid; q < min((MMR_SKIP & 2) ? 0 : nbig[2 * kb], kBigCache); q += RWG)
+    rend_setup(vs, bigq[kb * kMaxBig + q], Sz, row0, row1, iz_scale, bigs[q]);
+  {  // small triangles: one per 8-lane group, walked column by column
     const int ns = (MMR_SKIP & 1) ? 0 : nbig[2 * kb + 1];
     const int grp = tid / kGroup, gl = tid % kGroup;
     // one triangle ahead: the next triangle's vertex ids (table loads) are in flight while this
@@ -463,7 +471,8 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
     for (int q = 0; q < nb; q++) {
       const int t = __builtin_amdgcn_readfirstlane((int)bigq[kb * kMaxBig + q]);
       RTri T;
-      rend_setup(vs, t, Sz, row0, row1, iz_scale, T);
+      if (q < kBigCache) T = bigs[q];  // uniform address: LDS broadcast
+      else rend_setup(vs, t, Sz, row0, row1, iz_scale, T);
       for (int j = 0; j < kTPW; j++) {
         if (T.bx1 < tx[j] || T.bx0 > tx[j] + 15 || T.by1 < ty[j] || T.by0 > ty[j] + 15) continue;
         {  // lane 4e + c: edge e at tile corner c; a tile whose 4 corners all lie outside one edge
@@ -507,7 +516,7 @@ extern "C" hipError_t mmx_render_clock(unsigned long long* out, int reset) {
 extern "C" size_t mmx_render_lds_bytes() {
   return sizeof(float4) * MMR_NVERT + sizeof(float) * 19 * 12 + sizeof(uint32_t) * kZbWords +
          sizeof(unsigned short) * kBPW * kMaxBig + 8 * sizeof(int) + 12 * sizeof(float) + sizeof(uint32_t) * MMR_NTRI +
-         sizeof(float) * 8 * MMR_NMAT + sizeof(unsigned short) * kBPW * MMR_NTRI;
+         sizeof(float) * 8 * MMR_NMAT + sizeof(unsigned short) * kBPW * MMR_NTRI + sizeof(RTri) * kBigCache;
 }
 
 extern "C" hipError_t mmx_launch_render(const MMXState* S, int base, int count, hipStream_t st) {
