@@ -47,7 +47,7 @@ def algorithmic_bytes_per_env_step(nefc: float) -> float:
 def min_hbm_bytes_per_env_step() -> float:
     """Bytes the fused kernel must move per env step: env record in+out (qpos, qvel, ctrl,
     warm start, IK cache, target, stats, episode ints/floats, rng) + obs/reward/flags out."""
-    rec = 4 * (30 + 27 + 8 + 27 + 63 + 4 + 17 + 18 + 28) + 8 * 4 + 4
+    rec = 4 * (30 + 27 + 8 + 27 + 63 + 4 + 19 + 18 + 28) + 8 * 4 + 4
     return 2 * rec + 4 * (85 + 1 + 3 + 6)
 
 
@@ -81,6 +81,11 @@ def cpu_budget() -> tuple[int, dict]:
     return max(1, n), info
 
 
+# MuJoCo's default Newton settings (tolerance 1e-8, 100 iterations): the CPU baseline
+# solves to them, not to the parity tests' 1e-13 / 200
+MUJOCO_SOLVER = (1e-8, 100)
+
+
 def _expert_episode(e, seconds_left, t0):
     """One FSM-expert episode on an oracle env (generate_dataset.py:140-196): plan(16) -> abs_pos
     -> step until the FSM is done.  Returns (env steps, placed)."""
@@ -106,14 +111,17 @@ def _cpu_worker(args) -> tuple:
     from mujoco_manip_amd.constants import ALL_TASKS, BINS, OBJECTS
 
     pool = [(OBJECTS.index(o), BINS.index(b)) for o, b in ALL_TASKS]
-    steps, ep = 0, worker
+    steps, ep, solves, iters = 0, worker, 0, 0
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         e = O.OracleEnv(action_mode="abs_pos", reward_type="staged", randomize_objects=True, tasks=pool)
+        e.set_solver(*MUJOCO_SOLVER)
         e.reset(seed=O.episode_seed(42, ep))
         steps += _expert_episode(e, seconds, t0)
+        c, i = e.solver_stats()
+        solves, iters = solves + c, iters + i
         ep += nworkers
-    return steps, time.perf_counter() - t0, (ep - worker) // nworkers
+    return steps, time.perf_counter() - t0, (ep - worker) // nworkers, solves, iters
 
 
 def c1_single_thread(seconds: float = 5.0) -> dict:
@@ -126,6 +134,7 @@ def c1_single_thread(seconds: float = 5.0) -> dict:
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         e = O.OracleEnv(action_mode="abs_pos", reward_type="staged", task=(0, 0))
+        e.set_solver(*MUJOCO_SOLVER)
         e.reset(seed=len(lengths))
         n = _expert_episode(e, 1e9, t0)
         lengths.append(n)
@@ -153,10 +162,13 @@ def cpu_baseline(seconds: float = 30.0, workers: int | None = None) -> dict:
     steps = sum(r[0] for r in res)
     rate = sum(r[0] / r[1] for r in res)
     eps = sum(r[2] for r in res)
+    solves, iters = sum(r[3] for r in res), sum(r[4] for r in res)
     out = {"value": rate, "unit": "env steps/s", "cores": workers, "kind": "port",
            "sample": f"{steps} env steps ({eps} FSM-expert C3 episodes) in {seconds:.0f} s on each of {workers} "
                      f"worker processes (1 thread each, one per usable core); engine: oracle/ fp64 C restatement "
-                     f"(MuJoCo absent on the box)", **info}
+                     f"(MuJoCo absent on the box) with MuJoCo's default Newton settings",
+           "solver": {"tolerance": MUJOCO_SOLVER[0], "max_iterations": MUJOCO_SOLVER[1],
+                      "mean_iterations": iters / max(solves, 1)}, **info}
     out["c1"] = c1_single_thread()
     return out
 
@@ -170,17 +182,41 @@ def _free_port() -> int:
     return p
 
 
-def launch_ranks(n: int) -> int:
+def launch_ranks(n: int, cmd: list[str] | None = None, poll_s: float = 0.2, grace_s: float = 10.0) -> int:
     """`--gpus N` without torchrun: start N rank processes of this script (one GPU each, RCCL),
-    before this process touches any GPU; rank 0 prints the line.  Returns the worst exit code."""
+    before this process touches any GPU; rank 0 prints the line.  All ranks are polled: the first
+    non-zero exit terminates the others (a dead rank would otherwise leave its peers blocked in a
+    collective) and is returned; 0 once every rank exited cleanly.  `cmd` overrides the rank
+    command (tests)."""
     port = str(_free_port())
+    cmd = cmd or [sys.executable, os.path.abspath(__file__)] + sys.argv[1:]
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rcs = [p.wait() for p in procs]
-    return max(abs(rc) for rc in rcs)
+        procs.append(subprocess.Popen(cmd, env=env))
+    try:
+        while True:
+            codes = [p.poll() for p in procs]
+            bad = [c for c in codes if c not in (None, 0)]
+            if bad:
+                rc = abs(bad[0]) or 1
+                print(f"bench: a rank exited with {bad[0]}; stopping the other ranks", file=sys.stderr, flush=True)
+                return rc
+            if all(c == 0 for c in codes):
+                return 0
+            time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        t_end = time.monotonic() + grace_s
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, t_end - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
 
 
 # ----------------------------------------------------------------------------- PMC evidence
@@ -215,6 +251,7 @@ def main():
     # rehearsal of the N > 1 path on a 1-GPU box: ranks share device 0 and talk over gloo
     ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"))
     ap.add_argument("--share-device", action="store_true")
+    ap.add_argument("--dist-timeout", type=float, default=300.0, help="seconds for rendezvous and each collective")
     # 0 = the C3 workload (no images); 128 = C5's two 128 x 128 RGB cameras per env step
     ap.add_argument("--image-size", type=int, default=0)
     # BASELINE.json configs: c3 (default, the metric's config), c2 (1024 envs, fixed task
@@ -245,8 +282,11 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
+        import datetime
+
         torch.cuda.set_device(dev_index)
-        dist.init_process_group(args.dist_backend)
+        # bounded: a rank that never arrives ends the job instead of hanging it
+        dist.init_process_group(args.dist_backend, timeout=datetime.timedelta(seconds=args.dist_timeout))
     dev = torch.device(f"cuda:{dev_index}")
     torch.cuda.set_device(dev)
     # collectives run on device tensors over RCCL, on host tensors over gloo
@@ -300,7 +340,13 @@ def main():
             c = torch.tensor(eps + [errs_now], device=cdev, dtype=torch.float64)
             dist.all_reduce(c, op=dist.ReduceOp.SUM)
             eps, errs_now = c[:4].tolist(), float(c[4].item())
-        windows.append({"elapsed": elapsed, "kern_ms": kern_ms, "solver": solver,
+            rk = torch.zeros(world, device=cdev, dtype=torch.float64)
+            rk[rank] = kern_ms
+            dist.all_reduce(rk, op=dist.ReduceOp.SUM)
+            rank_kern_ms = rk.tolist()
+        else:
+            rank_kern_ms = [kern_ms]
+        windows.append({"elapsed": elapsed, "kern_ms": kern_ms, "rank_kernel_ms": rank_kern_ms, "solver": solver,
                         "episodes": {"completed": int(eps[0]), "successes": int(eps[1]), "placed": int(eps[2]),
                                      "error_resets": int(eps[3]), "envs_with_error_now": int(errs_now)}})
     values = [args.steps * N * world / w["elapsed"] for w in windows]
@@ -329,12 +375,15 @@ def main():
                     f"C5: C3 settings x {N} envs/GPU plus overhead + wrist RGB {args.image_size}x{args.image_size} "
                     "camera images rendered every env step")
         line = {
-            "metric": METRIC, "value": value, "unit": "env steps/s", "n_gpus": world, "steps": args.steps,
+            "metric": METRIC, "value": value, "unit": "env steps/s", "n_gpus": world,
+            # distinct GPUs the ranks ran on: 1 for the --share-device rehearsal of the N-rank path
+            "devices": 1 if args.share_device else world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1000.0 * med["elapsed"] / args.steps, "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic (seeded randomized scenes, FSM-expert actions)",
             "config": {"workload": workload, "envs_per_gpu": N, "global_envs": N * world, "substeps": SUBSTEPS,
-                       "image_size": args.image_size, "parallelism": f"env-batch dp{world}"},
+                       "image_size": args.image_size, "parallelism": f"env-batch dp{world}" + ("" if not args.share_device or world == 1
+                                                                         else " (rehearsal: ranks share one GPU)")},
             "repeats": {"n": len(values), "values": values, "median_of": "value"},
             "physics_steps_per_s": SUBSTEPS * value,
             "episodes": {**ep, "placed_rate": ep["placed"] / max(ep["completed"], 1),
@@ -344,7 +393,8 @@ def main():
                                  "its start pose, which the expert's retreat target does not reach"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "mmx_env_step_kernel", "kernel_ms": kern_ms, "concurrent_launches": lanes,
+                         "kernel": "mmx_env_step_kernel", "kernel_ms": kern_ms,
+                         "rank_kernel_ms": med["rank_kernel_ms"], "concurrent_launches": lanes,
                          "envs_per_launch": envs_per_launch, "env_steps_per_launch": steps_per_launch,
                          "algorithmic_bytes_per_env_step": bpe, "algorithmic_bytes_per_launch": bytes_per_launch,
                          "mean_nefc": solver["mean_nefc"],

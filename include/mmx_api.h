@@ -84,10 +84,12 @@ typedef struct {
   float* episode_f;          /* [N][28] T_init(12), hwm(5), target_kp(4), fsm_target(3), transit(3), return */
   float* kin;                /* [N][63] hand pos/mat, arm joint axes/anchors and cube positions of the
                                 last position stage (what data.xpos holds after mj_step) */
-  float* stats;              /* [N][17] sum nefc, sum ncon, sum solver iterations, substeps, max residual,
+  float* stats;              /* [N][19] sum nefc, sum ncon, sum solver iterations, substeps, max residual,
                                 then shader-clock cycles spent per phase: ik, kinematics, dynamics,
                                 collision, constraints, solver, integrate, step end (reward/obs/reset),
-                                4 sub-phase probes (cycle fields: diagnostic build only, else 0) */
+                                4 sub-phase probes (cycle fields: diagnostic build only, else 0), then
+                                the substeps whose solve ended above the tolerance: by no progress
+                                (step < 1e-9, an fp32 stall), by the iteration cap */
   float* contacts;           /* [N][64][12] dist, pos3, normal3, mu3, dim, geom1, geom2 (last substep) */
   uint8_t* images;           /* [N][2][S][S][3] RGB of the overhead and wrist cameras (S = image_size),
                                 rendered after every reset / step / forward; NULL when image_size = 0 */

@@ -17,14 +17,14 @@ from . import _build
 
 NQ, NV, NU, NOBS = 30, 27, 8, 85
 MAXCON, CON_F = 64, 12
-EPI_N, EPF_N, KIN_N, STAT_N = 18, 28, 63, 17
+EPI_N, EPF_N, KIN_N, STAT_N = 18, 28, 63, 19
 EPI_FIELDS = ("obj", "bin", "step_count", "flags", "fsm_state", "fsm_task_index", "fsm_settle", "fsm_gripper_open",
               "fsm_has_target", "env_error", "ncon", "nefc", "episodes", "rng_has32", "successes", "placed", "error_resets",
               "fsm_phases")
 EPI = {name: k for k, name in enumerate(EPI_FIELDS)}
 STAT_FIELDS = ("sum_nefc", "sum_ncon", "sum_solver_iter", "substeps", "max_resid", "cyc_ik", "cyc_kinematics",
                "cyc_dynamics", "cyc_collision", "cyc_constraints", "cyc_solver", "cyc_integrate", "cyc_step_end",
-               "cyc_aux0", "cyc_aux1", "cyc_aux2", "cyc_aux3")
+               "cyc_aux0", "cyc_aux1", "cyc_aux2", "cyc_aux3", "exit_stall", "exit_cap")
 ACTION_MODES = ("abs_pos", "ee_pos_quat_g", "ee_pos_rot6d_g", "ee_pos_quat_g_rel", "ee_pos_rot6d_g_rel")
 ACTION_DIMS = (4, 8, 10, 8, 10)
 REWARD_TYPES = ("dense", "sparse", "staged")
@@ -135,6 +135,10 @@ class Sim:
             raise ValueError(f"action_mode must be one of {ACTION_MODES}, got '{action_mode}'")
         if reward_type not in REWARD_TYPES:
             raise ValueError(f"reward_type must be one of {REWARD_TYPES}, got '{reward_type}'")
+        if not (0 <= int(image_size) <= 1024):
+            raise ValueError(f"image_size must be in [0, 1024] (0 = no cameras), got {image_size}")
+        if int(num_envs) <= 0:
+            raise ValueError(f"num_envs must be positive, got {num_envs}")
         self.L = load()
         cfg = MMXConfig()
         self.L.mmx_config_default(C.byref(cfg))

@@ -1045,8 +1045,8 @@ DEV float contact_row(EnvSh& E, int row, int c, int rr) {
   const V3 t1 = contact_t1(n);
   const V3 u = rr == 0 ? n : (rr == 1 ? t1 : (rr == 2 ? cross(n, t1) : V3{0.f, 0.f, 0.f}));
   const V3 w = rr == 3 ? n : V3{0.f, 0.f, 0.f};
-  // pyramidal cone: one R for every edge, the first edge's diagApprox (tran + mu0^2 tran) x
-  // 2 mu0^2 / impratio (impratio = 1; MuJoCo mj_makeImpedance, as in oracle/or_physics.c)
+  // pyramidal cone: one R for every edge, A_hat = 2 mu0^2 (tran + mu0^2 tran) / impratio (impratio
+  // = 1), R = (1 - d) / d A_hat; pinned by the closed-form scenes of tests/test_physics_kat.py
   float idiag = cc[CG_IT];  // impedance ratio x diagApprox
   if (dim > 1) {
     const float mu0 = cc[CON_MU0];
@@ -1870,7 +1870,9 @@ DEV float chol_solve(EnvSh& E, const float* hrow, float v, int cpl) {
   return y;
 }
 
-DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
+// exit: 0 converged (gradient below tol), 1 no progress (step below 1e-9 with the gradient above
+// tol: an fp32 stall), 2 iteration cap reached above tol
+DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid, int& exit) {
   float* stats = E.stats;
   CLK_DECL;
   const int nefc = E.nefc, nsingle = E.nsingle;
@@ -1905,6 +1907,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
   SYNC();
   int it = 0;
   resid = 0.f;
+  exit = 2;
   // Hessian rows and gradient persist across iterations: after the first full pass each later one
   // adds only the groups whose edge weights changed (hess_grad_delta); act holds the lane's edge
   // active bits (bit 2q: edge 0 of slice q, bit 2q + 1: edge 1) the current H was built from
@@ -1964,7 +1967,10 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
     }
     resid = sqrtf(wave_sum(g * g)) / scale;
     PROBE(1, stats, STAT_T_AUX1);
-    if (resid < tol) break;
+    if (resid < tol) {
+      exit = 0;
+      break;
+    }
     const float pj = chol_solve(E, hrow, -g, cpl);
     if (nd >= 0) E.p[nd] = pj;
     SYNC();
@@ -2045,6 +2051,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
     stepn = sqrtf(wave_sum(stepn));
     if (stepn < 1e-9f) {
       it++;
+      exit = 1;
       break;
     }
     gpred = nd >= 0 ? fmaf(alpha, hp, g) : 0.f;
@@ -2055,6 +2062,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid) {
       if (rn < tol) {
         resid = rn;
         it++;
+        exit = 0;
         break;
       }
     }
@@ -2310,7 +2318,8 @@ DEV void mj_step_wave(int max_iter, float tol, EnvSh& E, float* con_dst) {
   make_constraints_wave(E);
   CLK(stats, STAT_T_CON);
   float resid = 0.f;
-  const int it = newton_wave(E, max_iter, tol, resid);
+  int exit = 0;
+  const int it = newton_wave(E, max_iter, tol, resid, exit);
   CLK(stats, STAT_T_SOLVE);
   integrate_wave(E);
   CLK(stats, STAT_T_INT);
@@ -2320,6 +2329,9 @@ DEV void mj_step_wave(int max_iter, float tol, EnvSh& E, float* con_dst) {
     stats[STAT_SOLVER_ITER] += (float)it;
     stats[STAT_SUBSTEPS] += 1.f;
     stats[STAT_RESID] = fmaxf(stats[STAT_RESID], resid);
+    // solver exits above tolerance, by cause (no progress in fp32 / iteration cap)
+    stats[STAT_EXIT_STALL] += exit == 1 ? 1.f : 0.f;
+    stats[STAT_EXIT_CAP] += exit == 2 ? 1.f : 0.f;
 #ifdef MMX_PHASE_CLOCK
     if (MMX_PROBE == 12) {  // row / contact count distribution (sizes the LDS row capacity)
       stats[STAT_T_AUX0] = fmaxf(stats[STAT_T_AUX0], (float)E.nefc);  // stored (basis) rows
@@ -2818,6 +2830,9 @@ DEV void step_end(const MMXState& S, int i, EnvSh& E) {
         S.done[3 * (size_t)i + 2] = 0;
         EPI(EPI_NERROR) += 1;
       } else {
+        // an episode ended by the expert's FSM alone (no termination, no time limit) is reported as
+        // truncated, so every autoreset carries a done flag (ended outside the MDP, like a time limit)
+        if (!terminated) S.done[3 * (size_t)i + 1] = 1;
         EPI(EPI_NSUCCESS) += succ_flag;
         EPI(EPI_NPLACED) += in_target_bin(S, i, E) ? 1 : 0;
       }
@@ -2927,7 +2942,8 @@ __device__ __attribute__((MMX_SUBSTEP_ATTR)) void substep(int max_iter, float to
     make_constraints_wave(E);
     CLK(stats, STAT_T_CON);
     float resid = 0.f;
-    const int it = newton_wave(E, max_iter, tol, resid);
+    int exit = 0;
+    const int it = newton_wave(E, max_iter, tol, resid, exit);
     CLK(stats, STAT_T_SOLVE);
     integrate_wave(E);
     CLK(stats, STAT_T_INT);
@@ -2937,6 +2953,8 @@ __device__ __attribute__((MMX_SUBSTEP_ATTR)) void substep(int max_iter, float to
       stats[STAT_SOLVER_ITER] += (float)it;
       stats[STAT_SUBSTEPS] += 1.f;
       stats[STAT_RESID] = fmaxf(stats[STAT_RESID], resid);
+      stats[STAT_EXIT_STALL] += exit == 1 ? 1.f : 0.f;
+      stats[STAT_EXIT_CAP] += exit == 2 ? 1.f : 0.f;
     }
   }
   // no trailing barrier: wave 1's next phase (collision) waits at the XSYNC after the next

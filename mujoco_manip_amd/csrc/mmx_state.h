@@ -73,6 +73,9 @@ enum {
   STAT_NEFC = 0, STAT_NCON, STAT_SOLVER_ITER, STAT_SUBSTEPS, STAT_RESID,
   STAT_T_IK, STAT_T_KIN, STAT_T_DYN, STAT_T_COL, STAT_T_CON, STAT_T_SOLVE, STAT_T_INT, STAT_T_END,
   STAT_T_AUX0, STAT_T_AUX1, STAT_T_AUX2, STAT_T_AUX3,  // sub-phase probes (see the kernel source)
+  // substeps whose Newton solve ended above the tolerance: no progress (step < 1e-9, an fp32 stall)
+  // / the iteration cap
+  STAT_EXIT_STALL, STAT_EXIT_CAP,
   STAT_N
 };
 

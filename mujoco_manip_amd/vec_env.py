@@ -4,12 +4,14 @@ Mirrors PickPlaceGymEnv (mujoco_manip/gym_env.py:39-602) with a leading env dime
 same constructor keywords, same 5 action modes, same numeric observation keys and reward
 types.  Differences, all documented in DESIGN.md:
   * observations are torch tensors on the GPU ([N, ...]); with image_size > 0 the
-    `image_overhead` / `image_wrist` keys are uint8 [N, S, S, 3] from the batched HIP renderer
-    (mmx_render.hip: hull geometry, MuJoCo lights; DESIGN.md §10), image_size = 0 skips them;
+    `image_overhead` / `image_wrist` keys are uint8 [N, S, S, 3] from the batched HIP rasteriser
+    (mmx_render.hip: per-body hull geometry, flat-lit with the scene's lights, no shadows or
+    specular; DESIGN.md §8), image_size = 0 skips them;
   * reset(seed=s) seeds env i with s + i (gymnasium vector convention); a list gives one
     seed per env;
-  * with autoreset=True an env that terminated/truncated is reset inside the same step
-    (the returned obs is the first obs of the new episode).
+  * with autoreset=True an env that terminated/truncated (or whose FSM expert finished: reported
+    as truncated) is reset inside the same step (the returned obs is the first obs of the new
+    episode).
 """
 from __future__ import annotations
 
@@ -159,10 +161,14 @@ class PickPlaceVecEnv:
     def solver_stats(self) -> dict:
         s = self.stats.double().sum(dim=0).cpu().numpy()
         sub = max(s[3], 1.0)
+        ks, kc = _lib.STAT_FIELDS.index("exit_stall"), _lib.STAT_FIELDS.index("exit_cap")
         out = {"mean_nefc": s[0] / sub, "mean_ncon": s[1] / sub, "mean_solver_iter": s[2] / sub,
-               "max_resid": float(self.stats[:, 4].max().item())}
+               "max_resid": float(self.stats[:, 4].max().item()), "substeps": int(s[3]),
+               # substeps whose Newton solve ended above the tolerance, by cause
+               "exit_above_tol": {"no_progress": int(s[ks]), "iteration_cap": int(s[kc]),
+                                  "fraction": float((s[ks] + s[kc]) / sub)}}
         # per-phase shader-clock cycles per substep per env (s_memtime ticks = shader cycles)
-        for k, name in enumerate(_lib.STAT_FIELDS[5:], start=5):
+        for k, name in enumerate(_lib.STAT_FIELDS[5:17], start=5):
             out[name + "_per_substep"] = s[k] / sub
         return out
 

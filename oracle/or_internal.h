@@ -55,6 +55,9 @@ struct or_env {
   double qfrc_smooth[NV], qacc_smooth[NV], qacc[NV], qfrc_constraint[NV];
   double solver_res;
   int solver_iter;
+  double solver_tol;       /* Newton: relative gradient tolerance (default 1e-13: parity tests) */
+  int solver_maxiter;      /* iteration cap (default 200) */
+  long solver_calls, solver_iters_total;
   /* gym episode state */
   or_pcg64 rng;
   int obj, bin, step_count;

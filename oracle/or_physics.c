@@ -396,13 +396,13 @@ static void make_constraints(or_env* e) {
       add_row(e, EFC_CONTACT, Jt[0], con->dist, tran, con->solref, con->solimp);
       continue;
     }
-    /* Pyramidal regulariser: every edge of the contact gets ONE common R, taken from the first
-     * edge's diagApprox (tran + mu0^2 tran) scaled by 2 mu0^2 / impratio (MuJoCo 3.x
-     * mj_makeImpedance's pyramidal-cone branch; the same expression is MJX's
-     * constraint.py `invweight * 2 * fri[0]**2 / m.opt.impratio`).  impratio = 1: neither
-     * pick_and_place_scene.xml nor panda.xml sets <option impratio>.  Neither the MuJoCo source nor
-     * its docs are in this image, so this is restated from the published implementation as
-     * remembered, not checked against it. */
+    /* Pyramidal regulariser (MuJoCo documentation, Computation / soft constraints: R = (1 - d) / d
+     * * A_hat): every edge of a pyramidal contact shares A_hat = 2 mu0^2 (t + mu0^2 t) / impratio,
+     * t = the bodies' translational invweight0, impratio = 1 (neither pick_and_place_scene.xml nor
+     * panda.xml sets <option impratio>).  Checked by tests/test_physics_kat.py against closed-form
+     * answers derived from these equations: the resting cubes' penetration (24 edges x D aref =
+     * m g), every contact edge's R at that depth, and the first substep of a slow slide (the primal
+     * problem with all 24 edges active), each on this oracle and on the HIP kernel. */
     (void)rot;
     const double mu0 = con->friction[0];
     const double diag = 2.0 * mu0 * mu0 / OR_IMPRATIO * (tran + mu0 * mu0 * tran);
@@ -455,7 +455,7 @@ static void solve_newton(or_env* e) {
   double r[OR_MAXEFC], s[OR_MAXEFC], bp[OR_MAXEFC][2];
   double res = 0;
   int it;
-  for (it = 0; it < 200; it++) {
+  for (it = 0; it < e->solver_maxiter; it++) {
     double g[NV], dx[NV];
     for (int i = 0; i < NV; i++) dx[i] = x[i] - e->qacc_smooth[i];
     Mmul(e, dx, g);
@@ -481,7 +481,7 @@ static void solve_newton(or_env* e) {
       sc += e->qfrc_smooth[d] * e->qfrc_smooth[d];
     }
     res = sqrt(gn) / (1 + sqrt(sc));
-    if (res < 1e-13) break;
+    if (res < e->solver_tol) break;
     if (chol_factor(H, NV) != 0) break;
     double p[NV];
     for (int d = 0; d < NV; d++) p[d] = -g[d];
@@ -540,6 +540,8 @@ static void solve_newton(or_env* e) {
   }
   e->solver_res = res;
   e->solver_iter = it;
+  e->solver_calls++;
+  e->solver_iters_total += it;
   memcpy(e->qacc, x, sizeof(x));
   memset(e->qfrc_constraint, 0, sizeof(e->qfrc_constraint));
   for (int k = 0; k < n; k++) {
@@ -663,5 +665,22 @@ void or_get_contact(or_env* e, int i, int* geom, double* dist, double* pos, doub
 }
 void or_get_efc_force(or_env* e, double* f) { memcpy(f, e->efc_force, e->nefc * sizeof(double)); }
 double or_solver_residual(or_env* e) { return e->solver_res; }
+void or_set_solver(or_env* e, double tol, int maxiter) {
+  e->solver_tol = tol;
+  e->solver_maxiter = maxiter;
+}
+void or_solver_stats(or_env* e, long* calls, long* iters) {
+  *calls = e->solver_calls;
+  *iters = e->solver_iters_total;
+}
+int or_get_efc(or_env* e, int* type, double* pos, double* R, double* aref) {
+  for (int i = 0; i < e->nefc; i++) {
+    if (type) type[i] = e->efc_type[i];
+    if (pos) pos[i] = e->efc_pos[i];
+    if (R) R[i] = e->efc_R[i];
+    if (aref) aref[i] = e->efc_aref[i];
+  }
+  return e->nefc;
+}
 void or_get_qacc(or_env* e, double* qacc) { memcpy(qacc, e->qacc, sizeof(e->qacc)); }
 void or_get_mass_matrix(or_env* e, double* M) { memcpy(M, e->M, sizeof(e->M)); }

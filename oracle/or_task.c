@@ -428,6 +428,8 @@ or_env* or_create(int action_mode, int reward_type, int max_episode_steps, int r
   e->ntask = 9;
   for (int i = 0; i < 9; i++) { e->task_obj[i] = i / 3; e->task_bin[i] = i % 3; }
   e->fixed_obj = e->fixed_bin = -1;
+  e->solver_tol = 1e-13;
+  e->solver_maxiter = 200;
   or_pcg64_seed(&e->rng, 0);
   or_reset_keyframe(e);
   return e;

@@ -70,6 +70,13 @@ int or_nefc(or_env* e);
 void or_get_contact(or_env* e, int i, int* geom, double* dist, double* pos, double* frame);
 void or_get_efc_force(or_env* e, double* f);
 double or_solver_residual(or_env* e);
+/* Newton tolerance / iteration cap (defaults 1e-13 / 200 for the parity tests; MuJoCo's defaults
+ * are 1e-8 / 100, which the CPU baseline uses) and (solves, iterations) counted since creation */
+void or_set_solver(or_env* e, double tol, int maxiter);
+void or_solver_stats(or_env* e, long* calls, long* iters);
+/* constraint rows of the last solve: type (0 equality, 1 limit, 2 contact edge), pos, R, aref;
+ * returns nefc (NULL skips a field; arrays hold OR_MAXEFC) */
+int or_get_efc(or_env* e, int* type, double* pos, double* R, double* aref);
 void or_get_qacc(or_env* e, double* qacc);
 void or_get_mass_matrix(or_env* e, double* M); /* qM (dense NV x NV, CRBA + armature) of the last forward */
 void or_get_obs(or_env* e, float* obs85);

@@ -67,6 +67,10 @@ def lib():
         L.or_solver_residual.restype = C.c_double
         L.or_solver_residual.argtypes = [C.c_void_p]
         L.or_get_qacc.argtypes = [C.c_void_p, dp]
+        L.or_set_solver.argtypes = [C.c_void_p, C.c_double, C.c_int]
+        L.or_solver_stats.argtypes = [C.c_void_p, C.POINTER(C.c_long), C.POINTER(C.c_long)]
+        L.or_get_efc.restype = C.c_int
+        L.or_get_efc.argtypes = [C.c_void_p, ip, dp, dp, dp]
         L.or_get_mass_matrix.argtypes = [C.c_void_p, dp]
         L.or_get_obs.argtypes = [C.c_void_p, fp]
         L.or_get_initial_ee.argtypes = [C.c_void_p, dp]
@@ -268,6 +272,25 @@ class OracleEnv:
 
     def solver_residual(self):
         return lib().or_solver_residual(self.ptr)
+
+    def set_solver(self, tol=1e-13, maxiter=200):
+        """Newton tolerance / iteration cap (defaults: the parity tests' 1e-13 / 200; MuJoCo's own
+        defaults are 1e-8 / 100)."""
+        lib().or_set_solver(self.ptr, float(tol), int(maxiter))
+
+    def solver_stats(self):
+        """(solves, Newton iterations) since creation."""
+        c, i = C.c_long(), C.c_long()
+        lib().or_solver_stats(self.ptr, C.byref(c), C.byref(i))
+        return c.value, i.value
+
+    def efc(self):
+        """Constraint rows of the last solve: dict of type (0 equality, 1 limit, 2 contact edge),
+        pos, R, aref arrays."""
+        n = 640
+        t, pos, R, aref = np.zeros(n, np.int32), np.zeros(n), np.zeros(n), np.zeros(n)
+        m = lib().or_get_efc(self.ptr, _i(t), _d(pos), _d(R), _d(aref))
+        return dict(type=t[:m], pos=pos[:m], R=R[:m], aref=aref[:m])
 
     def qacc(self):
         q = np.zeros(NV)

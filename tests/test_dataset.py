@@ -262,6 +262,56 @@ def test_generate_then_replay_reproduces_trajectory(tmp_path):
         np.testing.assert_allclose(r6["obs_state"][j][:20], rec[1:21], atol=1e-4)
 
 
+def oracle_replay(path, episode_index, action_key):
+    """scripts/replay_actions.py:58-148 on the oracle: the episode's seed / task from
+    metadata.json, a fresh env in the key's action mode, one step per recorded action, and per
+    frame the decoded target, the EE position (robot.ee_pos after the step) and their distance."""
+    import oracle_py as O
+
+    from mujoco_manip_amd import replay as R
+
+    _, md, frames = D.read_lerobot_v3(path)
+    seed, task, sx, sy = R.episode_setup(md, episode_index)
+    mode = action_key.replace("action.", "").replace(".", "_")
+    e = O.OracleEnv(action_mode=mode, reward_type="staged", randomize_objects=seed is not None,
+                    spawn_x_range=sx, spawn_y_range=sy)
+    e.reset(seed=seed, task=None if task is None else (OBJECTS.index(task[0]), BINS.index(task[1])))
+    T_init = e.initial_ee()
+    tgt, ee = [], []
+    for a in frames[episode_index][action_key]:
+        obs, *_ = e.step(a)
+        tgt.append(O.decode_action(mode, a, T_init)[0])
+        ee.append(obs[:3].astype(float))
+    tgt, ee = np.array(tgt), np.array(ee)
+    return tgt, ee, np.linalg.norm(ee - tgt, axis=1)
+
+
+@pytest.mark.gpu
+def test_replay_report_matches_oracle(tmp_path):
+    """f4 against the oracle: a generated dataset's absolute-quaternion and
+    relative-6D actions replayed through the HIP path (replay.replay, all episodes in one batch)
+    and through the oracle (the reference's replay loop, replay_actions.py:128-148) give the same
+    per-frame report: decoded targets within 1e-5 m, EE positions within 5 mm (the
+    cube contacts of a whole episode are chaotic), errors within 5 mm per frame and 1 mm on the
+    episode mean."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs an MI355X")
+    from mujoco_manip_amd import replay as R
+
+    keys = ["observation.state", "action.ee.pos_quat_g", "action.ee.pos_rot6d_g_rel"]
+    path, _ = D.generate("user/rp", num_episodes=4, root=str(tmp_path), tasks="match", randomize_objects=True,
+                         seed=11, features=keys, num_envs=4)
+    for key in ("action.ee.pos_quat_g", "action.ee.pos_rot6d_g_rel"):
+        r = R.replay(path, None, key)
+        for j, ep in enumerate(r["episodes"]):
+            tgt, ee, err = oracle_replay(path, ep, key)
+            assert len(err) == len(r["err"][j])
+            np.testing.assert_allclose(r["target"][j], tgt, atol=1e-5, err_msg=f"{key} ep {ep}")
+            np.testing.assert_allclose(r["ee"][j], ee, atol=5e-3, err_msg=f"{key} ep {ep}")
+            assert np.abs(r["err"][j] - err).max() < 5e-3, (key, ep)
+            assert abs(r["err"][j].mean() - err.mean()) < 1e-3, (key, ep, r["err"][j].mean(), err.mean())
+
+
 @pytest.mark.gpu
 def test_image_frames_match_renderer_and_raycast(tmp_path):
     """f2 with cameras (generate_dataset.py:26-28, 250-260): the written PNG frames decode to

@@ -102,6 +102,27 @@ def test_bench_rejects_mismatched_world(monkeypatch):
     assert r.returncode != 0 and "WORLD_SIZE=1" in (r.stderr + r.stdout)
 
 
+def test_launcher_stops_peers_when_a_rank_dies():
+    """bench.py's own rank launcher (--gpus N without torchrun): rank 1 exits with 3 at once while
+    rank 0 would block (as in a collective waiting for the dead peer) for 120 s; the parent must
+    terminate rank 0 and return the failing rank's code well within the block."""
+    import time
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    code = ("import os, sys, time\n"
+            "if os.environ['RANK'] == '1': sys.exit(3)\n"
+            "time.sleep(120)\n")
+    t0 = time.monotonic()
+    rc = bench.launch_ranks(2, cmd=[sys.executable, "-c", code], grace_s=5.0)
+    assert rc == 3
+    assert time.monotonic() - t0 < 30.0
+    t0 = time.monotonic()
+    assert bench.launch_ranks(2, cmd=[sys.executable, "-c", "pass"]) == 0
+    assert time.monotonic() - t0 < 30.0
+
+
 @pytest.mark.gpu
 def test_two_rank_hip_rollout_matches_single_process(tmp_path):
     if not torch.cuda.is_available():

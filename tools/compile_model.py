@@ -725,6 +725,11 @@ def emit_header(model, path, real, prefix, guard):
     L.append(c_array(f"{P}geom_size", R, [(geoms[g]["size"] + [0, 0, 0])[:3] for g in col]))
     L.append(c_array(f"{P}geom_aabb", R, [geoms[g]["aabb"] for g in col]))
     L.append(c_array(f"{P}geom_rbound", R, [geoms[g]["rbound"] for g in col]))
+    # the kernel stores a contact as 4 basis rows and forms the pyramid edges from the tangent rows
+    # (mmx_kernels.hip edge_coef): a frictionless (condim 1) contact would get no edge at all
+    bad = [geoms[g].get("name", g) for g in col if geoms[g]["condim"] not in (3, 4)]
+    if bad:
+        raise SystemExit(f"compile_model: condim must be 3 or 4 for every colliding geom (kernel contact rows), got {bad}")
     L.append(c_array(f"{P}geom_condim", "int", [geoms[g]["condim"] for g in col]))
     L.append(c_array(f"{P}geom_friction", R, [geoms[g]["friction"] for g in col]))
     L.append(c_array(f"{P}geom_solref", R, [geoms[g]["solref"] for g in col]))
