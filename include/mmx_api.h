@@ -90,7 +90,8 @@ typedef struct {
                                 4 sub-phase probes (cycle fields: diagnostic build only, else 0), then
                                 the substeps whose solve ended above the tolerance: by no progress
                                 (step < 1e-9, an fp32 stall), by the iteration cap */
-  float* contacts;           /* [N][64][12] dist, pos3, normal3, mu3, dim, geom1, geom2 (last substep) */
+  float* contacts;           /* [N][64][13] dist, pos3, normal3, mu3 (slide, spin, roll), dim, geom1, geom2
+                                (last substep) */
   uint8_t* images;           /* [N][2][S][S][3] RGB of the overhead and wrist cameras (S = image_size),
                                 rendered after every reset / step / forward; NULL when image_size = 0 */
   uint8_t* seg;              /* [N][2][S][S] segment ids: 0 sky, 1 floor, 2 table, 3-5 bins (red, green,

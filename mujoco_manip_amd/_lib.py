@@ -16,7 +16,7 @@ import numpy as np
 from . import _build
 
 NQ, NV, NU, NOBS = 30, 27, 8, 85
-MAXCON, CON_F = 64, 12
+MAXCON, CON_F = 64, 13
 EPI_N, EPF_N, KIN_N, STAT_N = 18, 28, 63, 19
 EPI_FIELDS = ("obj", "bin", "step_count", "flags", "fsm_state", "fsm_task_index", "fsm_settle", "fsm_gripper_open",
               "fsm_has_target", "env_error", "ncon", "nefc", "episodes", "rng_has32", "successes", "placed", "error_resets",

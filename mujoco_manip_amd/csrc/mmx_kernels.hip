@@ -2989,6 +2989,25 @@ __device__ __attribute__((noinline)) void step_finish(const MMXState& S, int i) 
   step_end(S, i, E);
   store_env(S, i, E);
 }
+#ifdef MMX_PHASE_CLOCK
+// Diagnostic build only: per FSM state of the env step (the state the step's action was planned
+// in), the sums over env steps of the shader cycles of each phase (STAT_T_IK .. STAT_T_END), of
+// the whole step, of the solver iterations / MuJoCo rows / contacts, and the env-step count
+// (tools/gpu_probe.py fsm_profile).  Lane 0 of each env adds with global atomics.
+enum { FSMP_PHASES = STAT_T_END - STAT_T_IK + 1, FSMP_STEP = FSMP_PHASES, FSMP_ITER, FSMP_NEFC, FSMP_NCON, FSMP_COUNT,
+       FSMP_N };
+__device__ double g_fsm_prof[11 * FSMP_N];
+extern "C" hipError_t mmx_fsm_profile(double* out, int reset) {
+  hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fsm_prof), sizeof(g_fsm_prof));
+  if (e == hipSuccess && reset) {
+    static double z[11 * FSMP_N];
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_fsm_prof), z, sizeof(z));
+  }
+  return e;
+}
+extern "C" int mmx_fsm_profile_fields() { return FSMP_N; }
+#endif
+
 extern "C" __global__ void __launch_bounds__(STEP_WG) __attribute__((amdgpu_waves_per_eu(2, 2)))
 mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert, int base, int nsteps) {
   const int i = base + blockIdx.x;
@@ -3001,9 +3020,38 @@ mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert, int b
     }
     if (w0) step_begin(S, i, action, adim, expert);
     XSYNC();
+#ifdef MMX_PHASE_CLOCK
+    float snap[FSMP_N];
+    const int fsm = EPI(EPI_FSM_STATE);
+    const unsigned long long t_step = clk_now();
+    if (LANE == 0) {
+      for (int j = 0; j < FSMP_PHASES; j++) snap[j] = g_E.stats[STAT_T_IK + j];
+      snap[FSMP_ITER] = g_E.stats[STAT_SOLVER_ITER];
+      snap[FSMP_NEFC] = g_E.stats[STAT_NEFC];
+      snap[FSMP_NCON] = g_E.stats[STAT_NCON];
+    }
+#endif
     for (int sub = 0; sub < MMX_NSUBSTEP; sub++)
       substep(S.solver_max_iter, S.solver_tol, sub == MMX_NSUBSTEP - 1 ? contacts_dst(S, i) : nullptr);
+#ifdef MMX_PHASE_CLOCK
+    // (read before step_finish stores the record: an autoreset does not clear stats)
+    if (LANE == 0) {
+      double* g = g_fsm_prof + FSMP_N * min(max(fsm, 0), 10);
+      for (int j = 0; j < FSMP_PHASES; j++) atomicAdd(g + j, (double)(g_E.stats[STAT_T_IK + j] - snap[j]));
+      atomicAdd(g + FSMP_ITER, (double)(g_E.stats[STAT_SOLVER_ITER] - snap[FSMP_ITER]));
+      atomicAdd(g + FSMP_NEFC, (double)(g_E.stats[STAT_NEFC] - snap[FSMP_NEFC]));
+      atomicAdd(g + FSMP_NCON, (double)(g_E.stats[STAT_NCON] - snap[FSMP_NCON]));
+    }
+#endif
     if (w0) step_finish(S, i);
+#ifdef MMX_PHASE_CLOCK
+    if (LANE == 0) {
+      double* g = g_fsm_prof + FSMP_N * min(max(fsm, 0), 10);
+      atomicAdd(g + STAT_T_END - STAT_T_IK, (double)(g_E.stats[STAT_T_END] - snap[STAT_T_END - STAT_T_IK]));
+      atomicAdd(g + FSMP_STEP, (double)(clk_now() - t_step));
+      atomicAdd(g + FSMP_COUNT, 1.0);
+    }
+#endif
   }
 }
 

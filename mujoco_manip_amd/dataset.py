@@ -12,14 +12,15 @@ MI355X instead of one after another:
   reference loop); the slot is then re-reset with the next episode's seed and task
   (episode e: task `task_list[e % len(task_list)]`, seed `SeedSequence(seed).spawn(E)[e]`
   when `randomize_objects`, reference :267-277);
-* frames are gathered on device, copied to the host once, and written in the LeRobot v3.0
-  on-disk layout (parquet data files, `meta/info.json`, `meta/tasks.parquet`,
-  `meta/episodes/...parquet`, `meta/stats.json`) plus the reference's `metadata.json`
-  (generation config + `episode_seeds`, :306-319).
+* each step's frames are gathered on device and streamed to pinned host memory (device memory
+  O(envs)); finished episodes go to a streaming writer in the LeRobot v3.0 on-disk layout
+  (parquet data files, `meta/info.json`, `meta/tasks.parquet`, `meta/episodes/...parquet`,
+  `meta/stats.json`) plus the reference's `metadata.json` (generation config + `episode_seeds`,
+  :306-319), so host memory holds only the episodes in flight.
 
 Camera images (observation.images.overhead / .wrist, features.py:11-20, 224 x 224 RGB) come from
 the batched HIP renderer (mmx_render.hip): the PRE-step images of every active
-slot are gathered on device each step, PNG-encoded on the host and stored the way LeRobot stores
+slot are gathered on device each step, PNG-encoded by a host thread pool and stored the way LeRobot stores
 `dtype: image` features with use_videos=False (generate_dataset.py:250-260): a parquet struct
 column {bytes: PNG, path} per frame, per-channel image statistics in meta/stats.json.
 LeRobot itself is not importable here, so the on-disk layout follows LeRobot v3.0's documented
@@ -172,6 +173,7 @@ class Episode:
     seed: int | None
     frames: dict = field(default_factory=dict)  # feature -> np.ndarray [T, ...] (strings, PNG bytes: list)
     length: int = 0
+    image_stats: dict = field(default_factory=dict)  # image feature -> stats of a raw frame sample
 
 
 def resolve_tasks(task=None, tasks="all"):
@@ -227,15 +229,79 @@ def episode_seeds(seed: int, num_episodes: int) -> list[int]:
     return [_lib.episode_seed(seed, e) for e in range(num_episodes)]
 
 
+class _PinnedRing:
+    """Pinned host staging for the per-step frame copies: device tensors are copied with
+    non_blocking=True on a side stream that waits for the producing stream, an event marks
+    completion, and at most `depth` copies are in flight (older ones are waited first)."""
+
+    def __init__(self, dev, depth=4):
+        import torch
+
+        self.torch = torch
+        self.stream = torch.cuda.Stream(device=dev)
+        self.depth = depth
+        self.pending = []  # (event, host dict, payload)
+
+    def push(self, tensors: dict, payload):
+        torch = self.torch
+        self.stream.wait_stream(torch.cuda.current_stream(self.stream.device))
+        host = {}
+        with torch.cuda.stream(self.stream):
+            for k, v in tensors.items():
+                h = torch.empty(v.shape, dtype=v.dtype, pin_memory=True)
+                h.copy_(v, non_blocking=True)
+                v.record_stream(self.stream)
+                host[k] = h
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        self.pending.append((ev, host, payload))
+
+    def ready(self, block_over_depth=True):
+        """Completed copies, oldest first (waits for the oldest ones beyond `depth`)."""
+        out = []
+        while self.pending and (self.pending[0][0].query() or (block_over_depth and len(self.pending) > self.depth)):
+            ev, host, payload = self.pending.pop(0)
+            ev.synchronize()
+            out.append(({k: v.numpy() for k, v in host.items()}, payload))
+        return out
+
+    def drain(self):
+        out = []
+        while self.pending:
+            ev, host, payload = self.pending.pop(0)
+            ev.synchronize()
+            out.append(({k: v.numpy() for k, v in host.items()}, payload))
+        return out
+
+
+def _raw_image_stats(frames_u8: list) -> dict:
+    """Per-channel statistics of an image feature from raw uint8 frames [H, W, 3] (a sample),
+    pixels scaled to [0, 1], shaped (3, 1, 1) as LeRobot keeps them; also the raw sums so episode
+    statistics can be merged into the dataset's."""
+    x = np.stack(frames_u8).reshape(-1, 3).astype(np.float64) / 255.0
+    shape = lambda v: [[[float(a)]] for a in v]  # noqa: E731
+    return {"min": shape(x.min(0)), "max": shape(x.max(0)), "mean": shape(x.mean(0)), "std": shape(x.std(0)),
+            "_sum": x.sum(0).tolist(), "_sumsq": (x * x).sum(0).tolist(), "_n": int(len(x))}
+
+
 def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type="staged", randomize_objects=False,
                      seed=0, spawn_x_range=(-0.20, 0.20), spawn_y_range=(0.30, 0.45), num_envs=1024, device=0,
-                     max_gym_steps=5000, on_step=None):
+                     max_gym_steps=5000, on_step=None, sink=None, png_workers=None, image_size=IMAGE_SIZE,
+                     stats_frames=8):
     """Run `num_episodes` reference run_episode loops (generate_dataset.py:83-198) side by side.
 
-    Returns (episodes, seeds): a list of Episode with per-feature frame arrays in step order
-    (image features: lists of PNG bytes).  on_step(slots, episode_ids, env), when given, sees the
-    env before each batched step (the state the step's frames were recorded from).
+    Streaming: each step's frames (active slots only) are gathered on the device, copied to pinned
+    host memory on a side stream and split into their episodes on the host; camera frames are
+    PNG-encoded by a pool of `png_workers` threads (the reference's image writer uses 4,
+    generate_dataset.py:260) while the device runs the next steps.  Device memory is O(envs): no
+    frame stays on the device after its copy.  A finished episode (FSM DONE) is handed to
+    `sink(episode)` in episode-index order as soon as its frames are encoded, so the host holds
+    only the episodes in flight; without a sink the episodes are returned as a list.
+    on_step(slots, episode_ids, env), when given, sees the env before each batched step.
+    Returns (episodes or None, seeds).
     """
+    import concurrent.futures as cf
+
     import torch
 
     from .vec_env import PickPlaceVecEnv
@@ -243,19 +309,26 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
     E = int(num_episodes)
     seeds = episode_seeds(seed, E) if randomize_objects else None
     N = max(1, min(int(num_envs), E))
+    use_images = bool(set(feature_keys) & set(IMAGE_KEYS))
     env = PickPlaceVecEnv(N, tasks=[tuple(t) for t in task_list], action_mode="abs_pos", reward_type=reward_type,
                           randomize_objects=randomize_objects, spawn_x_range=tuple(spawn_x_range),
                           spawn_y_range=tuple(spawn_y_range), autoreset=False, device=device,
-                          image_size=IMAGE_SIZE if set(feature_keys) & set(IMAGE_KEYS) else 0)
+                          image_size=image_size if use_images else 0)
     dev = env.device
     need_actions = bool(set(feature_keys) & set(ACTION_KEYS))
     need_reward = "next.reward" in feature_keys and reward_type == "staged"
     obs_feats = [(k, f) for k, f in OBS_TO_FEATURE.items() if f in feature_keys]
     img_feats = [(cam, f) for cam, f in enumerate(IMAGE_KEYS) if f in feature_keys]
+    pool = cf.ThreadPoolExecutor(max_workers=png_workers or min(16, os.cpu_count() or 4)) if img_feats else None
 
     eps = [Episode(e, *task_list[e % len(task_list)], seeds[e] if seeds else None) for e in range(E)]
+    rows = [dict() for _ in range(E)]  # episode -> feature -> list of per-frame values (host)
     slot_ep = np.full(N, -1, np.int64)
     next_ep = 0
+    finished_marks = []  # (step index, episode): the episode's last frame is in steps < step index
+    out_eps = [] if sink is None else None
+    emitted = 0
+    done_eps = {}  # finished, awaiting in-order emission: episode -> True
 
     def assign(slots):
         nonlocal next_ep
@@ -275,16 +348,86 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
         if mask.any():
             env.sim.reset(seeds=sd if seeds else None, task_override=task, env_mask=mask)
 
+    steps_host = {}  # step id -> [host arrays of the step, episodes still reading it]
+    sid_counter = [0]
+
+    def absorb(host, payload):
+        """Index one step's host copy by episode (one row per active episode); images go to the
+        PNG pool straight away."""
+        slots, ep_ids = payload
+        if len(ep_ids) == 0:
+            return
+        sid = sid_counter[0]
+        sid_counter[0] += 1
+        steps_host[sid] = [host, len(ep_ids)]
+        for j, e in enumerate(ep_ids):
+            r = rows[e]
+            r.setdefault("_rows", []).append((sid, j))
+            for k in IMAGE_KEYS:
+                if k in host:
+                    im = host[k][j]
+                    lst = r.setdefault(k, [])
+                    if len(lst) < stats_frames:  # raw frames of the statistics sample
+                        r.setdefault(k + "/raw", []).append(im.copy())
+                    lst.append(pool.submit(png_encode, im))
+
+    def finalize(e):
+        ep = eps[e]
+        r = rows[e]
+        refs = r.get("_rows", [])
+        ep.length = len(refs)
+        ep.image_stats = {}
+        for k in feature_keys:
+            if k in IMAGE_KEYS:
+                ep.frames[k] = [f.result() for f in r.get(k, [])]
+                raw = r.get(k + "/raw")
+                ep.image_stats[k] = _raw_image_stats(raw) if raw else None
+            elif k == "observation.phase_description":
+                ep.frames[k] = [phase_description(steps_host[sid][0]["_fsm"][j], ep.obj, ep.bin) for sid, j in refs]
+            elif refs and k in steps_host[refs[0][0]][0]:
+                ep.frames[k] = np.stack([steps_host[sid][0][k][j] for sid, j in refs]).astype(np.float32)
+        for sid, _ in refs:  # release step buffers no episode reads any more
+            steps_host[sid][1] -= 1
+            if steps_host[sid][1] == 0:
+                del steps_host[sid]
+        rows[e] = None
+
+    def emit_ready(block=False):
+        nonlocal emitted
+        while emitted < E and emitted in done_eps:
+            e = emitted
+            r = rows[e]
+            if not block and r is not None and any(not f.done() for k in IMAGE_KEYS for f in r.get(k, [])):
+                return
+            finalize(e)
+            del done_eps[e]
+            if sink is not None:
+                sink(eps[e])
+                eps[e] = None  # the sink owns it now: host memory stays bounded by the episodes in flight
+            else:
+                out_eps.append(eps[e])
+            emitted += 1
+
+    ring = _PinnedRing(dev)
+    step_no = 0
+
+    def process(items):
+        for host, payload in items:
+            absorb(host, payload[:2])
+            for e in payload[2]:  # episodes whose last frame was in this or an earlier step
+                done_eps[e] = True
+
     assign(range(N))
-    rec = []  # per step: (slots [k], ep ids [k], dict feature -> device tensor [k, ...], fsm [k])
-    steps = 0
     fsm_view = env._epi[:, 4]
     while (slot_ep >= 0).any():
-        if steps >= max_gym_steps:
+        if step_no >= max_gym_steps:
             raise RuntimeError(f"episodes {sorted(set(slot_ep[slot_ep >= 0].tolist()))} did not finish "
                                f"within {max_gym_steps} gym steps")
+        # the slot reassignment needs the FSM state on the host: one small copy per step (the
+        # frames themselves never wait for it)
         done_before = (fsm_view == FSM_DONE).cpu().numpy()
         finished = np.where((slot_ep >= 0) & done_before)[0]
+        fin_eps = [int(slot_ep[s]) for s in finished]
         if len(finished):
             for s in finished:
                 slot_ep[s] = -1
@@ -292,6 +435,10 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
             done_before = (fsm_view == FSM_DONE).cpu().numpy()
         act_slots = np.where((slot_ep >= 0) & ~done_before)[0]
         if len(act_slots) == 0:
+            if fin_eps:
+                ring.push({}, (act_slots, np.zeros(0, np.int64), fin_eps))
+            process(ring.ready())
+            emit_ready()
             continue
         idx = torch.as_tensor(act_slots, device=dev)
         obs_pre = env._obs.index_select(0, idx)  # PRE-step obs (from the reset or the previous step)
@@ -309,38 +456,26 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
             for k in ACTION_KEYS:
                 if k in feature_keys:
                     frame[k] = enc[k]
-        fsm_after = fsm_view.index_select(0, idx).clone()
+        frame["_fsm"] = fsm_view.index_select(0, idx)
         if on_step is not None:
             on_step(act_slots, slot_ep[act_slots].copy(), env)
         env.step(action)
         if need_reward:
-            frame["next.reward"] = env._rc.index_select(0, idx).clone()
-        rec.append((act_slots, slot_ep[act_slots].copy(), frame, fsm_after))
-        steps += 1
+            frame["next.reward"] = env._rc.index_select(0, idx)
+        ring.push(frame, (act_slots, slot_ep[act_slots].copy(), fin_eps))
+        process(ring.ready())
+        emit_ready()
+        step_no += 1
+    process(ring.drain())
+    for e in range(E):  # every slot finished: the remaining episodes end here
+        if rows[e] is not None and e not in done_eps and eps[e] is not None:
+            done_eps[e] = True
+    emit_ready(block=True)
     torch.cuda.synchronize(dev)
-
-    # host side: split the step records into per-episode frame arrays (step order is frame order)
-    per_ep_rows = [[] for _ in range(E)]
-    host = []
-    for r, (slots, ep_ids, frame, fsm) in enumerate(rec):
-        hf = {k: v.cpu().numpy() for k, v in frame.items()}
-        for _, f in img_feats:
-            hf[f] = [png_encode(im) for im in hf[f]]
-        host.append((hf, fsm.cpu().numpy()))
-        for j, e in enumerate(ep_ids):
-            per_ep_rows[e].append((r, j))
-    for e, rows in enumerate(per_ep_rows):
-        ep = eps[e]
-        ep.length = len(rows)
-        for k in feature_keys:
-            if k == "observation.phase_description":
-                ep.frames[k] = [phase_description(host[r][1][j], ep.obj, ep.bin) for r, j in rows]
-            elif k in IMAGE_KEYS:
-                ep.frames[k] = [host[r][0][k][j] for r, j in rows]
-            elif host and k in host[0][0]:
-                ep.frames[k] = np.stack([host[r][0][k][j] for r, j in rows]).astype(np.float32)
     env.close()
-    return eps, seeds
+    if pool is not None:
+        pool.shutdown()
+    return out_eps, seeds
 
 
 # ----------------------------------------------------------------------------- LeRobot v3.0 writer
@@ -350,129 +485,171 @@ def _feature_stats(x: np.ndarray) -> dict:
             "std": x.std(0).tolist(), "count": [int(len(x))]}
 
 
-def _image_stats(pngs, max_frames=32) -> dict:
-    """Per-channel statistics of an image feature over a frame sample, pixels scaled to [0, 1],
-    shaped (3, 1, 1) as LeRobot keeps them for image / video features."""
-    idx = np.linspace(0, len(pngs) - 1, min(len(pngs), max_frames)).astype(int)
-    x = np.stack([png_decode(pngs[i]) for i in idx]).astype(np.float64) / 255.0  # [F, H, W, 3]
-    c = x.reshape(-1, 3)
-    shape = lambda v: [[[float(a)]] for a in v]  # noqa: E731
-    return {"min": shape(c.min(0)), "max": shape(c.max(0)), "mean": shape(c.mean(0)), "std": shape(c.std(0)),
-            "count": [int(len(pngs))]}
-
-
-def write_lerobot_v3(root: str, repo_id: str, episodes, features: dict, *, fps=CONTROL_FPS,
-                     robot_type="franka_panda", chunks_size=1000, data_files_size_in_mb=100, extra_info=None):
-    """Write episodes in the LeRobot v3.0 layout (use_videos=False: image features embedded as
-    parquet structs {bytes: PNG, path}).
+class LeRobotWriter:
+    """Streaming LeRobot v3.0 writer (use_videos=False: image features embedded as parquet structs
+    {bytes: PNG, path}).  Episodes are added one at a time in episode-index order and appended to
+    the open data file (pyarrow ParquetWriter), which rolls over at `data_files_size_in_mb`;
+    statistics accumulate as running sums, so memory does not grow with the dataset.
 
     data/chunk-XXX/file-YYY.parquet  frames of consecutive episodes (features + timestamp,
                                      frame_index, episode_index, index, task_index)
     meta/info.json, meta/tasks.parquet, meta/episodes/chunk-000/file-000.parquet, meta/stats.json
     """
-    import pyarrow as pa
-    import pyarrow.parquet as pq
 
-    os.makedirs(root, exist_ok=True)
-    tasks = []
-    for ep in episodes:
+    def __init__(self, root: str, repo_id: str, features: dict, *, fps=CONTROL_FPS, robot_type="franka_panda",
+                 chunks_size=1000, data_files_size_in_mb=100):
+        import pyarrow as pa
+
+        self.pa = pa
+        self.root, self.repo_id, self.features, self.fps = root, repo_id, features, fps
+        self.robot_type, self.chunks_size, self.data_files_size_in_mb = robot_type, chunks_size, data_files_size_in_mb
+        os.makedirs(root, exist_ok=True)
+        self.num_keys = [k for k, f in features.items() if f["dtype"] == "float32"]
+        self.str_keys = [k for k, f in features.items() if f["dtype"] == "string"]
+        self.img_keys = [k for k, f in features.items() if f["dtype"] == "image"]
+        self.img_type = pa.struct([("bytes", pa.binary()), ("path", pa.string())])
+        self.tasks, self.task_idx = [], {}
+        self.ep_rows = []
+        self.chunk, self.fileno, self.start = 0, 0, 0
+        self.writer, self.cur_bytes = None, 0
+        self.limit = data_files_size_in_mb * 1024 * 1024
+        self.num_acc = {}  # feature -> [min, max, sum, sumsq, count]
+        self.img_acc = {}  # feature -> [min, max, sum, sumsq, pixels, frames]
+        self.n_episodes = 0
+
+    def _task(self, ep):
         t = make_task_string(ep.obj, ep.bin)
-        if t not in tasks:
-            tasks.append(t)
-    task_idx = {t: i for i, t in enumerate(tasks)}
-    num_keys = [k for k, f in features.items() if f["dtype"] == "float32"]
-    str_keys = [k for k, f in features.items() if f["dtype"] == "string"]
-    img_keys = [k for k, f in features.items() if f["dtype"] == "image"]
-    img_type = pa.struct([("bytes", pa.binary()), ("path", pa.string())])
+        if t not in self.task_idx:
+            self.task_idx[t] = len(self.tasks)
+            self.tasks.append(t)
+        return t
 
-    def ep_table(ep, start):
+    def _table(self, ep, start):
+        pa = self.pa
         n = ep.length
         cols, fields = {}, []
-        for k in num_keys:
-            dim = int(np.prod(features[k]["shape"]))
+        for k in self.num_keys:
+            dim = int(np.prod(self.features[k]["shape"]))
             arr = np.asarray(ep.frames[k], np.float32).reshape(n, dim)
             cols[k] = pa.FixedSizeListArray.from_arrays(pa.array(arr.ravel(), pa.float32()), dim)
             fields.append(pa.field(k, pa.list_(pa.float32(), dim)))
-        for k in str_keys:
+        for k in self.str_keys:
             cols[k] = pa.array(list(ep.frames[k]), pa.string())
             fields.append(pa.field(k, pa.string()))
-        for k in img_keys:  # LeRobot's embedded image layout (images/<key>/episode_<e>/frame_<i>.png)
+        for k in self.img_keys:  # LeRobot's embedded image layout (images/<key>/episode_<e>/frame_<i>.png)
             cols[k] = pa.array([{"bytes": b, "path": f"images/{k}/episode_{ep.index:06d}/frame_{i:06d}.png"}
-                                for i, b in enumerate(ep.frames[k])], img_type)
-            fields.append(pa.field(k, img_type))
+                                for i, b in enumerate(ep.frames[k])], self.img_type)
+            fields.append(pa.field(k, self.img_type))
         fi = np.arange(n, dtype=np.int64)
-        extra = {"timestamp": pa.array((fi / fps).astype(np.float32)), "frame_index": pa.array(fi),
+        extra = {"timestamp": pa.array((fi / self.fps).astype(np.float32)), "frame_index": pa.array(fi),
                  "episode_index": pa.array(np.full(n, ep.index, np.int64)), "index": pa.array(start + fi),
-                 "task_index": pa.array(np.full(n, task_idx[make_task_string(ep.obj, ep.bin)], np.int64))}
+                 "task_index": pa.array(np.full(n, self.task_idx[make_task_string(ep.obj, ep.bin)], np.int64))}
         for k, v in extra.items():
             cols[k] = v
             fields.append(pa.field(k, v.type))
         return pa.Table.from_arrays([cols[f.name] for f in fields], schema=pa.schema(fields))
 
-    limit = data_files_size_in_mb * 1024 * 1024
-    ep_rows = []
-    chunk, fileno, cur, cur_bytes, start = 0, 0, [], 0, 0
+    def _close_file(self):
+        if self.writer is not None:
+            self.writer.close()
+            self.writer = None
+            self.fileno += 1
+            if self.fileno >= self.chunks_size:
+                self.chunk, self.fileno = self.chunk + 1, 0
+            self.cur_bytes = 0
 
-    def flush():
-        nonlocal chunk, fileno, cur, cur_bytes
-        if not cur:
-            return
-        d = os.path.join(root, "data", f"chunk-{chunk:03d}")
-        os.makedirs(d, exist_ok=True)
-        pq.write_table(pa.concat_tables(cur), os.path.join(d, f"file-{fileno:03d}.parquet"))
-        fileno += 1
-        if fileno >= chunks_size:
-            chunk, fileno = chunk + 1, 0
-        cur, cur_bytes = [], 0
+    def add_episode(self, ep):
+        import pyarrow.parquet as pq
 
-    for ep in sorted(episodes, key=lambda e: e.index):
-        tab = ep_table(ep, start)
-        if cur and cur_bytes + tab.nbytes > limit:
-            flush()
+        self._task(ep)
+        tab = self._table(ep, self.start)
+        if self.writer is not None and self.cur_bytes + tab.nbytes > self.limit:
+            self._close_file()
+        if self.writer is None:
+            d = os.path.join(self.root, "data", f"chunk-{self.chunk:03d}")
+            os.makedirs(d, exist_ok=True)
+            self.writer = pq.ParquetWriter(os.path.join(d, f"file-{self.fileno:03d}.parquet"), tab.schema)
+        self.writer.write_table(tab)
+        self.cur_bytes += tab.nbytes
         row = {"episode_index": ep.index, "tasks": [make_task_string(ep.obj, ep.bin)], "length": ep.length,
-               "data/chunk_index": chunk, "data/file_index": fileno, "dataset_from_index": start,
-               "dataset_to_index": start + ep.length, "meta/episodes/chunk_index": 0,
+               "data/chunk_index": self.chunk, "data/file_index": self.fileno, "dataset_from_index": self.start,
+               "dataset_to_index": self.start + ep.length, "meta/episodes/chunk_index": 0,
                "meta/episodes/file_index": 0}
-        for k in num_keys:
-            for s, v in _feature_stats(np.asarray(ep.frames[k])).items():
-                row[f"stats/{k}/{s}"] = v
-        for k in img_keys:
-            for s, v in _image_stats(ep.frames[k], 8).items():
-                row[f"stats/{k}/{s}"] = v
-        ep_rows.append(row)
-        cur.append(tab)
-        cur_bytes += tab.nbytes
-        start += ep.length
-    flush()
+        for k in self.num_keys:
+            x = np.asarray(ep.frames[k], np.float64).reshape(ep.length, -1)
+            for st, v in _feature_stats(x).items():
+                row[f"stats/{k}/{st}"] = v
+            acc = self.num_acc.get(k)
+            mn, mx, sm, sq = x.min(0), x.max(0), x.sum(0), (x * x).sum(0)
+            self.num_acc[k] = [mn, mx, sm, sq, len(x)] if acc is None else \
+                [np.minimum(acc[0], mn), np.maximum(acc[1], mx), acc[2] + sm, acc[3] + sq, acc[4] + len(x)]
+        for k in self.img_keys:
+            st = (getattr(ep, "image_stats", None) or {}).get(k)
+            if st is None:  # episodes built elsewhere: decode a frame sample
+                st = _raw_image_stats([png_decode(ep.frames[k][i])
+                                       for i in np.linspace(0, ep.length - 1, min(ep.length, 8)).astype(int)])
+            for name in ("min", "max", "mean", "std"):
+                row[f"stats/{k}/{name}"] = st[name]
+            row[f"stats/{k}/count"] = [int(ep.length)]
+            mn = np.array([c[0][0] for c in st["min"]])
+            mx = np.array([c[0][0] for c in st["max"]])
+            acc = self.img_acc.get(k)
+            vals = [mn, mx, np.array(st["_sum"]), np.array(st["_sumsq"]), st["_n"], ep.length]
+            self.img_acc[k] = vals if acc is None else [np.minimum(acc[0], mn), np.maximum(acc[1], mx), acc[2] + vals[2],
+                                                        acc[3] + vals[3], acc[4] + vals[4], acc[5] + vals[5]]
+        self.ep_rows.append(row)
+        self.start += ep.length
+        self.n_episodes += 1
 
-    meta = os.path.join(root, "meta")
-    os.makedirs(os.path.join(meta, "episodes", "chunk-000"), exist_ok=True)
-    pq.write_table(pa.Table.from_pylist(ep_rows), os.path.join(meta, "episodes", "chunk-000", "file-000.parquet"))
-    pq.write_table(pa.table({"task_index": pa.array(np.arange(len(tasks), dtype=np.int64)),
-                             "task": pa.array(tasks, pa.string())}), os.path.join(meta, "tasks.parquet"))
-    stats = {}
-    for k in num_keys:
-        allf = np.concatenate([np.asarray(ep.frames[k], np.float32).reshape(ep.length, -1) for ep in episodes])
-        stats[k] = _feature_stats(allf)
-    for k in img_keys:
-        stats[k] = _image_stats([b for ep in episodes for b in ep.frames[k]])
-    with open(os.path.join(meta, "stats.json"), "w") as f:
-        json.dump(stats, f, indent=1)
-    feats = {k: {"dtype": v["dtype"], "shape": list(v["shape"]), "names": v["names"]} for k, v in features.items()}
-    for k, dt in (("timestamp", "float32"), ("frame_index", "int64"), ("episode_index", "int64"),
-                  ("index", "int64"), ("task_index", "int64")):
-        feats[k] = {"dtype": dt, "shape": [1], "names": None}
-    info = {"codebase_version": "v3.0", "robot_type": robot_type, "total_episodes": len(episodes),
-            "total_frames": int(start), "total_tasks": len(tasks), "chunks_size": chunks_size,
-            "data_files_size_in_mb": data_files_size_in_mb, "video_files_size_in_mb": 500, "fps": fps,
-            "splits": {"train": f"0:{len(episodes)}"},
-            "data_path": "data/chunk-{chunk_index:03d}/file-{file_index:03d}.parquet", "video_path": None,
-            "features": feats}
-    if extra_info:
-        info.update(extra_info)
-    with open(os.path.join(meta, "info.json"), "w") as f:
-        json.dump(info, f, indent=4)
-    return info
+    def close(self, extra_info=None):
+        import pyarrow as pa
+        import pyarrow.parquet as pq
+
+        self._close_file()
+        meta = os.path.join(self.root, "meta")
+        os.makedirs(os.path.join(meta, "episodes", "chunk-000"), exist_ok=True)
+        rows = sorted(self.ep_rows, key=lambda r: r["episode_index"])
+        pq.write_table(pa.Table.from_pylist(rows), os.path.join(meta, "episodes", "chunk-000", "file-000.parquet"))
+        pq.write_table(pa.table({"task_index": pa.array(np.arange(len(self.tasks), dtype=np.int64)),
+                                 "task": pa.array(self.tasks, pa.string())}), os.path.join(meta, "tasks.parquet"))
+        stats = {}
+        for k, (mn, mx, sm, sq, n) in self.num_acc.items():
+            mean = sm / n
+            stats[k] = {"min": mn.tolist(), "max": mx.tolist(), "mean": mean.tolist(),
+                        "std": np.sqrt(np.maximum(sq / n - mean * mean, 0.0)).tolist(), "count": [int(n)]}
+        shape = lambda v: [[[float(a)]] for a in v]  # noqa: E731
+        for k, (mn, mx, sm, sq, npx, nfr) in self.img_acc.items():
+            mean = sm / npx
+            stats[k] = {"min": shape(mn), "max": shape(mx), "mean": shape(mean),
+                        "std": shape(np.sqrt(np.maximum(sq / npx - mean * mean, 0.0))), "count": [int(nfr)]}
+        with open(os.path.join(meta, "stats.json"), "w") as f:
+            json.dump(stats, f, indent=1)
+        feats = {k: {"dtype": v["dtype"], "shape": list(v["shape"]), "names": v["names"]}
+                 for k, v in self.features.items()}
+        for k, dt in (("timestamp", "float32"), ("frame_index", "int64"), ("episode_index", "int64"),
+                      ("index", "int64"), ("task_index", "int64")):
+            feats[k] = {"dtype": dt, "shape": [1], "names": None}
+        info = {"codebase_version": "v3.0", "robot_type": self.robot_type, "total_episodes": self.n_episodes,
+                "total_frames": int(self.start), "total_tasks": len(self.tasks), "chunks_size": self.chunks_size,
+                "data_files_size_in_mb": self.data_files_size_in_mb, "video_files_size_in_mb": 500, "fps": self.fps,
+                "splits": {"train": f"0:{self.n_episodes}"},
+                "data_path": "data/chunk-{chunk_index:03d}/file-{file_index:03d}.parquet", "video_path": None,
+                "features": feats}
+        if extra_info:
+            info.update(extra_info)
+        with open(os.path.join(meta, "info.json"), "w") as f:
+            json.dump(info, f, indent=4)
+        return info
+
+
+def write_lerobot_v3(root: str, repo_id: str, episodes, features: dict, *, fps=CONTROL_FPS,
+                     robot_type="franka_panda", chunks_size=1000, data_files_size_in_mb=100, extra_info=None):
+    """Write a list of episodes in the LeRobot v3.0 layout (LeRobotWriter, episodes in index order)."""
+    w = LeRobotWriter(root, repo_id, features, fps=fps, robot_type=robot_type, chunks_size=chunks_size,
+                      data_files_size_in_mb=data_files_size_in_mb)
+    for ep in sorted(episodes, key=lambda e: e.index):
+        w.add_episode(ep)
+    return w.close(extra_info)
 
 
 def read_lerobot_v3(root: str):
@@ -512,16 +689,19 @@ def read_lerobot_v3(root: str):
 # ----------------------------------------------------------------------------- entry point
 def generate(repo_id, num_episodes=100, root="./datasets", task=None, tasks="all", reward_type="staged",
              randomize_objects=False, seed=0, spawn_x_range=(-0.20, 0.20), spawn_y_range=(0.30, 0.45),
-             features=None, num_envs=1024, device=0):
-    """generate_dataset.main (generate_dataset.py:201-333) with the episodes batched on the GPU."""
+             features=None, num_envs=1024, device=0, png_workers=None, image_size=IMAGE_SIZE):
+    """generate_dataset.main (generate_dataset.py:201-333) with the episodes batched on the GPU and
+    streamed to the LeRobot writer as they finish."""
     if not repo_id:
         raise ValueError("repo_id is required (e.g. repo_id=user/pick-place)")
     task_list = resolve_tasks(task, tasks)
     feats = resolve_features(features, reward_type)
-    eps, seeds = collect_episodes(num_episodes, task_list, set(feats), reward_type=reward_type,
-                                  randomize_objects=randomize_objects, seed=seed, spawn_x_range=spawn_x_range,
-                                  spawn_y_range=spawn_y_range, num_envs=num_envs, device=device)
     path = os.path.join(root, repo_id)
+    writer = LeRobotWriter(path, repo_id, feats)
+    _, seeds = collect_episodes(num_episodes, task_list, set(feats), reward_type=reward_type,
+                                randomize_objects=randomize_objects, seed=seed, spawn_x_range=spawn_x_range,
+                                spawn_y_range=spawn_y_range, num_envs=num_envs, device=device, sink=writer.add_episode,
+                                png_workers=png_workers, image_size=image_size)
     cfg = {"repo_id": repo_id, "num_episodes": int(num_episodes), "root": root,
            "task": list(task) if task is not None else None, "tasks": tasks, "reward_type": reward_type,
            "randomize_objects": bool(randomize_objects), "seed": int(seed), "spawn_x_range": list(spawn_x_range),
@@ -529,7 +709,7 @@ def generate(repo_id, num_episodes=100, root="./datasets", task=None, tasks="all
            "features": list(features) if features is not None else None}
     if seeds is not None:
         cfg["episode_seeds"] = [int(s) for s in seeds]
-    info = write_lerobot_v3(path, repo_id, eps, feats, extra_info={"generation_config": cfg})
+    info = writer.close(extra_info={"generation_config": cfg})
     with open(os.path.join(path, "metadata.json"), "w") as f:
         json.dump(cfg, f, indent=2)
     return path, info

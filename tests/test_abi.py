@@ -62,6 +62,20 @@ def test_state_layout_constants_match_header():
     assert len(names) == _lib.EPI_N == len(_lib.EPI_FIELDS)
     assert [n.split("=")[0].strip() for n in names][-4:] == ["EPI_NSUCCESS", "EPI_NPLACED", "EPI_NERROR", "EPI_PHASES"]
 
+    def enum_count(first, last):
+        """Value of `last` in the C enum that starts with `first` (explicit values honoured)."""
+        body = re.search(rf"enum \{{\s*({first}.*?){last}\s*\}}", src, re.S).group(1)
+        body = re.sub(r"//[^\n]*", "", body)
+        v = -1
+        for t in [t.strip() for t in body.replace("\n", " ").split(",") if t.strip()]:
+            v = int(t.split("=")[1]) if "=" in t else v + 1
+        return v + 1
+
+    assert enum_count("CON_DIST", "CON_F") == _lib.CON_F  # contact record width (r02 binding said 12)
+    assert enum_count("STAT_NEFC", "STAT_N") == _lib.STAT_N == len(_lib.STAT_FIELDS)
+    hdr = open(os.path.join(REPO, "include", "mmx_api.h")).read()
+    assert f"[N][{_lib.MAXCON}][{_lib.CON_F}]" in hdr and f"[N][{_lib.STAT_N}]" in hdr
+
 
 def test_obs_layout_covers_reference_keys():
     from mujoco_manip_amd.constants import OBS_SLICES

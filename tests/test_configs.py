@@ -1,8 +1,9 @@
 """BASELINE.json configs C2 and C4 on the HIP path against the oracle (VERDICT r02 "next" #1).
 
   * C2 (configs[1]): keyframe start, fixed task (obj_red, bin_red), randomize_objects=False, the
-    plan(16) expert (generate_dataset.py:140-196) with autoreset on FSM done.  Every env runs two
-    whole episodes; each is compared with the oracle's run_episode at the SURVEY §8d L2 bar.
+    plan(16) expert (generate_dataset.py:140-196): to FSM done against the oracle's run_episode at
+    the SURVEY §8d L2 bar, and under the bench's gym autoreset (episodes end at the staged
+    reward's termination) against the oracle's gym episode.
   * C4 (configs[3]): shards r = 0 and r = 7 of the real 8 x 4096 layout, each a full 4096-env
     batch seeded by global index (shard_seeds(42, r, 8, 4096)); every env runs its first episode to
     FSM done.  Properties over the whole shard (every cube placed, no error), and 16 sampled envs
@@ -88,30 +89,86 @@ def run_episodes(env, n_episodes, max_steps=600):
     return length, succ, final, task
 
 
-def test_c2_fixed_task_keyframe_expert_matches_oracle():
-    """C2 on 16 envs for two autoreset episodes each: every env and episode equals the oracle's
-    run_episode of the keyframe (obj_red, bin_red) task at the L2 bar; the 16 lockstep envs are
-    bit-identical, and the autoreset episode repeats the first exactly (reset restores the whole
-    keyframe state, warm start included)."""
+def _c2_env(n, autoreset):
     from mujoco_manip_amd.vec_env import PickPlaceVecEnv
 
+    env = PickPlaceVecEnv(n, task=("obj_red", "bin_red"), tasks="all", action_mode="abs_pos", reward_type="staged",
+                          randomize_objects=False, image_size=0, autoreset=autoreset)
+    env.reset(seed=list(range(n)))
+    return env
+
+
+def test_c2_fixed_task_keyframe_expert_matches_oracle():
+    """C2 to FSM done (run_episode semantics: terminated / truncated ignored,
+    generate_dataset.py:140-196) on 16 lockstep envs: each equals the oracle's run_episode of the
+    keyframe (obj_red, bin_red) task at the L2 bar, and the 16 envs are bit-identical."""
     N = 16
-    env = PickPlaceVecEnv(N, task=("obj_red", "bin_red"), tasks="all", action_mode="abs_pos", reward_type="staged",
-                          randomize_objects=False, image_size=0, autoreset=True)
-    env.reset(seed=list(range(N)))
-    length, succ, final, task = run_episodes(env, 2)
+    env = _c2_env(N, autoreset=False)
+    length, succ, final, task = run_episodes(env, 1)
+    length, succ, final, task = length[:, 0], succ[:, 0], final[:, 0], task[:, 0]
     assert (length >= 0).all(), length
-    assert (env.env_error.cpu().numpy() == 0).all()
-    assert (task == 0).all()
+    assert (env.env_error.cpu().numpy() == 0).all() and (task == 0).all()
     (o, b), n, rs, rcube, rplaced = oracle_episode(0, fixed_task=(0, 0), randomize=False)
     assert (o, b) == (0, 0) and rplaced
     for k in range(N):
-        for e in range(2):
-            d = float(np.linalg.norm(final[k, e] - rcube))
-            assert abs(int(length[k, e]) - n) <= 2 and d <= 0.01, (k, e, int(length[k, e]), n, d)
-            assert bool(succ[k, e]) == rs and _placed(final[k, e], 0) == rplaced, (k, e)
-    assert (length == length[0, 0]).all() and (final == final[0, 0]).all()
-    print(f"C2 episode length {int(length[0, 0])} (oracle {n}), cube error {np.linalg.norm(final[0, 0] - rcube):.2e}")
+        d = float(np.linalg.norm(final[k] - rcube))
+        assert abs(int(length[k]) - n) <= 2 and d <= 0.01, (k, int(length[k]), n, d)
+        assert bool(succ[k]) == rs and _placed(final[k], 0) == rplaced, k
+    assert (length == length[0]).all() and (final == final[0]).all()
+    print(f"C2 run_episode length {int(length[0])} (oracle {n}), cube error {np.linalg.norm(final[0] - rcube):.2e}")
+    env.close()
+
+
+def oracle_gym_episode(fixed_task=(0, 0)):
+    """One C2 episode under gym autoreset semantics (the bench's C2): plan(16) -> step until the
+    step reports terminated / truncated or the FSM is done.  Returns (env steps including the
+    ending one, ended by termination, cube placed at the end)."""
+    import oracle_py as O
+
+    e = O.OracleEnv(action_mode="abs_pos", reward_type="staged", randomize_objects=False, task=fixed_task)
+    e.reset(seed=0)
+    o, b = e.task()
+    e.fsm_init([(o, b)])
+    for t in range(500):
+        if e.fsm_plan(16) == 10:
+            return t, False, _placed(e.get_state()[0][9 + 7 * o: 12 + 7 * o], b)
+        f = e.fsm_get()
+        _, _, term, trunc, _ = e.step(np.array([*f["target"], float(f["gripper_open"])], np.float32))
+        if term or trunc:
+            return t + 1, term, _placed(e.get_state()[0][9 + 7 * o: 12 + 7 * o], b)
+    raise AssertionError("oracle C2 episode did not end")
+
+
+def test_c2_autoreset_episodes_match_oracle():
+    """C2 as the bench runs it (gym autoreset): the keyframe episode ends with the staged reward's
+    robot x obstacle termination during RETREAT (gym_env.py:428-430, reward -1), the cube already
+    in the bin; 16 envs x 3 episodes end at the oracle's ending step (+-2), are all counted as
+    placed by the sticky counter, and every episode repeats the first bit for bit."""
+    from mujoco_manip_amd import _lib
+
+    n_ref, term_ref, placed_ref = oracle_gym_episode()
+    assert term_ref and placed_ref
+    N, E = 16, 3
+    env = _c2_env(N, autoreset=True)
+    ends = [[] for _ in range(N)]
+    t0 = np.zeros(N, int)
+    for t in range(E * (n_ref + 10)):
+        _, r, term, trunc, _ = env.step(env.expert_plan(16))
+        d = (term | trunc).cpu().numpy()
+        for k in np.where(d)[0]:
+            ends[k].append((t + 1 - t0[k], bool(term[k])))
+            t0[k] = t + 1
+        if min(len(x) for x in ends) >= E:
+            break
+    epi = env._epi.cpu().numpy()
+    for k in range(N):
+        assert len(ends[k]) >= E, (k, ends[k])
+        for length, by_term in ends[k][:E]:
+            assert abs(length - n_ref) <= 2 and by_term == term_ref, (k, ends[k], n_ref)
+        assert ends[k][:E] == ends[0][:E]
+    assert (epi[:, _lib.EPI["placed"]] == epi[:, _lib.EPI["episodes"]] - 1).all()
+    assert (epi[:, _lib.EPI["error_resets"]] == 0).all()
+    print(f"C2 autoreset episode length {ends[0][0][0]} (oracle {n_ref}), ended by termination")
     env.close()
 
 

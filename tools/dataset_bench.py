@@ -1,0 +1,85 @@
+"""f2 throughput probe: generate a LeRobot dataset with camera images from batched expert episodes
+and report frames/s, PNG bytes, peak host RSS and device memory over the run.
+
+  python tools/dataset_bench.py --num-envs 8192 --episodes 8192 --image-size 128 --out gpurun_out/ds.json
+
+Diagnostic tool; writes the dataset under --root (deleted afterwards unless --keep).
+"""
+import argparse
+import json
+import os
+import resource
+import shutil
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--num-envs", type=int, default=8192)
+    ap.add_argument("--episodes", type=int, default=8192)
+    ap.add_argument("--image-size", type=int, default=128)
+    ap.add_argument("--png-workers", type=int, default=16)
+    ap.add_argument("--root", default="/tmp/mmx_ds")
+    ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "dataset_bench.json"))
+    ap.add_argument("--keep", action="store_true")
+    a = ap.parse_args()
+
+    import torch
+
+    from mujoco_manip_amd import dataset as D
+
+    free0, total = torch.cuda.mem_get_info()
+    used = []
+    t_first = [None]
+
+    def on_step(slots, ep_ids, env):
+        if t_first[0] is None:
+            t_first[0] = time.perf_counter()
+        if len(used) % 8 == 0:
+            f, _ = torch.cuda.mem_get_info()
+            used.append(total - f)
+        else:
+            used.append(used[-1])
+
+    feats = D.resolve_features(None, "staged")
+    shutil.rmtree(a.root, ignore_errors=True)
+    path = os.path.join(a.root, "u", "bench")
+    writer = D.LeRobotWriter(path, "u/bench", feats)
+    frames = [0]
+    png_bytes = [0]
+
+    def sink(ep):
+        frames[0] += ep.length
+        png_bytes[0] += sum(len(b) for k in D.IMAGE_KEYS for b in ep.frames.get(k, []))
+        writer.add_episode(ep)
+
+    t0 = time.perf_counter()
+    D.collect_episodes(a.episodes, D.TASK_SETS["all"], set(feats), randomize_objects=True, seed=0,
+                       num_envs=a.num_envs, sink=sink, png_workers=a.png_workers, image_size=a.image_size,
+                       on_step=on_step)
+    info = writer.close()
+    dt = time.perf_counter() - t0
+    rss = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0  # MB (Linux: KB)
+    size = sum(os.path.getsize(os.path.join(d, f)) for d, _, fs in os.walk(path) for f in fs)
+    rec = {"config": {"num_envs": a.num_envs, "episodes": a.episodes, "image_size": a.image_size,
+                      "png_workers": a.png_workers, "features": "all (2 cameras, numeric, actions, reward, phase)"},
+           "episodes": info["total_episodes"], "frames": info["total_frames"], "seconds": dt,
+           "frames_per_s": info["total_frames"] / dt, "images_per_s": 2 * info["total_frames"] / dt,
+           "png_mean_bytes": png_bytes[0] / max(2 * frames[0], 1), "dataset_bytes": size,
+           "peak_host_rss_mb": rss, "device_used_mb_start": (total - free0) / 2**20,
+           "device_used_mb_max": max(used) / 2**20 if used else None,
+           "device_used_mb_min_after_start": min(used) / 2**20 if used else None, "gym_steps": len(used),
+           "host_cpus": len(os.sched_getaffinity(0))}
+    os.makedirs(os.path.dirname(a.out), exist_ok=True)
+    json.dump(rec, open(a.out, "w"), indent=1)
+    print(json.dumps(rec))
+    if not a.keep:
+        shutil.rmtree(a.root, ignore_errors=True)
+
+
+if __name__ == "__main__":
+    main()

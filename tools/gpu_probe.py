@@ -125,6 +125,51 @@ def rollout_speed(N=4096, steps=100, warm=50):
     return {"env_steps_per_s": N * steps / dt, "ms_per_step": 1000 * dt / steps, "solver": env.solver_stats()}
 
 
+FSM_NAMES = ("idle", "pre_grasp", "grasp", "close_gripper", "lift", "move_to_bin", "settle_at_bin", "lower_to_bin",
+             "release", "retreat", "done")
+
+
+def fsm_profile(N=4096, steps=160, warm=0):
+    """Diagnostic (profiling) build: per FSM state of the C3 rollout, env steps, mean shader cycles
+    per env step (whole step and per phase), solver iterations / rows / contacts per substep.
+    Cycles are one wave's wall time in shader clocks (two waves share a SIMD)."""
+    import ctypes as C
+
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    L = _lib.load()
+    env = PickPlaceVecEnv(N, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
+                          autoreset=True)
+    env.reset(seed=[_lib.episode_seed(42, i) for i in range(N)])
+    if warm:
+        env.rollout_expert(warm)
+    torch.cuda.synchronize()
+    nf = L.mmx_fsm_profile_fields()
+    buf = (C.c_double * (11 * nf))()
+    L.mmx_fsm_profile.argtypes = [C.POINTER(C.c_double), C.c_int]
+    L.mmx_fsm_profile(buf, 1)
+    env.rollout_expert(steps)
+    torch.cuda.synchronize()
+    L.mmx_fsm_profile(buf, 1)
+    a = np.array(buf[:]).reshape(11, nf)
+    phases = ["ik", "kinematics", "dynamics", "collision", "constraints", "solver", "integrate", "step_end"]
+    out = {}
+    tot = a[:, nf - 1].sum()
+    for s in range(11):
+        n = a[s, nf - 1]
+        if n == 0:
+            continue
+        out[FSM_NAMES[s]] = {"env_steps": int(n), "share": n / tot, "cycles_per_env_step": a[s, len(phases)] / n,
+                             **{p + "_per_substep": a[s, j] / (16 * n) for j, p in enumerate(phases[:-1])},
+                             "step_end": a[s, len(phases) - 1] / n,
+                             "solver_iter_per_substep": a[s, len(phases) + 1] / (16 * n),
+                             "nefc_per_substep": a[s, len(phases) + 2] / (16 * n),
+                             "ncon_per_substep": a[s, len(phases) + 3] / (16 * n)}
+    allc = (a[:, len(phases)]).sum() / tot
+    out["all"] = {"env_steps": int(tot), "cycles_per_env_step": allc}
+    return out
+
+
 def nefc_dist(N=4096, steps=400):
     """Probe set 12 build: max nefc / ncon per env over a C3 rollout, substeps with nefc > 192 / 224."""
     from mujoco_manip_amd.vec_env import PickPlaceVecEnv
@@ -149,7 +194,7 @@ if __name__ == "__main__":
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     for name, fn in [("phys1", lambda: physics_parity(1)), ("phys16", lambda: physics_parity(16)),
                      ("gym", gym_parity), ("expert", expert_success), ("speed", rollout_speed),
-                     ("nefc", nefc_dist)]:
+                     ("nefc", nefc_dist), ("fsm", fsm_profile)]:
         if len(sys.argv) > 1 and name not in sys.argv[1:]:
             continue
         t = time.time()

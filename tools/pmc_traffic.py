@@ -50,7 +50,7 @@ def timed_mean(rows: list[dict], n_last: int) -> dict:
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--round", default="r02")
+    ap.add_argument("--round", default="r03")
     ap.add_argument("--workload", default="c3")
     ap.add_argument("--prof", required=True)
     ap.add_argument("--timed-steps", type=int, default=64)
@@ -78,6 +78,11 @@ def main():
     sq_names = ["SQ_WAVE_CYCLES", "SQ_WAVES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU",
                 "SQ_ACTIVE_INST_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_ANY"]
     sq = timed_mean(per_dispatch(os.path.join(a.prof, "sq"), sq_names), n_timed)
+    lanes_dir = os.path.join(a.prof, "lanes")
+    lane_util = None
+    if os.path.isdir(lanes_dir):
+        ln = timed_mean(per_dispatch(lanes_dir, ["SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU"]), n_timed)
+        lane_util = ln["SQ_THREAD_CYCLES_VALU"] / max(64.0 * ln["SQ_ACTIVE_INST_VALU"], 1.0)
     waves_per_simd = 2  # 8 one-wave workgroups per CU (LDS- and VGPR-bound), 4 SIMDs
     per_wave = sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_WAVE_CYCLES"]
     hbm = 2.0 * fetch * 1024.0 + write * 1024.0
@@ -95,6 +100,9 @@ def main():
                  "valu_insts_per_env_step": sq["SQ_INSTS_VALU"] / unit,
                  "lds_bank_conflict_per_lds_active": sq["SQ_LDS_BANK_CONFLICT"] / max(sq["SQ_ACTIVE_INST_LDS"], 1.0),
                  "wait_any_per_wave_cycle": sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"],
+                 # mean fraction of the 64 lanes active per VALU instruction (rocprofiler's
+                 # AvgNumActiveThreads / 64 for gfx950); None when the pass is missing
+                 "active_lane_fraction": lane_util,
                  "note": "SIMD VALU issue utilisation = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (per wave, same "
                          "quad-cycle units) x resident waves per SIMD; 1.0 = the VALU issues every cycle"},
         "note": "FETCH_SIZE x2 (gfx950 wide-read tally, MI355X_MICROARCH.md §HBM); dword-per-lane reads uncalibrated; "

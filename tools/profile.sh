@@ -6,7 +6,7 @@
 #   3. tools/pmc_traffic.py condenses them into profiles/<round>_* and profiles/pmc_<workload>.json
 #      (per env step, tagged with the configuration; bench.py uses it only for a matching line)
 set -e
-ROUND=${1:-r02}
+ROUND=${1:-r03}
 WL=${WORKLOAD:-c3}
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/prof_$WL
@@ -24,5 +24,8 @@ timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write
 timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAVES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU \
   SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY --output-format csv -d $OUT/sq -o run -- \
   python3 $ROOT/bench.py $ARGS > $OUT/bench_sq.log 2>&1
+# lane utilisation: thread-cycles of VALU work / (VALU instruction cycles x 64 lanes)
+timeout -s KILL 300 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU --output-format csv -d $OUT/lanes -o run -- \
+  python3 $ROOT/bench.py $ARGS > $OUT/bench_lanes.log 2>&1
 cd $ROOT
 python3 tools/pmc_traffic.py --round $ROUND --workload $WL --prof $OUT --timed-steps $STEPS
