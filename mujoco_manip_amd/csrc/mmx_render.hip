@@ -6,8 +6,8 @@
 // setup and take turns in one LDS z-buffer:
 //   1. body poses of the env (stored by the step / reset / forward kernels in S.rpose) and the
 //      camera pose (overhead: fixed; wrist: on the hand, env.py:52-65) -> LDS;
-//   2. all render vertices (tools/compile_render.py: floor grid, table / bins / cubes as boxes
-//      and prisms, each Panda body as the hull of its visual meshes) to camera space and, once
+//   2. all render vertices (tools/compile_render.py: table / bins / cubes as boxes and prisms, the
+//      Panda's visual parts as convex pieces / clustered meshes) to camera space and, once
 //      per vertex, to the screen (MuJoCo pinhole, fovy, row 0 at the top) -> LDS (screen x, y,
 //      1 / depth: the camera-space point is recovered from them where the shading needs it);
 //   3. triangles, one lane each: near cull, back-face cull, bounding box, flat face light, then
@@ -21,7 +21,9 @@
 //      (0.8) and point (0.4) lights (pick_and_place_scene.xml:6-9,33-36), the floor checker (0.1 m
 //      squares), sky gradient elsewhere; RGB u8 and the segment id written as packed dwords.
 // Not modelled (documented in DESIGN.md): shadows, specular, reflectance, bin transparency
-// (alpha 0.4 -> opaque), visual-mesh detail beyond each body's convex hull.
+// (alpha 0.4 -> opaque); the Panda's visual meshes are reduced per part (tools/compile_render.py:
+// convex pieces for the links, clustered hand / fingers; robot-mask IoU vs the full meshes in
+// tests/test_render.py).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -513,6 +515,11 @@ extern "C" hipError_t mmx_render_clock(unsigned long long* out, int reset) {
 }
 #endif
 
+static_assert(sizeof(float4) * MMR_NVERT + sizeof(float) * 19 * 12 + sizeof(uint32_t) * kZbWords +
+                  sizeof(unsigned short) * kBPW * kMaxBig + 8 * sizeof(int) + 12 * sizeof(float) +
+                  sizeof(uint32_t) * MMR_NTRI + sizeof(float) * 8 * MMR_NMAT + sizeof(unsigned short) * kBPW * MMR_NTRI +
+                  sizeof(RTri) * kBigCache <= 80 * 1024,
+              "render model too large for two workgroups per CU (LDS)");
 extern "C" size_t mmx_render_lds_bytes() {
   return sizeof(float4) * MMR_NVERT + sizeof(float) * 19 * 12 + sizeof(uint32_t) * kZbWords +
          sizeof(unsigned short) * kBPW * kMaxBig + 8 * sizeof(int) + 12 * sizeof(float) + sizeof(uint32_t) * MMR_NTRI +

@@ -12,10 +12,11 @@ Geometry (all vertices in their BODY frame, so the device only needs body poses)
     `groundplane` (rgb1/rgb2, texrepeat 5 5, texuniform: 0.1 m squares);
   * every box geom of the table, bins and cubes (:43-125) as 12 triangles, the table legs
     (cylinders) as 16-gon prisms, each with its own material rgba;
-  * each Panda body as the convex hull of all its visual meshes (panda.xml:123-246, the
-    134 k-triangle visual set is far beyond what a batched per-env rasterizer should carry),
-    reduced to <= MAX_HULL_VERTS points by farthest-point sampling, coloured with the
-    material of the body's largest visual part.
+  * the Panda's visual meshes (panda.xml:123-246, 134,888 triangles, far beyond what a batched
+    per-env rasterizer should carry) reduced per visual part, each part in its own material:
+    arm links as convex pieces (k-means clusters of ~6 cm, each the hull of <= 12 points), the
+    hand and fingers (the wrist camera's close-up) as vertex-clustered meshes (12 mm / 4 mm
+    cells, the file's winding kept).
 Segment ids (the mask-level parity channel): 0 sky, 1 floor, 2 table, 3/4/5 bins red/green/blue,
 6/7/8 cubes red/green/blue, 9 robot.
 """
@@ -33,9 +34,18 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import compile_model as CM  # noqa: E402
 
 MAX_HULL_VERTS = 96
+# robot geometry (robot-mask IoU against the full 134,888-triangle visual meshes,
+# tests/golden/robot_masks.npz, 8 states, 128 x 128): one hull per body gave 0.89 (overhead) /
+# 0.75 (wrist); convex pieces of ~7 cm per link part (<= 10 points) + clustered hand (20 mm) /
+# fingers (6 mm) give 0.92 / 0.97 with 2,033 robot triangles (was 1,956), inside the renderer's
+# LDS budget for two workgroups per CU (finer: 6 cm / 12 / 4 mm gave 0.94 / 0.98 with 2,967)
+LINK_PIECE_SIZE = 0.07
+LINK_PIECE_VERTS = 10
+HAND_CELL = 0.02
+FINGER_CELL = 0.006
 FLOOR_GRID = 8
 FLOOR_HALF = 2.0  # floor geom size 2 2 (pick_and_place_scene.xml:40)
-CYL_SIDES = 16
+CYL_SIDES = 12  # table legs (hidden under the top from both cameras)
 SEG = {"floor": 1, "table": 2, "bin_red": 3, "bin_green": 4, "bin_blue": 5, "obj_red": 6, "obj_green": 7,
        "obj_blue": 8, "robot": 9}
 ROBOT = ["link0", "link1", "link2", "link3", "link4", "link5", "link6", "link7", "hand", "left_finger",
@@ -92,6 +102,64 @@ def hull_mesh(points, k=MAX_HULL_VERTS):
     remap = {int(j): i for i, j in enumerate(h2.vertices)}
     faces = [[remap[int(j)] for j in s] for s in h2.simplices]
     return v, oriented_faces(v, type("H", (), {"simplices": np.array(faces)})), float(h.volume)
+
+
+def load_obj_tris(path):
+    """OBJ vertices and fan-triangulated faces (v / v/vt / v/vt/vn forms, 1-based or negative)."""
+    verts, faces = [], []
+    with open(path) as f:
+        for line in f:
+            if line.startswith("v "):
+                verts.append([float(x) for x in line.split()[1:4]])
+            elif line.startswith("f "):
+                idx = []
+                for tok in line.split()[1:]:
+                    i = int(tok.split("/")[0])
+                    idx.append(i - 1 if i > 0 else len(verts) + i)
+                for k in range(1, len(idx) - 1):
+                    faces.append([idx[0], idx[k], idx[k + 1]])
+    return np.asarray(verts, float), np.asarray(faces, np.int64)
+
+
+def cluster_mesh(v, t, cell):
+    """Vertex-clustering decimation: vertices merged per `cell`-sized grid cell (cell mean),
+    triangles that collapse dropped; the surviving triangles keep the file's winding."""
+    q = np.floor(v / cell).astype(np.int64)
+    keys, inv = np.unique(q, axis=0, return_inverse=True)
+    inv = inv.ravel()
+    rep = np.zeros((len(keys), 3))
+    cnt = np.zeros(len(keys))
+    np.add.at(rep, inv, v)
+    np.add.at(cnt, inv, 1)
+    rep /= cnt[:, None]
+    tt = inv[t]
+    tt = tt[(tt[:, 0] != tt[:, 1]) & (tt[:, 1] != tt[:, 2]) & (tt[:, 0] != tt[:, 2])]
+    tt = np.unique(tt, axis=0)
+    used = np.unique(tt)
+    remap = np.full(len(rep), -1)
+    remap[used] = np.arange(len(used))
+    return rep[used], remap[tt]
+
+
+def convex_pieces(v, size, k):
+    """A part's vertices split into ceil(extent / size) spatial clusters (k-means, fixed seed), each
+    drawn as its convex hull (<= k points): concave links keep their silhouette far better than
+    one hull per body at a fraction of the visual mesh's triangles."""
+    from scipy.cluster.vq import kmeans2
+
+    m = max(1, int(np.ceil(np.ptp(v, 0).max() / size)))
+    groups = [v]
+    if m > 1 and len(v) >= 8 * m:
+        _, lab = kmeans2(v, m, minit="++", seed=0)
+        groups = [v[lab == i] for i in range(m) if (lab == i).sum() >= 4]
+    out = []
+    for g in groups:
+        try:
+            hv, hf, _ = hull_mesh(g, k)
+        except Exception:  # a degenerate (flat) cluster: covered by its neighbours
+            continue
+        out.append((hv, hf))
+    return out
 
 
 def geom_to_body(v, pos, quat):
@@ -162,18 +230,18 @@ def build():
     def walk(be):
         name = be.get("name")
         if name in ROBOT:
-            pts, best, best_vol = [], None, -1.0
             for ge in be.findall("geom"):
                 if ge.get("class") != "visual":
                     continue
                 assert ge.get("pos") is None and ge.get("quat") is None
-                p = CM.load_obj(meshfile[ge.get("mesh")])
-                vol = ConvexHull(p).volume
-                if vol > best_vol:
-                    best, best_vol = ge.get("material"), vol
-                pts.append(p)
-            v, f, _ = hull_mesh(np.concatenate(pts))
-            parts.append((bnames.index(name), v, f, material(best, SEG["robot"])))
+                v, t = load_obj_tris(meshfile[ge.get("mesh")])
+                mat = material(ge.get("material"), SEG["robot"])
+                if name.startswith("link"):  # arm links: convex pieces of each visual part
+                    for pv, pf in convex_pieces(v, LINK_PIECE_SIZE, LINK_PIECE_VERTS):
+                        parts.append((bnames.index(name), pv, pf, mat))
+                else:  # hand and fingers (the wrist camera's close-up): clustered meshes
+                    cv, cf = cluster_mesh(v, t, HAND_CELL if name == "hand" else FINGER_CELL)
+                    parts.append((bnames.index(name), cv, cf.tolist(), mat))
         for c in be.findall("body"):
             walk(c)
 
@@ -197,16 +265,23 @@ def build():
 def emit(rm, path):
     L = ["/* generated by tools/compile_render.py -- do not edit */\n#ifndef MMX_RENDER_GEN_H\n"
          "#define MMX_RENDER_GEN_H\n\n#ifndef MMR_QUAL\n#define MMR_QUAL static const\n#endif\n\n"]
-    nv, nt, nm = len(rm["verts"]), len(rm["tris"]), len(rm["materials"])
+    # the floor plane (body 0, material 0, checker) is not in the device tables: the renderer shades
+    # it analytically behind everything (the CPU ray caster keeps its grid triangles)
+    vkeep = np.array(rm["vert_body"]) != 0
+    vmap = np.cumsum(vkeep) - 1
+    tris = np.array(rm["tris"])
+    tkeep = vkeep[tris].all(1)
+    verts = [v for v, k in zip(rm["verts"], vkeep) if k]
+    vbody = [b for b, k in zip(rm["vert_body"], vkeep) if k]
+    dtris = vmap[tris[tkeep]].tolist()
+    dmat = [m for m, k in zip(rm["tri_mat"], tkeep) if k]
+    nv, nt, nm = len(verts), len(dtris), len(rm["materials"])
     L.append(f"#define MMR_NVERT {nv}\n#define MMR_NTRI {nt}\n#define MMR_NMAT {nm}\n")
-    # the floor plane: its triangles come first (material 0, checker); the renderer shades it
-    # analytically behind everything instead of rasterising it
-    L.append(f"#define MMR_FLOOR_TRIS {2 * FLOOR_GRID * FLOOR_GRID}\n#define MMR_FLOOR_HALF {FLOOR_HALF!r}f\n"
-             "#define MMR_FLOOR_MAT 0\n\n")
-    L.append(CM.c_array("MMR_vert", "float", rm["verts"], "{:.9g}"))
-    L.append(CM.c_array("MMR_vert_body", "unsigned char", rm["vert_body"], "{}"))
-    L.append(CM.c_array("MMR_tri", "unsigned short", rm["tris"], "{}"))
-    L.append(CM.c_array("MMR_tri_mat", "unsigned char", rm["tri_mat"], "{}"))
+    L.append(f"#define MMR_FLOOR_TRIS 0\n#define MMR_FLOOR_HALF {FLOOR_HALF!r}f\n#define MMR_FLOOR_MAT 0\n\n")
+    L.append(CM.c_array("MMR_vert", "float", verts, "{:.9g}"))
+    L.append(CM.c_array("MMR_vert_body", "unsigned char", vbody, "{}"))
+    L.append(CM.c_array("MMR_tri", "unsigned short", dtris, "{}"))
+    L.append(CM.c_array("MMR_tri_mat", "unsigned char", dmat, "{}"))
     L.append(CM.c_array("MMR_mat_rgb", "float", [m["rgb"] + m["rgb2"] for m in rm["materials"]], "{:.9g}"))
     L.append(CM.c_array("MMR_mat_checker", "float", [m["checker"] for m in rm["materials"]], "{:.9g}"))
     L.append(CM.c_array("MMR_mat_seg", "unsigned char", [m["seg"] for m in rm["materials"]], "{}"))
