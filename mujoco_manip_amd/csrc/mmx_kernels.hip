@@ -1700,20 +1700,19 @@ DEV float chol_block_free(const float* hrow, float v) {
 }
 // arm-cube coupling (a grasp), no cube-cube coupling: arrow order, the three cube blocks first (6
 // lockstep steps) with the arm lanes forming their coupling columns L[arm][cube] and the arm
-// block's Schur complement as each cube pivot passes, then the arm block (9 steps in row 0); the
-// transposed solve in reverse order.  Cross-row values: a cube pivot's 1 / d, its column below the
-// pivot and its y reach the arm lanes by v_readlane; the Schur update's arm values stay in DPP row 0
-// (row_newbcast, no SGPR round trip), and the arm lanes' column L[arm][cube pivot] goes to LDS
-// (E.con, free during the solve) for the transposed solve of the cube rows.
-DEV float chol_block_arm(EnvSh& E, const float* hrow, float v, int cpla) {
+// block's Schur complement as each cube pivot passes (v_readlane of the cube rows' values), then
+// the arm block (9 steps in row 0); the transposed solve in reverse order
+DEV float chol_block_arm(const float* hrow, float v, int cpla) {
   const int L = LANE, r = L >> 4, kk = L & 15;
   const bool cube = r != 0;
   const bool valid = cube ? kk < 6 : kk < 9;
-  float* Lx = lrow_of(E);  // [cube b 1..3][pivot k][arm i]: L[arm i][cube pivot]
-  float hb[9], c[9], dinv[9], hx[18];
+  float hb[9], c[9], cx[9], dinv[9], hx[18];
   block_row(hrow, hb);
 #pragma unroll
-  for (int m = 0; m < 9; m++) c[m] = 0.f;
+  for (int m = 0; m < 9; m++) {
+    c[m] = 0.f;
+    cx[m] = 0.f;
+  }
 #pragma unroll
   for (int m = 0; m < 18; m++) hx[m] = hrow[9 + m];  // arm lanes: the coupling columns
   float y = valid ? v : 0.f;
@@ -1741,8 +1740,11 @@ DEV float chol_block_arm(EnvSh& E, const float* hrow, float v, int cpla) {
 #pragma unroll
       for (int m = k + 1; m < 6; m++) hx[6 * (b - 1) + m] = fmaf(-readlane_f(l, 16 * b + m), la, hx[6 * (b - 1) + m]);
 #pragma unroll
-      for (int i = 0; i < 9; i++) hb[i] = fmaf(-row_bcast(la, i), la, hb[i]);  // Schur complement (la = 0 off row 0)
-      if (L < 9) Lx[(6 * b + k) * 9 + L] = la;
+      for (int i = 0; i < 9; i++) {  // Schur complement of the arm block
+        const float li = readlane_f(la, i);
+        hb[i] = fmaf(-li, la, hb[i]);
+        cx[i] = L == 16 * b + k ? li : cx[i];
+      }
       y = fmaf(-la, readlane_f(y, 16 * b + k), y);  // the cube pivot's y is final
     }
   }
@@ -1769,20 +1771,13 @@ DEV float chol_block_arm(EnvSh& E, const float* hrow, float v, int cpla) {
       y = kk == k ? zk : (kk < k ? fmaf(-c[k], zk, y) : y);
     }
   }
-  SYNC();  // Lx written (arm lanes) before the cube lanes read it
-  const bool coupled = cube && valid && ((cpla >> r) & 1);
-  const float* lx = Lx + (6 * r + kk) * 9;
 #pragma unroll
-  for (int i = 0; i < 9; i++) {  // cube rows: y -= L[arm][cube row]' z_arm
-    const float zi = readlane_f(y, i);
-    y = coupled ? fmaf(-lx[i], zi, y) : y;
-  }
+  for (int i = 0; i < 9; i++) y = fmaf(-cx[i], readlane_f(y, i), y);  // (cx = 0 off the coupled cubes)
 #pragma unroll
   for (int k = 5; k >= 0; k--) {
     const float zk = row_bcast(y, k) * dinv[k];
     y = cube ? (kk == k ? zk : (kk < k ? fmaf(-c[k], zk, y) : y)) : y;
   }
-  SYNC();  // (E.con is scratch of the next phase)
   return valid ? y : 0.f;
 }
 
@@ -1867,7 +1862,7 @@ DEV float chol_solve(EnvSh& E, const float* hrow, float v, int cpl) {
   CLK_DECL;
   const bool cube_cube = !MMX_CHOL_BLOCK || (cpl & 0x6AC0) != 0;  // bits 4 x + y with x, y in 1..3, x != y
   const float y = cube_cube ? chol_solve_arrow(E, hrow, v, cpl)
-                            : ((cpl & 0xE) ? chol_block_arm(E, hrow, v, cpl & 0xE) : chol_block_free(hrow, v));
+                            : ((cpl & 0xE) ? chol_block_arm(hrow, v, cpl & 0xE) : chol_block_free(hrow, v));
   // probe set 9: cycles of the uncoupled / arm-coupled / cube-cube solves; AUX3 counts the
   // arm-coupled solves + 1000 x the cube-cube ones
   PROBE(9, stats, cube_cube ? STAT_T_AUX1 : ((cpl & 0xE) ? STAT_T_AUX2 : STAT_T_AUX0));
@@ -2999,8 +2994,8 @@ __device__ __attribute__((noinline)) void step_finish(const MMXState& S, int i) 
 // in), the sums over env steps of the shader cycles of each phase (STAT_T_IK .. STAT_T_END), of
 // the whole step, of the solver iterations / MuJoCo rows / contacts, and the env-step count
 // (tools/gpu_probe.py fsm_profile).  Lane 0 of each env adds with global atomics.
-enum { FSMP_PHASES = STAT_T_END - STAT_T_IK + 1, FSMP_STEP = FSMP_PHASES, FSMP_ITER, FSMP_NEFC, FSMP_NCON, FSMP_COUNT,
-       FSMP_N };
+enum { FSMP_PHASES = STAT_T_AUX3 - STAT_T_IK + 1, FSMP_STEP = FSMP_PHASES, FSMP_ITER, FSMP_NEFC, FSMP_NCON,
+       FSMP_COUNT, FSMP_N };
 __device__ double g_fsm_prof[11 * FSMP_N];
 extern "C" hipError_t mmx_fsm_profile(double* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fsm_prof), sizeof(g_fsm_prof));

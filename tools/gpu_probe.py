@@ -152,20 +152,22 @@ def fsm_profile(N=4096, steps=160, warm=0):
     torch.cuda.synchronize()
     L.mmx_fsm_profile(buf, 1)
     a = np.array(buf[:]).reshape(11, nf)
-    phases = ["ik", "kinematics", "dynamics", "collision", "constraints", "solver", "integrate", "step_end"]
-    out = {}
+    phases = ["ik", "kinematics", "dynamics", "collision", "constraints", "solver", "integrate", "step_end", "aux0",
+              "aux1", "aux2", "aux3"]
+    P = len(phases)
+    out = {"probe_set": os.environ.get("MMX_LIB_PATH", "libmmx_prof.so")}
     tot = a[:, nf - 1].sum()
     for s in range(11):
         n = a[s, nf - 1]
         if n == 0:
             continue
-        out[FSM_NAMES[s]] = {"env_steps": int(n), "share": n / tot, "cycles_per_env_step": a[s, len(phases)] / n,
-                             **{p + "_per_substep": a[s, j] / (16 * n) for j, p in enumerate(phases[:-1])},
-                             "step_end": a[s, len(phases) - 1] / n,
-                             "solver_iter_per_substep": a[s, len(phases) + 1] / (16 * n),
-                             "nefc_per_substep": a[s, len(phases) + 2] / (16 * n),
-                             "ncon_per_substep": a[s, len(phases) + 3] / (16 * n)}
-    allc = (a[:, len(phases)]).sum() / tot
+        out[FSM_NAMES[s]] = {"env_steps": int(n), "share": n / tot, "cycles_per_env_step": a[s, P] / n,
+                             **{p + "_per_substep": a[s, j] / (16 * n) for j, p in enumerate(phases) if p != "step_end"},
+                             "step_end": a[s, 7] / n,
+                             "solver_iter_per_substep": a[s, P + 1] / (16 * n),
+                             "nefc_per_substep": a[s, P + 2] / (16 * n),
+                             "ncon_per_substep": a[s, P + 3] / (16 * n)}
+    allc = (a[:, P]).sum() / tot
     out["all"] = {"env_steps": int(tot), "cycles_per_env_step": allc}
     return out
 
