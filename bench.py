@@ -318,6 +318,7 @@ def main():
         env.clear_stats()
         epi0 = env._epi[:, cnt].sum(0).double()
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        env.sim.kernel_timing(True)  # HIP event pair around every launch, on its own stream
         if dist:
             dist.barrier()
         torch.cuda.synchronize()
@@ -329,7 +330,12 @@ def main():
         if dist:
             dist.barrier()
         elapsed = time.perf_counter() - t0
-        kern_ms = ev0.elapsed_time(ev1) / launches  # per launch
+        env.sim.kernel_timing(False)
+        kt = env.sim.kernel_times()
+        span_ms = ev0.elapsed_time(ev1) / launches  # the rollout's span per launch round
+        # the step kernel's average launch duration (each launch: envs_per_launch envs x spl steps)
+        kern_ms = kt["step_ms"] / max(kt["step_launches"], 1)
+        render_ms = kt["render_ms"] / kt["render_launches"] if kt["render_launches"] else None
         eps = (env._epi[:, cnt].sum(0).double() - epi0).tolist()
         errs_now = float((env.env_error != 0).sum().item())
         solver = env.solver_stats()
@@ -346,7 +352,9 @@ def main():
             rank_kern_ms = rk.tolist()
         else:
             rank_kern_ms = [kern_ms]
-        windows.append({"elapsed": elapsed, "kern_ms": kern_ms, "rank_kernel_ms": rank_kern_ms, "solver": solver,
+        windows.append({"elapsed": elapsed, "kern_ms": kern_ms, "span_ms": span_ms, "render_ms": render_ms,
+                        "launch_counts": [kt["step_launches"], kt["render_launches"]],
+                        "rank_kernel_ms": rank_kern_ms, "solver": solver,
                         "episodes": {"completed": int(eps[0]), "successes": int(eps[1]), "placed": int(eps[2]),
                                      "error_resets": int(eps[3]), "envs_with_error_now": int(errs_now)}})
     values = [args.steps * N * world / w["elapsed"] for w in windows]
@@ -365,6 +373,22 @@ def main():
     min_bytes = min_hbm_bytes_per_env_step() * envs_per_launch * steps_per_launch
     ep = med["episodes"]
 
+    render = None
+    if med["render_ms"]:
+        # mmx_render_kernel: per env of a launch, 2 cameras x S^2 x (RGB + segment id) bytes written
+        # and the 14 body poses read; one launch per rollout lane and env step, lanes side by side
+        S = args.image_size
+        rbytes = envs_per_launch * (2 * S * S * 4 + 14 * 12 * 4)
+        r_achieved = lanes * rbytes / (med["render_ms"] * 1e-3) / 1e9
+        rpmc = pmc_evidence("render", N, 1, lanes)
+        render = {"kernel": "mmx_render_kernel", "kernel_ms": med["render_ms"], "concurrent_launches": lanes,
+                  "envs_per_launch": envs_per_launch, "image_size": S, "bytes_per_launch": rbytes,
+                  "bound": "valu", "hbm_achieved_GBs": r_achieved, "hbm_frac": r_achieved / HBM_PEAK_GBS,
+                  "share_of_kernel_time": med["render_ms"] / (med["render_ms"] + kern_ms),
+                  "pixels_per_s": lanes * envs_per_launch * 2 * S * S / (med["render_ms"] * 1e-3),
+                  "valu": None if rpmc is None else rpmc.get("valu"),
+                  "note": "HBM is not the render kernel's roof (it writes 4 B per pixel); VALU issue is "
+                          "(valu: SQ counters of tools/render_pmc.sh for this configuration)"}
     if rank == 0:
         pmc = pmc_evidence(args.workload, N, spl, lanes)
         traffic = None if pmc is None else pmc["hbm_bytes_per_env_step"] * envs_per_launch * steps_per_launch
@@ -393,7 +417,7 @@ def main():
                                  "its start pose, which the expert's retreat target does not reach"},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "mmx_env_step_kernel", "kernel_ms": kern_ms,
+                         "kernel": "mmx_env_step_kernel", "kernel_ms": kern_ms, "span_ms_per_launch_round": med["span_ms"],
                          "rank_kernel_ms": med["rank_kernel_ms"], "concurrent_launches": lanes,
                          "envs_per_launch": envs_per_launch, "env_steps_per_launch": steps_per_launch,
                          "algorithmic_bytes_per_env_step": bpe, "algorithmic_bytes_per_launch": bytes_per_launch,
@@ -402,6 +426,7 @@ def main():
                          "min_hbm_bytes_per_launch": min_bytes,
                          "min_hbm_GBs": lanes * min_bytes / (kern_ms * 1e-3) / 1e9},
             "valu": None if pmc is None else pmc.get("valu"),
+            "render": render,
             "cpu_baseline": cpu,
             "solver": solver,
         }

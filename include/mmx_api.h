@@ -54,7 +54,8 @@ typedef struct {
   int8_t task_bin[9];
   int32_t fixed_task_obj;       /* -1: sample from the pool (gym_env.py:511-517) */
   int32_t fixed_task_bin;
-  int32_t image_size;           /* camera image side (multiple of 16, <= 1024); 0 = no rendering */
+  int32_t image_size;           /* camera image side (any, <= 1024; sides that are multiples of 16 write
+                                   whole dwords); 0 = no rendering */
   int32_t autoreset;            /* same-step autoreset on terminated/truncated/FSM done */
   int32_t solver_iterations;    /* Newton iteration cap (default 30) */
   float solver_tolerance;       /* relative gradient-norm tolerance (default 1e-6) */
@@ -137,6 +138,15 @@ int mmx_rollout_lanes(const mmx_sim* sim);
  * envs' steps back to back inside each workgroup; the trajectories are bit-identical to one
  * launch per step.  0 for a null sim. */
 int mmx_rollout_steps_per_launch(const mmx_sim* sim);
+
+/* Per-launch kernel timing of mmx_rollout_expert (measurement): with enable = 1 every step-kernel
+ * and render-kernel launch is bracketed by a HIP event pair on the stream it runs on (a new
+ * collection starts); enable = 0 stops collecting.  mmx_kernel_times waits for the recorded events
+ * and returns the summed launch durations (ms) and launch counts of each kernel; NULL skips a
+ * field.  Not part of the reference interface. */
+int mmx_kernel_timing(mmx_sim* sim, int32_t enable);
+int mmx_kernel_times(mmx_sim* sim, float* step_ms, int32_t* step_launches, float* render_ms,
+                     int32_t* render_launches);
 
 /* Physics-level entry points (parity harnesses): n x mujoco.mj_step with the current ctrl
  * (env.py:119-121), optionally preceded by IKController.compute toward the decoded target

@@ -55,7 +55,8 @@ class MMXBuffers(C.Structure):
 EXPORTED = ("mmx_config_default", "mmx_create", "mmx_destroy", "mmx_last_error", "mmx_reset", "mmx_step",
             "mmx_expert_plan", "mmx_rollout_expert", "mmx_physics_step", "mmx_forward", "mmx_get_buffers",
             "mmx_synchronize", "mmx_get_state", "mmx_set_state", "mmx_episode_seed", "mmx_rollout_lanes",
-            "mmx_rollout_steps_per_launch", "mmx_expert_physics", "mmx_eval_reward")
+            "mmx_rollout_steps_per_launch", "mmx_expert_physics", "mmx_eval_reward", "mmx_kernel_timing",
+            "mmx_kernel_times")
 
 _lib = None
 
@@ -91,6 +92,8 @@ def load(build_if_missing: bool = True):
     L.mmx_forward.argtypes = [vp]
     L.mmx_expert_physics.argtypes = [vp, C.c_int32]
     L.mmx_eval_reward.argtypes = [vp, vp, vp, vp, vp, C.c_int32]
+    L.mmx_kernel_timing.argtypes = [vp, C.c_int32]
+    L.mmx_kernel_times.argtypes = [vp, fp, i32p, fp, i32p]
     L.mmx_get_buffers.argtypes = [vp, C.POINTER(MMXBuffers)]
     L.mmx_synchronize.argtypes = [vp]
     L.mmx_get_state.argtypes = [vp, fp, fp, fp, fp]
@@ -99,7 +102,7 @@ def load(build_if_missing: bool = True):
     L.mmx_episode_seed.argtypes = [C.c_uint64, C.c_int32]
     for name in ("mmx_create", "mmx_reset", "mmx_step", "mmx_expert_plan", "mmx_rollout_expert", "mmx_physics_step",
                  "mmx_forward", "mmx_get_buffers", "mmx_synchronize", "mmx_get_state", "mmx_set_state",
-                 "mmx_expert_physics", "mmx_eval_reward"):
+                 "mmx_expert_physics", "mmx_eval_reward", "mmx_kernel_timing", "mmx_kernel_times"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L
@@ -218,6 +221,17 @@ class Sim:
 
     def rollout_expert(self, n_env_steps: int):
         self._check(self.L.mmx_rollout_expert(self.ptr, n_env_steps), "mmx_rollout_expert")
+
+    def kernel_timing(self, enable: bool):
+        """Start (True: a new collection) / stop bracketing every rollout launch with HIP events."""
+        self._check(self.L.mmx_kernel_timing(self.ptr, int(bool(enable))), "mmx_kernel_timing")
+
+    def kernel_times(self) -> dict:
+        """Summed launch durations (ms) and launch counts since kernel_timing(True); waits for them."""
+        sm, rm, sn, rn = C.c_float(), C.c_float(), C.c_int32(), C.c_int32()
+        self._check(self.L.mmx_kernel_times(self.ptr, C.byref(sm), C.byref(sn), C.byref(rm), C.byref(rn)),
+                    "mmx_kernel_times")
+        return {"step_ms": sm.value, "step_launches": sn.value, "render_ms": rm.value, "render_launches": rn.value}
 
     @property
     def rollout_lanes(self) -> int:

@@ -45,6 +45,12 @@ struct mmx_sim {
   int fuse = 16;
   hipStream_t lane[kMaxLanes] = {};
   hipEvent_t ev_fork = nullptr, ev_join[kMaxLanes] = {};
+  // per-launch kernel timing (mmx_kernel_timing): an event pair around every step / render launch
+  // on the stream it runs on; pairs come from a pool reused after each read-out
+  bool timing = false;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  std::vector<std::pair<size_t, size_t>> t_step, t_render;
 };
 
 namespace {
@@ -154,6 +160,32 @@ T* dalloc(mmx_sim* sim, size_t count) {
 
 }  // namespace
 
+namespace {
+// an event of the timing pool recorded on `st` (its index), or SIZE_MAX when the pool cannot grow
+size_t timing_mark(mmx_sim* sim, hipStream_t st) {
+  if (sim->ev_used == sim->ev_pool.size()) {
+    hipEvent_t ev;
+    if (hipEventCreate(&ev) != hipSuccess) return SIZE_MAX;
+    sim->ev_pool.push_back(ev);
+  }
+  const size_t k = sim->ev_used;
+  if (hipEventRecord(sim->ev_pool[k], st) != hipSuccess) return SIZE_MAX;
+  sim->ev_used++;
+  return k;
+}
+// launch `f` on `st`, bracketed by a timing event pair when timing is on
+template <class F>
+hipError_t timed(mmx_sim* sim, hipStream_t st, std::vector<std::pair<size_t, size_t>>& pairs, F f) {
+  const size_t a = sim->timing ? timing_mark(sim, st) : SIZE_MAX;
+  const hipError_t e = f();
+  if (a != SIZE_MAX && e == hipSuccess) {
+    const size_t b = timing_mark(sim, st);
+    if (b != SIZE_MAX) pairs.emplace_back(a, b);
+  }
+  return e;
+}
+}  // namespace
+
 extern "C" {
 
 void mmx_config_default(mmx_config* c) {
@@ -181,7 +213,7 @@ void mmx_config_default(mmx_config* c) {
 int mmx_create(const mmx_config* cfg, mmx_sim** out) {
   if (!cfg || !out) return MMX_EINVAL;
   *out = nullptr;
-  if (cfg->image_size < 0 || cfg->image_size % 16 != 0 || cfg->image_size > 1024) return MMX_EINVAL;
+  if (cfg->image_size < 0 || cfg->image_size > 1024) return MMX_EINVAL;
   if (cfg->num_envs <= 0 || cfg->action_mode < 0 || cfg->action_mode > 4 || cfg->reward_type < 0 ||
       cfg->reward_type > 2 || cfg->n_tasks < 1 || cfg->n_tasks > 9)
     return MMX_EINVAL;
@@ -299,6 +331,7 @@ void mmx_destroy(mmx_sim* sim) {
     (void)hipStreamDestroy(sim->lane[l]);
   }
   if (sim->ev_fork) (void)hipEventDestroy(sim->ev_fork);
+  for (hipEvent_t ev : sim->ev_pool) (void)hipEventDestroy(ev);
   delete sim;
 }
 
@@ -370,6 +403,40 @@ int mmx_expert_plan(mmx_sim* sim, int32_t n_steps, float* action_dev_out) {
   return hip_check(sim, mmx_launch_expert(&sim->S, n_steps, action_dev_out, sim->stream), "mmx_expert_plan");
 }
 
+
+int mmx_kernel_timing(mmx_sim* sim, int32_t enable) {
+  if (!sim) return MMX_EINVAL;
+  DeviceGuard guard(sim);
+  if (enable) {  // start a new collection (the pool's events are reused)
+    sim->ev_used = 0;
+    sim->t_step.clear();
+    sim->t_render.clear();
+  }
+  sim->timing = enable != 0;
+  return MMX_OK;
+}
+
+int mmx_kernel_times(mmx_sim* sim, float* step_ms, int32_t* step_launches, float* render_ms, int32_t* render_launches) {
+  if (!sim) return MMX_EINVAL;
+  DeviceGuard guard(sim);
+  auto sum = [&](const std::vector<std::pair<size_t, size_t>>& v, float* ms, int32_t* n) -> hipError_t {
+    double tot = 0.0;
+    for (const auto& pr : v) {
+      hipError_t e = hipEventSynchronize(sim->ev_pool[pr.second]);
+      float t = 0.f;
+      if (e == hipSuccess) e = hipEventElapsedTime(&t, sim->ev_pool[pr.first], sim->ev_pool[pr.second]);
+      if (e != hipSuccess) return e;
+      tot += t;
+    }
+    if (ms) *ms = (float)tot;
+    if (n) *n = (int32_t)v.size();
+    return hipSuccess;
+  };
+  hipError_t e = sum(sim->t_step, step_ms, step_launches);
+  if (e == hipSuccess) e = sum(sim->t_render, render_ms, render_launches);
+  return hip_check(sim, e, "mmx_kernel_times");
+}
+
 int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
   if (!sim || sim->S.action_mode != MMX_ACTION_ABS_POS) return MMX_EINVAL;
   DeviceGuard guard(sim);
@@ -388,8 +455,10 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
     for (int l = 0; l < L && e == hipSuccess; l++) {
       const int b0 = (int)((long)N * l / L), b1 = (int)((long)N * (l + 1) / L);
       hipStream_t st = l ? sim->lane[l] : sim->stream;
-      e = mmx_launch_step(&sim->S, sim->expert_action, 4, 1, b0, b1 - b0, ns, st);
-      if (e == hipSuccess) e = mmx_launch_render(&sim->S, b0, b1 - b0, st);
+      e = timed(sim, st, sim->t_step,
+                [&] { return mmx_launch_step(&sim->S, sim->expert_action, 4, 1, b0, b1 - b0, ns, st); });
+      if (e == hipSuccess && sim->S.image_size > 0)
+        e = timed(sim, st, sim->t_render, [&] { return mmx_launch_render(&sim->S, b0, b1 - b0, st); });
     }
   }
   if (L > 1)  // join: the caller's stream sees the whole rollout, as with a single launch chain

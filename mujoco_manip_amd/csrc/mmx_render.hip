@@ -189,7 +189,7 @@ DEV uint32_t rend_cover(const RTri& T, int t, int px, int py, float q0) {
 // its ray meets the floor, the sky gradient elsewhere; RGB u8 (3 dwords) and segment ids (1 dword)
 DEV void shade4(const uint32_t* keys, int px0, int py, int Sz, float half, float f, const M3& cR, const V3& cx,
                 const V3& l_top, const V3& lp_cam, const uint32_t* tinfo, const float* mrgb, uint32_t* rgb_out,
-                uint32_t* seg_out) {
+                uint32_t* seg_out, int nvalid) {
   {
     uint32_t rgbw[3] = {0u, 0u, 0u}, segw = 0u;
     for (int u = 0; u < 4; u++) {
@@ -231,8 +231,17 @@ DEV void shade4(const uint32_t* keys, int px0, int py, int Sz, float half, float
       }
       segw |= (uint32_t)sid << (8 * u);
     }
-    rgb_out[0] = rgbw[0]; rgb_out[1] = rgbw[1]; rgb_out[2] = rgbw[2];
-    seg_out[0] = segw;
+    if (nvalid == 4) {  // the image side is a multiple of 16: 4 whole pixels, dword-aligned
+      rgb_out[0] = rgbw[0]; rgb_out[1] = rgbw[1]; rgb_out[2] = rgbw[2];
+      seg_out[0] = segw;
+    } else {  // other sides: byte stores of the pixels inside the image
+      unsigned char* rb = reinterpret_cast<unsigned char*>(rgb_out);
+      unsigned char* sb = reinterpret_cast<unsigned char*>(seg_out);
+      for (int u = 0; u < nvalid; u++) {
+        for (int k = 0; k < 3; k++) rb[3 * u + k] = (unsigned char)(rgbw[(3 * u + k) >> 2] >> (8 * ((3 * u + k) & 3)));
+        sb[u] = (unsigned char)(segw >> (8 * u));
+      }
+    }
   }
 }
 
@@ -251,9 +260,11 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
   RTri* bigs = reinterpret_cast<RTri*>(smallq + kBPW * MMR_NTRI);                 // [kBigCache] setups
 
   const int tid = threadIdx.x;
-  const int Sz = S.image_size;
-  const int rows = rend_band_rows(Sz);
-  const int Zs = Sz + MMR_ZPAD;  // z-buffer row stride
+  const int Sz = S.image_size;        // image side (projection, output)
+  const int Sg = (Sz + 15) & ~15;     // raster grid side: bands, 16 x 16 tiles, z-buffer rows
+  const bool whole = Sz == Sg;        // every tile lies inside the image
+  const int rows = rend_band_rows(Sg);
+  const int Zs = Sg + MMR_ZPAD;  // z-buffer row stride
   const int rowA = blockIdx.x * kBPW * rows, rowB = min(Sz, rowA + kBPW * rows);  // the workgroup's bands
   const int ci = blockIdx.y;  // 0 overhead, 1 wrist
   const int i = env_base + blockIdx.z;
@@ -353,7 +364,7 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
       else smallq[kb * MMR_NTRI + atomicAdd(nbig + 2 * kb + 1, 1)] = (unsigned short)t;
     }
   }
-  const int tcols = Sz >> 4;
+  const int tcols = Sg >> 4;
   const int lane = tid & 63, lx = 4 * (lane & 3), ly = lane >> 2;
   unsigned char* img = S.images + ((size_t)i * 2 + ci) * Sz * Sz * 3;
   unsigned char* seg = S.seg + ((size_t)i * 2 + ci) * Sz * Sz;
@@ -468,7 +479,7 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
       tx[j] = (tile - trow * tcols) * 16;
       ty[j] = row0 + trow * 16;
       const int py = ty[j] + ly;
-      for (int u = 0; u < 4; u++) best[j][u] = py < row1 ? zb[(py - row0) * Zs + tx[j] + lx + u] : 0u;
+      for (int u = 0; u < 4; u++) best[j][u] = py < row1 ? zb[(py - row0) * Zs + tx[j] + lx + u] : 0u;  // (x < Sg)
     }
     for (int q = 0; q < nb; q++) {
       const int t = __builtin_amdgcn_readfirstlane((int)bigq[kb * kMaxBig + q]);
@@ -495,9 +506,11 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
     for (int j = 0; j < kTPW; j++) {
       const int py = ty[j] + ly;
       if (tb + j >= ntiles || py >= row1) continue;
+      const int nvalid = whole ? 4 : min(4, Sz - (tx[j] + lx));
+      if (nvalid <= 0) continue;
       const size_t p0 = (size_t)py * Sz + tx[j] + lx;  // image pixel of the lane's first pixel
       shade4(best[j], tx[j] + lx, py, Sz, half, f, cR, cx, l_top, lp_cam, tinfo, mrgb,
-             reinterpret_cast<uint32_t*>(img + 3 * p0), reinterpret_cast<uint32_t*>(seg + p0));
+             reinterpret_cast<uint32_t*>(img + 3 * p0), reinterpret_cast<uint32_t*>(seg + p0), nvalid);
     }
   }
   }  // bands
@@ -528,7 +541,7 @@ extern "C" size_t mmx_render_lds_bytes() {
 
 extern "C" hipError_t mmx_launch_render(const MMXState* S, int base, int count, hipStream_t st) {
   if (count <= 0 || S->image_size <= 0) return hipSuccess;
-  const int rows = rend_band_rows(S->image_size);
+  const int rows = rend_band_rows((S->image_size + 15) & ~15);
   const int bands = (S->image_size + rows - 1) / rows;
   hipLaunchKernelGGL(mmx_render_kernel, dim3((bands + kBPW - 1) / kBPW, 2, count), dim3(RWG), mmx_render_lds_bytes(), st, *S, base);
   return hipGetLastError();

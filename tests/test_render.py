@@ -78,18 +78,22 @@ def _gpu_states(n=3, steps=40, size=64):
 
 
 @pytest.mark.gpu
-def test_render_masks_match_raycast():
+@pytest.mark.parametrize("size", [64, 84])
+def test_render_masks_match_raycast(size):
+    """Segment masks vs the ray caster; 84 is not a multiple of 16 (the reference accepts any
+    image size: the raster grid rounds up, the pixels outside the image are not written)."""
     if not torch.cuda.is_available():
         pytest.skip("needs an MI355X")
     import render_ref as RR
 
-    env, obs = _gpu_states(n=3, steps=40, size=64)
+    env, obs = _gpu_states(n=3, steps=40, size=size)
     seg = env.segmentation.cpu().numpy()
+    assert seg.shape == (3, 2, size, size) and obs["image_wrist"].shape == (3, size, size, 3)
     qpos = env.qpos.cpu().numpy()
     for i in range(3):
         pose = _oracle_pose_fn(qpos[i])
         for ci, cam in enumerate(("overhead", "wrist")):
-            ref = RR.render_seg(pose, cam, 64)
+            ref = RR.render_seg(pose, cam, size)
             agree = (seg[i, ci] == ref).mean()
             assert agree > 0.98, (i, cam, agree)  # silhouette edges may differ by a pixel
             for sid in np.unique(ref):

@@ -11,7 +11,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--round", default="r02")
+    ap.add_argument("--round", default="r03")
     ap.add_argument("--prof", default=os.path.join(REPO, "gpurun_out", "rpmc"))
     ap.add_argument("--last", type=int, default=32)
     ap.add_argument("--wg-per-dispatch", type=int, default=2048 * 2)  # envs x cameras (128^2: both bands in one workgroup)
@@ -36,8 +36,17 @@ def main():
            "per_workgroup": {k: v / a.wg_per_dispatch for k, v in out.items()},
            "valu_issue_per_wave_cycle": out.get("SQ_ACTIVE_INST_VALU", 0) / max(out.get("SQ_WAVE_CYCLES", 1), 1),
            "valu_insts_per_px": out.get("SQ_INSTS_VALU", 0) * 64 / a.px_per_dispatch}
+    # what bench.py's C5 line cites (its `render.valu`), tagged with the configuration measured
+    waves_per_simd = 4  # 512-lane workgroups (8 waves), two per CU (LDS), 4 SIMDs
+    res["config"] = {"workload": "render", "envs_per_gpu": 8192, "env_steps_per_launch": 1, "lanes": 4}
+    res["valu"] = {"bound": "valu-issue", "valu_insts_per_px": res["valu_insts_per_px"],
+                   "active_inst_valu_per_wave_cycle": res["valu_issue_per_wave_cycle"],
+                   "waves_per_simd": waves_per_simd, "frac": res["valu_issue_per_wave_cycle"] * waves_per_simd,
+                   "wait_any_per_wave_cycle": out.get("SQ_WAIT_ANY", 0) / max(out.get("SQ_WAVE_CYCLES", 1), 1),
+                   "source": f"profiles/{a.round}_render_pmc.json"}
     dst = os.path.join(REPO, "profiles", f"{a.round}_render_pmc.json")
     json.dump(res, open(dst, "w"), indent=1)
+    json.dump(res, open(os.path.join(REPO, "profiles", "pmc_render.json"), "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 
