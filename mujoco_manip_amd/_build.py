@@ -14,7 +14,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libmmx.so")
 LIB_PROF = os.path.join(PKG, "libmmx_prof.so")
-SOURCES = ["mmx_kernels.hip", "mmx_render.hip", "mmx_api.cpp"]
+SOURCES = ["mmx_kernels.hip", "mmx_render.hip", "mmx_png.hip", "mmx_api.cpp"]
 HEADERS = ["mmx_model_gen.h", "mmx_render_gen.h", "mmx_state.h", "mmx_device.h", "mmx_geom.h", "mmx_clock.h",
            os.path.join("..", "..", "include", "mmx_api.h")]
 ARCH = os.environ.get("MMX_OFFLOAD_ARCH", "gfx950")

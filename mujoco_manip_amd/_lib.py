@@ -56,7 +56,7 @@ EXPORTED = ("mmx_config_default", "mmx_create", "mmx_destroy", "mmx_last_error",
             "mmx_expert_plan", "mmx_rollout_expert", "mmx_physics_step", "mmx_forward", "mmx_get_buffers",
             "mmx_synchronize", "mmx_get_state", "mmx_set_state", "mmx_episode_seed", "mmx_rollout_lanes",
             "mmx_rollout_steps_per_launch", "mmx_expert_physics", "mmx_eval_reward", "mmx_kernel_timing",
-            "mmx_kernel_times")
+            "mmx_kernel_times", "mmx_png_bound", "mmx_png_scratch", "mmx_png_encode", "mmx_png_pack")
 
 _lib = None
 
@@ -93,6 +93,12 @@ def load(build_if_missing: bool = True):
     L.mmx_expert_physics.argtypes = [vp, C.c_int32]
     L.mmx_eval_reward.argtypes = [vp, vp, vp, vp, vp, C.c_int32]
     L.mmx_kernel_timing.argtypes = [vp, C.c_int32]
+    L.mmx_png_bound.argtypes = [C.c_int32, C.c_int32]
+    L.mmx_png_bound.restype = C.c_int64
+    L.mmx_png_scratch.argtypes = [C.c_int32, C.c_int32]
+    L.mmx_png_scratch.restype = C.c_int64
+    L.mmx_png_encode.argtypes = [vp, vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, vp, C.c_int64, vp, vp]
+    L.mmx_png_pack.argtypes = [vp, vp, C.c_int64, vp, vp, C.c_int32, vp]
     L.mmx_kernel_times.argtypes = [vp, fp, i32p, fp, i32p]
     L.mmx_get_buffers.argtypes = [vp, C.POINTER(MMXBuffers)]
     L.mmx_synchronize.argtypes = [vp]
@@ -102,7 +108,8 @@ def load(build_if_missing: bool = True):
     L.mmx_episode_seed.argtypes = [C.c_uint64, C.c_int32]
     for name in ("mmx_create", "mmx_reset", "mmx_step", "mmx_expert_plan", "mmx_rollout_expert", "mmx_physics_step",
                  "mmx_forward", "mmx_get_buffers", "mmx_synchronize", "mmx_get_state", "mmx_set_state",
-                 "mmx_expert_physics", "mmx_eval_reward", "mmx_kernel_timing", "mmx_kernel_times"):
+                 "mmx_expert_physics", "mmx_eval_reward", "mmx_kernel_timing", "mmx_kernel_times", "mmx_png_encode",
+                 "mmx_png_pack"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L
@@ -232,6 +239,43 @@ class Sim:
         self._check(self.L.mmx_kernel_times(self.ptr, C.byref(sm), C.byref(sn), C.byref(rm), C.byref(rn)),
                     "mmx_kernel_times")
         return {"step_ms": sm.value, "step_launches": sn.value, "render_ms": rm.value, "render_launches": rn.value}
+
+    def png_encode(self, images, max_batch: int = 4096):
+        """PNG files of RGB8 images [n, H, W, 3] (a CUDA uint8 tensor, any row-contiguous layout)
+        encoded on the device (mmx_png_encode), in batches of `max_batch`.  Returns (packed uint8
+        CUDA tensor, int64 offsets [n + 1] on the host): file i is packed[offsets[i]:offsets[i + 1]].
+        One host synchronisation per batch (the packed size)."""
+        import torch
+
+        n, H, W, c = images.shape
+        assert c == 3 and images.dtype == torch.uint8 and images.is_cuda
+        if n == 0:
+            return torch.empty(0, dtype=torch.uint8, device=images.device), np.zeros(1, np.int64)
+        imgs = images.contiguous()
+        bound, scr = int(self.L.mmx_png_bound(W, H)), int(self.L.mmx_png_scratch(W, H))
+        if bound < 0:
+            raise ValueError(f"unsupported image size {W} x {H}")
+        dev = imgs.device
+        parts, offs = [], [0]
+        for b0 in range(0, n, max_batch):
+            m = min(max_batch, n - b0)
+            out = torch.empty(m * bound, dtype=torch.uint8, device=dev)
+            scratch = torch.empty(m * scr, dtype=torch.uint8, device=dev)
+            sizes = torch.empty(m, dtype=torch.int32, device=dev)
+            self._check(self.L.mmx_png_encode(self.ptr, C.c_void_p(imgs[b0].data_ptr()), H * W * 3, m, W, H,
+                                              C.c_void_p(out.data_ptr()), bound, C.c_void_p(sizes.data_ptr()),
+                                              C.c_void_p(scratch.data_ptr())), "mmx_png_encode")
+            ends = torch.cumsum(sizes.to(torch.int64), 0)
+            starts = ends - sizes.to(torch.int64)
+            total = int(ends[-1].item())
+            packed = torch.empty(total, dtype=torch.uint8, device=dev)
+            self._check(self.L.mmx_png_pack(self.ptr, C.c_void_p(out.data_ptr()), bound, C.c_void_p(sizes.data_ptr()),
+                                            C.c_void_p(starts.data_ptr()), m, C.c_void_p(packed.data_ptr())),
+                        "mmx_png_pack")
+            parts.append(packed)
+            offs.extend((ends.cpu().numpy() + offs[-1]).tolist())
+        packed = torch.cat(parts) if len(parts) > 1 else parts[0]
+        return packed, np.asarray(offs, np.int64)
 
     @property
     def rollout_lanes(self) -> int:

@@ -23,6 +23,12 @@ extern "C" hipError_t mmx_launch_expert(const MMXState* S, int n, float* action,
 extern "C" hipError_t mmx_launch_physics(const MMXState* S, int n, int with_ik, hipStream_t st);
 extern "C" hipError_t mmx_launch_forward(const MMXState* S, hipStream_t st);
 extern "C" hipError_t mmx_launch_render(const MMXState* S, int base, int count, hipStream_t st);
+extern "C" hipError_t mmx_launch_png(const uint8_t* rgb, int64_t img_stride, int n, int W, int H, uint8_t* out,
+                                     int64_t out_stride, int32_t* sizes, uint32_t* scratch, hipStream_t st);
+extern "C" hipError_t mmx_launch_png_pack(const uint8_t* out, int64_t out_stride, const int32_t* sizes,
+                                          const int64_t* offsets, int n, uint8_t* packed, hipStream_t st);
+extern "C" int64_t mmx_png_bound_bytes(int width, int height);
+extern "C" int64_t mmx_png_scratch_bytes(int width, int height);
 extern "C" hipError_t mmx_launch_expert_physics(const MMXState* S, int n, hipStream_t st);
 extern "C" hipError_t mmx_launch_reward(const MMXState* S, const float* obj, const float* ee, const float* ctrl7,
                                         const int* pairs, int max_pairs, hipStream_t st);
@@ -471,6 +477,32 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
 }
 
 int mmx_rollout_lanes(const mmx_sim* sim) { return sim ? sim->nlanes : 0; }
+
+int64_t mmx_png_bound(int32_t width, int32_t height) {
+  return width > 0 && height > 0 && height <= 1024 ? mmx_png_bound_bytes(width, height) : -1;
+}
+int64_t mmx_png_scratch(int32_t width, int32_t height) {
+  return width > 0 && height > 0 && height <= 1024 ? mmx_png_scratch_bytes(width, height) : -1;
+}
+
+int mmx_png_encode(mmx_sim* sim, const uint8_t* rgb_dev, int64_t img_stride, int32_t n, int32_t width, int32_t height,
+                   uint8_t* out_dev, int64_t out_stride, int32_t* sizes_dev, void* scratch_dev) {
+  if (!sim || n < 0 || (n > 0 && (!rgb_dev || !out_dev || !sizes_dev || !scratch_dev)) || width <= 0 || height <= 0 ||
+      height > 1024 || img_stride < 3LL * width * height || out_stride < mmx_png_bound_bytes(width, height))
+    return sim ? fail(sim, MMX_EINVAL, "mmx_png_encode: bad arguments") : MMX_EINVAL;
+  DeviceGuard guard(sim);
+  return hip_check(sim, mmx_launch_png(rgb_dev, img_stride, n, width, height, out_dev, out_stride, sizes_dev,
+                                       static_cast<uint32_t*>(scratch_dev), sim->stream), "mmx_png_encode");
+}
+
+int mmx_png_pack(mmx_sim* sim, const uint8_t* out_dev, int64_t out_stride, const int32_t* sizes_dev,
+                 const int64_t* offsets_dev, int32_t n, uint8_t* packed_dev) {
+  if (!sim || n < 0 || (n > 0 && (!out_dev || !sizes_dev || !offsets_dev || !packed_dev)))
+    return sim ? fail(sim, MMX_EINVAL, "mmx_png_pack: bad arguments") : MMX_EINVAL;
+  DeviceGuard guard(sim);
+  return hip_check(sim, mmx_launch_png_pack(out_dev, out_stride, sizes_dev, offsets_dev, n, packed_dev, sim->stream),
+                   "mmx_png_pack");
+}
 
 int mmx_rollout_steps_per_launch(const mmx_sim* sim) {
   return sim ? (sim->S.image_size > 0 ? 1 : sim->fuse) : 0;

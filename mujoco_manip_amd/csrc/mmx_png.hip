@@ -1,0 +1,300 @@
+// Batched PNG encoder for gfx950 (LeRobot stores `dtype: image` features as
+// embedded PNG frames, generate_dataset.py:250-260).  The camera images never leave the device
+// raw: each RGB8 image becomes a complete PNG file in one workgroup, so the host receives
+// compressed bytes (flat-shaded renders compress ~8x) and does no image work.
+//
+// One 256-lane workgroup per image:
+//   1. rows in parallel (one row per lane): the PNG scanline (filter byte 0 + RGB bytes) is parsed
+//      greedily into deflate symbols with two match candidates, the same pixel 3 bytes back and
+//      the byte one scanline above (distance 3 S + 1); matches stay inside their row, so every
+//      row parses independently.  Pass 1 counts each row's bits (fixed Huffman codes, RFC 1951
+//      §3.2.6) and its Adler-32 partial sums; a workgroup scan gives every row its bit offset in
+//      the single final block; pass 2 re-parses and writes the row's bits to a row-private
+//      scratch stream;
+//   2. every lane assembles whole dwords of the block from the rows that overlap them (no atomics),
+//      then the zlib stream (header 78 01, block, Adler-32) is cut into IDAT chunks of kChunk
+//      bytes written after the signature and IHDR; one lane per chunk computes its CRC-32; IEND
+//      closes the file.  The size goes to sizes[image].
+// Valid for any PNG decoder (a fixed-Huffman block, standard chunks); tests/test_png.py decodes
+// with PIL and zlib and compares pixels exactly.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define PNG_WG 256
+static constexpr int kChunk = 512;  // IDAT data bytes per chunk (12 bytes of framing each)
+static constexpr int kMaxMatch = 258;
+
+__host__ __device__ inline int64_t png_row_words(int width) {  // row scratch: worst case 9 bits per byte
+  return ((int64_t)(3 * width + 1) * 9 + 31) / 32 + 1;
+}
+__host__ __device__ inline int64_t png_zlib_bound(int width, int height) {
+  const int64_t bits = 3 + (int64_t)height * (3 * width + 1) * 9 + 7;
+  return 2 + (bits + 7) / 8 + 4;
+}
+// worst-case PNG size: signature + IHDR + chunked IDAT + IEND
+__host__ __device__ inline int64_t png_bound(int width, int height) {
+  const int64_t z = png_zlib_bound(width, height);
+  return 8 + 25 + z + 12 * ((z + kChunk - 1) / kChunk) + 12;
+}
+
+__device__ inline uint32_t bit_reverse(uint32_t v, int n) { return __builtin_bitreverse32(v) >> (32 - n); }
+
+// fixed-Huffman literal / length symbol -> (reversed code, bits)
+__device__ inline void lit_code(int sym, uint32_t& code, int& nb) {
+  if (sym < 144) { code = 0x30 + sym; nb = 8; }
+  else if (sym < 256) { code = 0x190 + (sym - 144); nb = 9; }
+  else if (sym < 280) { code = sym - 256; nb = 7; }
+  else { code = 0xC0 + (sym - 280); nb = 8; }
+  code = bit_reverse(code, nb);
+}
+// match length 3..258 -> symbol 257..285, extra bits, extra value
+__device__ inline void len_sym(int len, int& sym, int& eb, int& ev) {
+  if (len == 258) { sym = 285; eb = 0; ev = 0; return; }
+  if (len <= 10) { sym = 254 + len; eb = 0; ev = 0; return; }
+  // lengths 11..257: groups of 4 codes per extra-bit count e = 1..5, base 3 + 4 * 2^e
+  const int v = len - 3;               // 8 .. 254
+  const int e = 29 - __builtin_clz(v);  // floor(log2 v) - 2 (v >= 8 -> e >= 1)
+  const int base = (4 + ((v >> e) - 4)) << e;  // (4 + q) << e with q = (v >> e) - 4 in 0..3
+  sym = 265 + 4 * (e - 1) + ((v >> e) - 4);
+  eb = e;
+  ev = v - base;
+}
+// distance 1..32768 -> code 0..29, extra bits, extra value
+__device__ inline void dist_code(int d, int& code, int& eb, int& ev) {
+  if (d <= 4) { code = d - 1; eb = 0; ev = 0; return; }
+  const int v = d - 1;
+  const int e = 30 - __builtin_clz(v);  // floor(log2 v) - 1
+  const int hi = (v >> e) & 1;
+  code = 2 * e + 2 + hi;
+  eb = e;
+  ev = v - ((2 + hi) << e);
+}
+
+struct BitSink {  // LSB-first bit writer into a row-private word stream
+  uint32_t* w;
+  uint64_t acc;
+  int n;
+  int64_t words;
+  __device__ void put(uint32_t v, int nb) {
+    acc |= (uint64_t)v << n;
+    n += nb;
+    if (n >= 32) {
+      w[words++] = (uint32_t)acc;
+      acc >>= 32;
+      n -= 32;
+    }
+  }
+  __device__ void flush() {
+    if (n > 0) w[words++] = (uint32_t)acc;
+  }
+};
+
+// row r's scanline byte t (t = 0: filter byte 0, else RGB byte t - 1)
+__device__ inline int scan_byte(const uint8_t* row, int t) { return t == 0 ? 0 : row[t - 1]; }
+
+// greedy parse of one scanline; EMIT = false counts bits, true writes them
+template <bool EMIT>
+__device__ int64_t parse_row(const uint8_t* row, const uint8_t* above, int L1, BitSink* bs) {
+  int64_t bits = 0;
+  const int dfar = L1;  // one scanline back
+  int t = 0;
+  while (t < L1) {
+    const int lim = min(kMaxMatch, L1 - t);
+    int m2 = 0, m1 = 0;
+    if (above) {  // the byte above (filter bytes are both 0)
+      while (m2 < lim && scan_byte(row, t + m2) == scan_byte(above, t + m2)) m2++;
+    }
+    if (t >= 3) {  // the same channel one pixel back (inside the row)
+      while (m1 < lim && scan_byte(row, t + m1) == scan_byte(row, t + m1 - 3)) m1++;
+    }
+    const bool near = m1 >= m2;  // ties: the 3-byte distance (no extra bits)
+    const int m = near ? m1 : m2;
+    if (m >= 3) {
+      int sym, eb, ev, dc, deb, dev;
+      len_sym(m, sym, eb, ev);
+      dist_code(near ? 3 : dfar, dc, deb, dev);
+      uint32_t code;
+      int nb;
+      lit_code(sym, code, nb);
+      bits += nb + eb + 5 + deb;
+      if (EMIT) {
+        bs->put(code, nb);
+        if (eb) bs->put((uint32_t)ev, eb);
+        bs->put(bit_reverse((uint32_t)dc, 5), 5);
+        if (deb) bs->put((uint32_t)dev, deb);
+      }
+      t += m;
+    } else {
+      uint32_t code;
+      int nb;
+      lit_code(scan_byte(row, t), code, nb);
+      bits += nb;
+      if (EMIT) bs->put(code, nb);
+      t++;
+    }
+  }
+  return bits;
+}
+
+__device__ inline void put_be32(uint8_t* p, uint32_t v) {
+  p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
+}
+
+__device__ uint32_t crc_table(int k) {  // CRC-32 (IEEE, reflected) table entry, computed on the fly
+  uint32_t c = (uint32_t)k;
+  for (int j = 0; j < 8; j++) c = (c & 1u) ? 0xEDB88320u ^ (c >> 1) : (c >> 1);
+  return c;
+}
+
+extern "C" __global__ void __launch_bounds__(PNG_WG)
+mmx_png_kernel(const uint8_t* rgb, int64_t img_stride, int W, int H, uint8_t* out, int64_t out_stride,
+               int32_t* sizes, uint32_t* scratch) {
+  __shared__ int64_t s_off[1025];  // bit offset of each row in the block (H <= 1024)
+  __shared__ uint64_t s_a1[PNG_WG], s_a2[PNG_WG];
+  __shared__ uint32_t s_crc[256];
+  __shared__ int64_t s_tot;
+  const int img = blockIdx.x, tid = threadIdx.x;
+  const uint8_t* im = rgb + (int64_t)img * img_stride;
+  const int L = 3 * W, L1 = L + 1;
+  const int64_t rw = png_row_words(W);
+  uint32_t* scr = scratch + (int64_t)img * H * rw;
+  uint8_t* o = out + (int64_t)img * out_stride;
+  s_crc[tid] = crc_table(tid);  // (PNG_WG = 256 entries)
+  // pass 1: row bit counts and Adler-32 partial sums (s1: sum of bytes, s2: sum of (n - i) byte_i)
+  const uint64_t n = (uint64_t)H * L1;
+  uint64_t a1 = 0, a2 = 0;
+  for (int r = tid; r < H; r += PNG_WG) {
+    const uint8_t* row = im + (int64_t)r * L;
+    s_off[r + 1] = parse_row<false>(row, r ? row - L : nullptr, L1, nullptr);
+    const uint64_t i0 = (uint64_t)r * L1 + 1;  // the filter byte (0) adds nothing
+    for (int k = 0; k < L; k++) {
+      const uint64_t b = row[k];
+      a1 += b;
+      a2 += (n - (i0 + k)) * b;
+    }
+  }
+  s_a1[tid] = a1;
+  s_a2[tid] = a2;
+  __syncthreads();
+  if (tid == 0) {  // exclusive scan of the row bit counts after the 3 block-header bits; Adler-32
+    s_off[0] = 3;
+    for (int r = 0; r < H; r++) s_off[r + 1] += s_off[r];
+    uint64_t A1 = 1, A2 = n;  // s2 = n (the initial 1 of s1 counted at each byte) + sum (n - i) b_i
+    for (int k = 0; k < PNG_WG; k++) {
+      A1 += s_a1[k];
+      A2 += s_a2[k];
+    }
+    s_a1[0] = ((A2 % 65521u) << 16) | (A1 % 65521u);
+    s_tot = s_off[H] + 7;  // + end of block (code 256: seven 0 bits)
+  }
+  __syncthreads();
+  // pass 2: each row's bits into its private stream
+  for (int r = tid; r < H; r += PNG_WG) {
+    const uint8_t* row = im + (int64_t)r * L;
+    BitSink bs{scr + (int64_t)r * rw, 0ull, 0, 0};
+    parse_row<true>(row, r ? row - L : nullptr, L1, &bs);
+    bs.flush();
+  }
+  __threadfence();  // the streams are read by other lanes of the workgroup
+  __syncthreads();
+  const uint32_t adler = (uint32_t)s_a1[0];
+  const int64_t nbits = s_tot, nd = (nbits + 7) / 8;  // deflate bytes
+  const int64_t zlen = 2 + nd + 4;
+  const int64_t nchunk = (zlen + kChunk - 1) / kChunk;
+  uint8_t* idat = o + 8 + 25;
+  // deflate block dword w: the header bits and the rows overlapping [32 w, 32 w + 32); written as
+  // bytes into the chunked layout (zlib byte j lives at idat + 12 (j / kChunk) + 8 + j % kChunk)
+  const int64_t nw = (nbits + 31) / 32;
+  for (int64_t w = tid; w < nw; w += PNG_WG) {
+    const int64_t b0 = 32 * w, b1 = b0 + 32;
+    uint32_t v = w == 0 ? 3u : 0u;  // BFINAL = 1, BTYPE = 01 (fixed Huffman)
+    int lo = 0, hi = H;             // first row whose range ends after b0
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (s_off[mid + 1] <= b0) lo = mid + 1;
+      else hi = mid;
+    }
+    for (int r = lo; r < H && s_off[r] < b1; r++) {
+      const int64_t rs = s_off[r], re = s_off[r + 1];
+      const int64_t lb = max(b0, rs) - rs;  // local bit in the row's stream
+      const int64_t take = min(b1, re) - (rs + lb);
+      if (take <= 0) continue;
+      const uint32_t* rwp = scr + (int64_t)r * rw;
+      const int64_t k = lb >> 5;
+      const int s = (int)(lb & 31);
+      uint64_t bits = rwp[k];
+      if (s + take > 32) bits |= (uint64_t)rwp[k + 1] << 32;
+      bits >>= s;
+      if (take < 32) bits &= (1ull << take) - 1;
+      v |= (uint32_t)(bits << (rs + lb - b0));
+    }
+    for (int q = 0; q < 4; q++) {
+      const int64_t j = 2 + 4 * w + q;  // zlib byte
+      if (j - 2 < nd) idat[12 * (j / kChunk) + 8 + j % kChunk] = (uint8_t)(v >> (8 * q));
+    }
+  }
+  if (tid == 0) {  // signature, IHDR, zlib header and Adler-32, chunk headers, IEND, size
+    const uint8_t sig[8] = {0x89, 'P', 'N', 'G', 0x0D, 0x0A, 0x1A, 0x0A};
+    for (int k = 0; k < 8; k++) o[k] = sig[k];
+    uint8_t* ih = o + 8;
+    put_be32(ih, 13);
+    ih[4] = 'I'; ih[5] = 'H'; ih[6] = 'D'; ih[7] = 'R';
+    put_be32(ih + 8, (uint32_t)W);
+    put_be32(ih + 12, (uint32_t)H);
+    ih[16] = 8; ih[17] = 2; ih[18] = 0; ih[19] = 0; ih[20] = 0;  // 8-bit RGB, deflate, no interlace
+    uint32_t c = 0xFFFFFFFFu;
+    for (int k = 4; k < 21; k++) c = crc_table((c ^ ih[k]) & 255) ^ (c >> 8);
+    put_be32(ih + 21, ~c);
+    const uint8_t zh[2] = {0x78, 0x01};
+    for (int j = 0; j < 2; j++) idat[12 * (j / kChunk) + 8 + j % kChunk] = zh[j];
+    for (int q = 0; q < 4; q++) {
+      const int64_t j = 2 + nd + q;
+      idat[12 * (j / kChunk) + 8 + j % kChunk] = (uint8_t)(adler >> (24 - 8 * q));
+    }
+    for (int64_t ch = 0; ch < nchunk; ch++) {
+      uint8_t* hp = idat + ch * (kChunk + 12);
+      put_be32(hp, (uint32_t)min((int64_t)kChunk, zlen - ch * kChunk));
+      hp[4] = 'I'; hp[5] = 'D'; hp[6] = 'A'; hp[7] = 'T';
+    }
+    uint8_t* ie = idat + nchunk * 12 + zlen;
+    const uint8_t iend[12] = {0, 0, 0, 0, 'I', 'E', 'N', 'D', 0xAE, 0x42, 0x60, 0x82};
+    for (int k = 0; k < 12; k++) ie[k] = iend[k];
+    sizes[img] = (int32_t)(8 + 25 + nchunk * 12 + zlen + 12);
+  }
+  __threadfence();
+  __syncthreads();
+  for (int64_t ch = tid; ch < nchunk; ch += PNG_WG) {  // one lane per chunk: CRC of type + data
+    uint8_t* hp = idat + ch * (kChunk + 12);
+    const int64_t len = min((int64_t)kChunk, zlen - ch * kChunk);
+    uint32_t c = 0xFFFFFFFFu;
+    for (int64_t k = 4; k < 8 + len; k++) c = s_crc[(c ^ hp[k]) & 255] ^ (c >> 8);
+    put_be32(hp + 8 + len, ~c);
+  }
+}
+
+// packed[offsets[i] ..] = the first sizes[i] bytes of image i's slot
+extern "C" __global__ void __launch_bounds__(PNG_WG)
+mmx_png_pack_kernel(const uint8_t* out, int64_t out_stride, const int32_t* sizes, const int64_t* offsets, uint8_t* packed) {
+  const int i = blockIdx.x;
+  const uint8_t* src = out + (int64_t)i * out_stride;
+  uint8_t* dst = packed + offsets[i];
+  for (int k = threadIdx.x; k < sizes[i]; k += PNG_WG) dst[k] = src[k];
+}
+
+extern "C" int64_t mmx_png_bound_bytes(int width, int height) { return png_bound(width, height); }
+extern "C" int64_t mmx_png_scratch_bytes(int width, int height) { return (int64_t)height * png_row_words(width) * 4; }
+
+extern "C" hipError_t mmx_launch_png(const uint8_t* rgb, int64_t img_stride, int n, int W, int H, uint8_t* out,
+                                     int64_t out_stride, int32_t* sizes, uint32_t* scratch, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (W <= 0 || H <= 0 || H > 1024 || out_stride < png_bound(W, H)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(mmx_png_kernel, dim3(n), dim3(PNG_WG), 0, st, rgb, img_stride, W, H, out, out_stride, sizes,
+                     scratch);
+  return hipGetLastError();
+}
+extern "C" hipError_t mmx_launch_png_pack(const uint8_t* out, int64_t out_stride, const int32_t* sizes,
+                                          const int64_t* offsets, int n, uint8_t* packed, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mmx_png_pack_kernel, dim3(n), dim3(PNG_WG), 0, st, out, out_stride, sizes, offsets, packed);
+  return hipGetLastError();
+}

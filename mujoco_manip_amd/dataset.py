@@ -20,7 +20,7 @@ MI355X instead of one after another:
 
 Camera images (observation.images.overhead / .wrist, features.py:11-20, 224 x 224 RGB) come from
 the batched HIP renderer (mmx_render.hip): the PRE-step images of every active
-slot are gathered on device each step, PNG-encoded by a host thread pool and stored the way LeRobot stores
+slot are gathered on device each step, encoded to PNG files on the device (mmx_png.hip) and stored the way LeRobot stores
 `dtype: image` features with use_videos=False (generate_dataset.py:250-260): a parquet struct
 column {bytes: PNG, path} per frame, per-channel image statistics in meta/stats.json.
 LeRobot itself is not importable here, so the on-disk layout follows LeRobot v3.0's documented
@@ -284,24 +284,42 @@ def _raw_image_stats(frames_u8: list) -> dict:
             "_sum": x.sum(0).tolist(), "_sumsq": (x * x).sum(0).tolist(), "_n": int(len(x))}
 
 
+def _frame_image_stats(imgs):
+    """Per-frame channel statistics of uint8 images [k, H, W, 3] on the device: min, max, sum and
+    sum of squares of the pixel values scaled to [0, 1] -> float64 [k, 4, 3]."""
+    import torch
+
+    x = imgs.reshape(imgs.shape[0], -1, 3).to(torch.float64) * (1.0 / 255.0)
+    return torch.stack([x.amin(1), x.amax(1), x.sum(1), (x * x).sum(1)], 1)
+
+
+def _merge_image_stats(fs: np.ndarray, npx: int) -> dict:
+    """Episode image statistics from its frames' [T, 4, 3] statistics (same layout as
+    _raw_image_stats, over every pixel of every frame)."""
+    mn, mx, sm, sq = fs[:, 0].min(0), fs[:, 1].max(0), fs[:, 2].sum(0), fs[:, 3].sum(0)
+    n = npx * len(fs)
+    mean = sm / n
+    shape = lambda v: [[[float(a)]] for a in v]  # noqa: E731
+    return {"min": shape(mn), "max": shape(mx), "mean": shape(mean),
+            "std": shape(np.sqrt(np.maximum(sq / n - mean * mean, 0.0))), "_sum": sm.tolist(), "_sumsq": sq.tolist(),
+            "_n": int(n)}
+
+
 def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type="staged", randomize_objects=False,
                      seed=0, spawn_x_range=(-0.20, 0.20), spawn_y_range=(0.30, 0.45), num_envs=1024, device=0,
-                     max_gym_steps=5000, on_step=None, sink=None, png_workers=None, image_size=IMAGE_SIZE,
-                     stats_frames=8):
+                     max_gym_steps=5000, on_step=None, sink=None, image_size=IMAGE_SIZE):
     """Run `num_episodes` reference run_episode loops (generate_dataset.py:83-198) side by side.
 
     Streaming: each step's frames (active slots only) are gathered on the device, copied to pinned
-    host memory on a side stream and split into their episodes on the host; camera frames are
-    PNG-encoded by a pool of `png_workers` threads (the reference's image writer uses 4,
-    generate_dataset.py:260) while the device runs the next steps.  Device memory is O(envs): no
-    frame stays on the device after its copy.  A finished episode (FSM DONE) is handed to
-    `sink(episode)` in episode-index order as soon as its frames are encoded, so the host holds
-    only the episodes in flight; without a sink the episodes are returned as a list.
-    on_step(slots, episode_ids, env), when given, sees the env before each batched step.
-    Returns (episodes or None, seeds).
+    host memory on a side stream and split into their episodes on the host.  Camera frames are
+    encoded to PNG files on the device (mmx_png_encode; LeRobot embeds image features as PNG,
+    generate_dataset.py:250-260) with their per-channel statistics, so only the compressed files
+    cross PCIe and the host does no image work.  Device memory is O(envs): no frame stays on the
+    device after its copy.  A finished episode (FSM DONE) is handed to `sink(episode)` in
+    episode-index order, so the host holds only the episodes in flight; without a sink the episodes
+    are returned as a list.  on_step(slots, episode_ids, env), when given, sees the env before each
+    batched step.  Returns (episodes or None, seeds).
     """
-    import concurrent.futures as cf
-
     import torch
 
     from .vec_env import PickPlaceVecEnv
@@ -319,13 +337,12 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
     need_reward = "next.reward" in feature_keys and reward_type == "staged"
     obs_feats = [(k, f) for k, f in OBS_TO_FEATURE.items() if f in feature_keys]
     img_feats = [(cam, f) for cam, f in enumerate(IMAGE_KEYS) if f in feature_keys]
-    pool = cf.ThreadPoolExecutor(max_workers=png_workers or min(16, os.cpu_count() or 4)) if img_feats else None
+    npx = image_size * image_size
 
     eps = [Episode(e, *task_list[e % len(task_list)], seeds[e] if seeds else None) for e in range(E)]
-    rows = [dict() for _ in range(E)]  # episode -> feature -> list of per-frame values (host)
+    rows = [dict() for _ in range(E)]  # episode -> "_rows": [(step id, row)], image key -> [PNG bytes]
     slot_ep = np.full(N, -1, np.int64)
     next_ep = 0
-    finished_marks = []  # (step index, episode): the episode's last frame is in steps < step index
     out_eps = [] if sink is None else None
     emitted = 0
     done_eps = {}  # finished, awaiting in-order emission: episode -> True
@@ -352,26 +369,22 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
     sid_counter = [0]
 
     def absorb(host, payload):
-        """Index one step's host copy by episode (one row per active episode); images go to the
-        PNG pool straight away."""
-        slots, ep_ids = payload
+        """Index one step's host copy by episode (one row per active episode); the PNG files are
+        cut out of the step's packed buffer."""
+        slots, ep_ids, png_offs = payload
         if len(ep_ids) == 0:
             return
         sid = sid_counter[0]
         sid_counter[0] += 1
+        for k, offs in png_offs.items():
+            buf = host.pop(k + "/png").tobytes()
+            for j, e in enumerate(ep_ids):
+                rows[e].setdefault(k, []).append(buf[offs[j]:offs[j + 1]])
         steps_host[sid] = [host, len(ep_ids)]
         for j, e in enumerate(ep_ids):
-            r = rows[e]
-            r.setdefault("_rows", []).append((sid, j))
-            for k in IMAGE_KEYS:
-                if k in host:
-                    im = host[k][j]
-                    lst = r.setdefault(k, [])
-                    if len(lst) < stats_frames:  # raw frames of the statistics sample
-                        r.setdefault(k + "/raw", []).append(im.copy())
-                    lst.append(pool.submit(png_encode, im))
+            rows[e].setdefault("_rows", []).append((sid, j))
 
-    def finalize(e):
+def finalize(e):
         ep = eps[e]
         r = rows[e]
         refs = r.get("_rows", [])
@@ -379,9 +392,9 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
         ep.image_stats = {}
         for k in feature_keys:
             if k in IMAGE_KEYS:
-                ep.frames[k] = [f.result() for f in r.get(k, [])]
-                raw = r.get(k + "/raw")
-                ep.image_stats[k] = _raw_image_stats(raw) if raw else None
+                ep.frames[k] = r.get(k, [])
+                fs = np.stack([steps_host[sid][0][k + "/stats"][j] for sid, j in refs]) if refs else None
+                ep.image_stats[k] = _merge_image_stats(fs, npx) if fs is not None else None
             elif k == "observation.phase_description":
                 ep.frames[k] = [phase_description(steps_host[sid][0]["_fsm"][j], ep.obj, ep.bin) for sid, j in refs]
             elif refs and k in steps_host[refs[0][0]][0]:
@@ -396,9 +409,6 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
         nonlocal emitted
         while emitted < E and emitted in done_eps:
             e = emitted
-            r = rows[e]
-            if not block and r is not None and any(not f.done() for k in IMAGE_KEYS for f in r.get(k, [])):
-                return
             finalize(e)
             del done_eps[e]
             if sink is not None:
@@ -413,7 +423,7 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
 
     def process(items):
         for host, payload in items:
-            absorb(host, payload[:2])
+            absorb(host, (payload[0], payload[1], payload[3]))
             for e in payload[2]:  # episodes whose last frame was in this or an earlier step
                 done_eps[e] = True
 
@@ -436,7 +446,7 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
         act_slots = np.where((slot_ep >= 0) & ~done_before)[0]
         if len(act_slots) == 0:
             if fin_eps:
-                ring.push({}, (act_slots, np.zeros(0, np.int64), fin_eps))
+                ring.push({}, (act_slots, np.zeros(0, np.int64), fin_eps, {}))
             process(ring.ready())
             emit_ready()
             continue
@@ -447,8 +457,11 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
         for k, f in obs_feats:
             a, b, _ = OBS_SLICES[k]
             frame[f] = obs_pre[:, a:b]
+        png_offs = {}
         for cam, f in img_feats:  # PRE-step images (rendered after the reset / previous step)
-            frame[f] = env._images[:, cam].index_select(0, idx)
+            imgs = env._images[:, cam].index_select(0, idx)
+            frame[f + "/png"], png_offs[f] = env.sim.png_encode(imgs)
+            frame[f + "/stats"] = _frame_image_stats(imgs)
         a_sel = action.index_select(0, idx)
         if need_actions:
             T = env.initial_ee_se3.index_select(0, idx)
@@ -462,7 +475,7 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
         env.step(action)
         if need_reward:
             frame["next.reward"] = env._rc.index_select(0, idx)
-        ring.push(frame, (act_slots, slot_ep[act_slots].copy(), fin_eps))
+        ring.push(frame, (act_slots, slot_ep[act_slots].copy(), fin_eps, png_offs))
         process(ring.ready())
         emit_ready()
         step_no += 1
@@ -473,8 +486,6 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
     emit_ready(block=True)
     torch.cuda.synchronize(dev)
     env.close()
-    if pool is not None:
-        pool.shutdown()
     return out_eps, seeds
 
 
@@ -689,7 +700,7 @@ def read_lerobot_v3(root: str):
 # ----------------------------------------------------------------------------- entry point
 def generate(repo_id, num_episodes=100, root="./datasets", task=None, tasks="all", reward_type="staged",
              randomize_objects=False, seed=0, spawn_x_range=(-0.20, 0.20), spawn_y_range=(0.30, 0.45),
-             features=None, num_envs=1024, device=0, png_workers=None, image_size=IMAGE_SIZE):
+             features=None, num_envs=1024, device=0, image_size=IMAGE_SIZE):
     """generate_dataset.main (generate_dataset.py:201-333) with the episodes batched on the GPU and
     streamed to the LeRobot writer as they finish."""
     if not repo_id:
@@ -701,7 +712,7 @@ def generate(repo_id, num_episodes=100, root="./datasets", task=None, tasks="all
     _, seeds = collect_episodes(num_episodes, task_list, set(feats), reward_type=reward_type,
                                 randomize_objects=randomize_objects, seed=seed, spawn_x_range=spawn_x_range,
                                 spawn_y_range=spawn_y_range, num_envs=num_envs, device=device, sink=writer.add_episode,
-                                png_workers=png_workers, image_size=image_size)
+                                image_size=image_size)
     cfg = {"repo_id": repo_id, "num_episodes": int(num_episodes), "root": root,
            "task": list(task) if task is not None else None, "tasks": tasks, "reward_type": reward_type,
            "randomize_objects": bool(randomize_objects), "seed": int(seed), "spawn_x_range": list(spawn_x_range),

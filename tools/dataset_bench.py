@@ -22,7 +22,6 @@ def main():
     ap.add_argument("--num-envs", type=int, default=8192)
     ap.add_argument("--episodes", type=int, default=8192)
     ap.add_argument("--image-size", type=int, default=128)
-    ap.add_argument("--png-workers", type=int, default=16)
     ap.add_argument("--root", default="/tmp/mmx_ds")
     ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "dataset_bench.json"))
     ap.add_argument("--keep", action="store_true")
@@ -59,14 +58,14 @@ def main():
 
     t0 = time.perf_counter()
     D.collect_episodes(a.episodes, D.TASK_SETS["all"], set(feats), randomize_objects=True, seed=0,
-                       num_envs=a.num_envs, sink=sink, png_workers=a.png_workers, image_size=a.image_size,
+                       num_envs=a.num_envs, sink=sink, image_size=a.image_size,
                        on_step=on_step)
     info = writer.close()
     dt = time.perf_counter() - t0
     rss = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0  # MB (Linux: KB)
     size = sum(os.path.getsize(os.path.join(d, f)) for d, _, fs in os.walk(path) for f in fs)
     rec = {"config": {"num_envs": a.num_envs, "episodes": a.episodes, "image_size": a.image_size,
-                      "png_workers": a.png_workers, "features": "all (2 cameras, numeric, actions, reward, phase)"},
+                      "png": "device (mmx_png_encode)", "features": "all (2 cameras, numeric, actions, reward, phase)"},
            "episodes": info["total_episodes"], "frames": info["total_frames"], "seconds": dt,
            "frames_per_s": info["total_frames"] / dt, "images_per_s": 2 * info["total_frames"] / dt,
            "png_mean_bytes": png_bytes[0] / max(2 * frames[0], 1), "dataset_bytes": size,
