@@ -384,7 +384,7 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
         for j, e in enumerate(ep_ids):
             rows[e].setdefault("_rows", []).append((sid, j))
 
-def finalize(e):
+    def finalize(e):
         ep = eps[e]
         r = rows[e]
         refs = r.get("_rows", [])
