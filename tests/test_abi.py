@@ -10,7 +10,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared_functions():
     src = open(os.path.join(REPO, "include", "mmx_api.h")).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|const char\*|uint32_t)\s+(mmx_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|int64_t|void|const char\*|uint32_t)\s+(mmx_\w+)\s*\(", src, re.M)))
 
 
 def test_library_exports_every_declared_symbol():
