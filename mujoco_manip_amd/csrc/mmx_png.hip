@@ -136,6 +136,9 @@ __device__ int64_t parse_row(const uint8_t* row, const uint8_t* above, int L1, B
   return bits;
 }
 
+// zlib byte j inside the chunked IDAT area: chunk j / kChunk, after its 8-byte length + type
+__device__ inline int64_t zpos(int64_t j) { return j + 12 * (j / kChunk) + 8; }
+
 __device__ inline void put_be32(uint8_t* p, uint32_t v) {
   p[0] = (uint8_t)(v >> 24); p[1] = (uint8_t)(v >> 16); p[2] = (uint8_t)(v >> 8); p[3] = (uint8_t)v;
 }
@@ -203,7 +206,7 @@ mmx_png_kernel(const uint8_t* rgb, int64_t img_stride, int W, int H, uint8_t* ou
   const int64_t nchunk = (zlen + kChunk - 1) / kChunk;
   uint8_t* idat = o + 8 + 25;
   // deflate block dword w: the header bits and the rows overlapping [32 w, 32 w + 32); written as
-  // bytes into the chunked layout (zlib byte j lives at idat + 12 (j / kChunk) + 8 + j % kChunk)
+  // bytes into the chunked layout (zlib byte j lives at idat + zpos(j))
   const int64_t nw = (nbits + 31) / 32;
   for (int64_t w = tid; w < nw; w += PNG_WG) {
     const int64_t b0 = 32 * w, b1 = b0 + 32;
@@ -230,7 +233,7 @@ mmx_png_kernel(const uint8_t* rgb, int64_t img_stride, int W, int H, uint8_t* ou
     }
     for (int q = 0; q < 4; q++) {
       const int64_t j = 2 + 4 * w + q;  // zlib byte
-      if (j - 2 < nd) idat[12 * (j / kChunk) + 8 + j % kChunk] = (uint8_t)(v >> (8 * q));
+      if (j - 2 < nd) idat[zpos(j)] = (uint8_t)(v >> (8 * q));
     }
   }
   if (tid == 0) {  // signature, IHDR, zlib header and Adler-32, chunk headers, IEND, size
@@ -246,10 +249,10 @@ mmx_png_kernel(const uint8_t* rgb, int64_t img_stride, int W, int H, uint8_t* ou
     for (int k = 4; k < 21; k++) c = crc_table((c ^ ih[k]) & 255) ^ (c >> 8);
     put_be32(ih + 21, ~c);
     const uint8_t zh[2] = {0x78, 0x01};
-    for (int j = 0; j < 2; j++) idat[12 * (j / kChunk) + 8 + j % kChunk] = zh[j];
+    for (int j = 0; j < 2; j++) idat[zpos(j)] = zh[j];
     for (int q = 0; q < 4; q++) {
       const int64_t j = 2 + nd + q;
-      idat[12 * (j / kChunk) + 8 + j % kChunk] = (uint8_t)(adler >> (24 - 8 * q));
+      idat[zpos(j)] = (uint8_t)(adler >> (24 - 8 * q));
     }
     for (int64_t ch = 0; ch < nchunk; ch++) {
       uint8_t* hp = idat + ch * (kChunk + 12);
