@@ -156,19 +156,32 @@ DEV int clip_poly(const V3* in, int n, V3* out, V3 a, float b) {
   return m;
 }
 
-// box-box: 15-axis SAT; face contacts clip the incident face against the reference face
-// (<= 8 points), edge-edge contacts give one point at the midpoint of the closest points.
 DEV V3 sel3(V3 a0, V3 a1, V3 a2, int k) { return k == 0 ? a0 : (k == 1 ? a1 : a2); }
 DEV float self3(float a0, float a1, float a2, int k) { return k == 0 ? a0 : (k == 1 ? a1 : a2); }
 
-// poly, tmp: 8 V3 each of per-lane LDS scratch (a quad clipped by 4 half-planes has <= 8 corners)
-template <class Sink>
-DEV void box_box(Sink& cs, const Geom& G1, const Geom& G2, V3 hb1, V3 hb2, V3* poly, V3* tmp) {
-  CLK_DECL;
-  const float h1[3] = {hb1.x, hb1.y, hb1.z}, h2[3] = {hb2.x, hb2.y, hb2.z};
-  const V3 A[3] = {col(G1.R, 0), col(G1.R, 1), col(G1.R, 2)};
-  const V3 B[3] = {col(G2.R, 0), col(G2.R, 1), col(G2.R, 2)};
+// box-box, split in the parts the lane-per-pair (box_box) and lane-quad (box_box_quad) forms share:
+// the 15-axis SAT, the edge-edge contact and the face-contact setup (reference / incident faces).
+struct BoxSat {
+  V3 A[3], B[3], d;
+  float h1[3], h2[3];
+  float best_face, best_edge;
+  int face_axis, ei, ej;
+  bool sep;
+};
+DEV void box_sat(const Geom& G1, const Geom& G2, V3 hb1, V3 hb2, BoxSat& S) {
+  S.h1[0] = hb1.x; S.h1[1] = hb1.y; S.h1[2] = hb1.z;
+  S.h2[0] = hb2.x; S.h2[1] = hb2.y; S.h2[2] = hb2.z;
+  const float* h1 = S.h1;
+  const float* h2 = S.h2;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    S.A[k] = col(G1.R, k);
+    S.B[k] = col(G2.R, k);
+  }
+  const V3* A = S.A;
+  const V3* B = S.B;
   const V3 d = G2.x - G1.x;
+  S.d = d;
   // SAT in the relative-rotation form (R = A'B, t = A'd, u = B'd): face axes of box 1, of box 2,
   // then the 9 edge-edge axes A_i x B_j, whose projections are again entries of R (unit axes;
   // depths divided by |A_i x B_j|).  Same axes, order and strict-minimum tie rule as the
@@ -216,32 +229,54 @@ DEV void box_box(Sink& cs, const Geom& G1, const Geom& G2, V3 hb1, V3 hb2, V3* p
         ej = b;
       }
     }
-  if (sep) return;
-  V3 eL = V3{0.f, 0.f, 0.f};
-  if (ei >= 0) eL = normalize(cross(sel3(A[0], A[1], A[2], ei), sel3(B[0], B[1], B[2], ej)));
-  PROBEF(8, cs.E->stats, STAT_T_AUX0);
-  if (ei >= 0 && best_edge < 0.95f * best_face - 1e-9f) {
-    const V3 L = dot(eL, d) < 0.f ? -eL : eL;
-    V3 ca = G1.x, cb = G2.x;
+  S.best_face = best_face;
+  S.best_edge = best_edge;
+  S.face_axis = face_axis;
+  S.ei = ei;
+  S.ej = ej;
+  S.sep = sep;
+}
+DEV bool box_edge_contact(const BoxSat& S) { return S.ei >= 0 && S.best_edge < 0.95f * S.best_face - 1e-9f; }
+// edge-edge: one point at the midpoint of the closest points of the two edges
+template <class Sink>
+DEV void box_edge(Sink& cs, const Geom& G1, const Geom& G2, const BoxSat& S) {
+  const V3* A = S.A;
+  const V3* B = S.B;
+  const float* h1 = S.h1;
+  const float* h2 = S.h2;
+  const int ei = S.ei, ej = S.ej;
+  const V3 eL = normalize(cross(sel3(A[0], A[1], A[2], ei), sel3(B[0], B[1], B[2], ej)));
+  const V3 L = dot(eL, S.d) < 0.f ? -eL : eL;
+  V3 ca = G1.x, cb = G2.x;
 #pragma unroll
-    for (int k = 0; k < 3; k++) {
-      if (k != ei) ca = ca + A[k] * (dot(A[k], L) >= 0.f ? h1[k] : -h1[k]);
-      if (k != ej) cb = cb + B[k] * (dot(B[k], L) >= 0.f ? -h2[k] : h2[k]);
-    }
-    const V3 ua = sel3(A[0], A[1], A[2], ei), ub = sel3(B[0], B[1], B[2], ej), w = ca - cb;
-    const float bb = dot(ua, ub), dd = dot(ua, w), ee = dot(ub, w);
-    const float den = 1.f - bb * bb;
-    float ta = den > 1e-9f ? (bb * ee - dd) / den : 0.f;
-    float tb = den > 1e-9f ? (ee - bb * dd) / den : 0.f;
-    ta = fminf(fmaxf(ta, -h1[ei]), h1[ei]);
-    tb = fminf(fmaxf(tb, -h2[ej]), h2[ej]);
-    cs.add(G1.g, G2.g, -best_edge, ((ca + ua * ta) + (cb + ub * tb)) * 0.5f, L);
-    return;
+  for (int k = 0; k < 3; k++) {
+    if (k != ei) ca = ca + A[k] * (dot(A[k], L) >= 0.f ? h1[k] : -h1[k]);
+    if (k != ej) cb = cb + B[k] * (dot(B[k], L) >= 0.f ? -h2[k] : h2[k]);
   }
-  // face contact: every per-axis pick is a select over the three axes (no dynamically indexed
-  // private arrays -> no scratch); the polygons live in the caller's per-lane LDS buffers
-  const bool ref1 = face_axis < 3;
-  const int k = ref1 ? face_axis : face_axis - 3;
+  const V3 ua = sel3(A[0], A[1], A[2], ei), ub = sel3(B[0], B[1], B[2], ej), w = ca - cb;
+  const float bb = dot(ua, ub), dd = dot(ua, w), ee = dot(ub, w);
+  const float den = 1.f - bb * bb;
+  float ta = den > 1e-9f ? (bb * ee - dd) / den : 0.f;
+  float tb = den > 1e-9f ? (ee - bb * dd) / den : 0.f;
+  ta = fminf(fmaxf(ta, -self3(h1[0], h1[1], h1[2], ei)), self3(h1[0], h1[1], h1[2], ei));
+  tb = fminf(fmaxf(tb, -self3(h2[0], h2[1], h2[2], ej)), self3(h2[0], h2[1], h2[2], ej));
+  cs.add(G1.g, G2.g, -S.best_edge, ((ca + ua * ta) + (cb + ub * tb)) * 0.5f, L);
+}
+// face contact setup: the incident face's corners q[0..3] (in the clip order), the reference
+// face's centre cr, its normal nref (toward the incident box), its two side axes and half extents,
+// and the contact normal from geom 1 to geom 2.  Every per-axis pick is a select over the three
+// axes (no dynamically indexed private arrays -> no scratch).
+struct BoxFace {
+  V3 q[4], cr, nref, ax0, ax1, nout;
+  float hru, hrv;
+};
+DEV void box_face(const Geom& G1, const Geom& G2, const BoxSat& S, BoxFace& F) {
+  const V3* A = S.A;
+  const V3* B = S.B;
+  const float* h1 = S.h1;
+  const float* h2 = S.h2;
+  const bool ref1 = S.face_axis < 3;
+  const int k = ref1 ? S.face_axis : S.face_axis - 3;
   const V3 Rr0 = ref1 ? A[0] : B[0], Rr1 = ref1 ? A[1] : B[1], Rr2 = ref1 ? A[2] : B[2];
   const V3 Ri0 = ref1 ? B[0] : A[0], Ri1 = ref1 ? B[1] : A[1], Ri2 = ref1 ? B[2] : A[2];
   const float hr0 = ref1 ? h1[0] : h2[0], hr1 = ref1 ? h1[1] : h2[1], hr2 = ref1 ? h1[2] : h2[2];
@@ -263,43 +298,69 @@ DEV void box_box(Sink& cs, const Geom& G1, const Geom& G2, V3 hb1, V3 hb2, V3* p
   const int u = bj == 2 ? 0 : bj + 1, v = bj == 0 ? 2 : bj - 1;
   const V3 Ru = sel3(Ri0, Ri1, Ri2, u) * self3(hi0, hi1, hi2, u);
   const V3 Rv = sel3(Ri0, Ri1, Ri2, v) * self3(hi0, hi1, hi2, v);
-  const V3 q0 = ci + Ru + Rv, q1 = ci - Ru + Rv, q2 = ci - Ru - Rv, q3 = ci + Ru - Rv;
-  const V3 cr = pr + nref * self3(hr0, hr1, hr2, k);
+  F.q[0] = ci + Ru + Rv;
+  F.q[1] = ci - Ru + Rv;
+  F.q[2] = ci - Ru - Rv;
+  F.q[3] = ci + Ru - Rv;
+  F.cr = pr + nref * self3(hr0, hr1, hr2, k);
   const int ru = k == 2 ? 0 : k + 1, rv = k == 0 ? 2 : k - 1;
-  const V3 ax0 = sel3(Rr0, Rr1, Rr2, ru), ax1 = sel3(Rr0, Rr1, Rr2, rv);
-  const float hru = self3(hr0, hr1, hr2, ru), hrv = self3(hr0, hr1, hr2, rv);
-  const V3 nout = ref1 ? nref : -nref;
+  F.ax0 = sel3(Rr0, Rr1, Rr2, ru);
+  F.ax1 = sel3(Rr0, Rr1, Rr2, rv);
+  F.hru = self3(hr0, hr1, hr2, ru);
+  F.hrv = self3(hr0, hr1, hr2, rv);
+  F.nref = nref;
+  F.nout = ref1 ? nref : -nref;
+}
+
+// box-box, one pair per lane: 15-axis SAT; face contacts clip the incident face against the
+// reference face (<= 8 points), edge-edge contacts give one point at the midpoint of the closest
+// points.  poly, tmp: 8 V3 each of per-lane LDS scratch (a quad clipped by 4 half-planes has <= 8
+// corners).
+template <class Sink>
+DEV void box_box(Sink& cs, const Geom& G1, const Geom& G2, V3 hb1, V3 hb2, V3* poly, V3* tmp) {
+  CLK_DECL;
+  BoxSat S;
+  box_sat(G1, G2, hb1, hb2, S);
+  if (S.sep) return;
+  PROBEF(8, cs.E->stats, STAT_T_AUX0);
+  if (box_edge_contact(S)) {
+    box_edge(cs, G1, G2, S);
+    return;
+  }
+  BoxFace F;
+  box_face(G1, G2, S, F);
+  const V3 cr = F.cr, nref = F.nref, ax0 = F.ax0, ax1 = F.ax1, nout = F.nout;
+  const float hru = F.hru, hrv = F.hrv;
   {  // incident face entirely inside the reference face (a cube resting on a larger box): the
      // clip below would return the 4 corners unchanged, in order
     const float b0 = dot(ax0, cr) + hru, b1 = dot(-ax0, cr) + hru, b2 = dot(ax1, cr) + hrv, b3 = dot(-ax1, cr) + hrv;
-    const V3 qs[4] = {q0, q1, q2, q3};
     bool inside = true;
 #pragma unroll
     for (int c = 0; c < 4; c++)
-      inside = inside && dot(qs[c], ax0) - b0 <= 0.f && dot(qs[c], -ax0) - b1 <= 0.f && dot(qs[c], ax1) - b2 <= 0.f &&
-               dot(qs[c], -ax1) - b3 <= 0.f;
+      inside = inside && dot(F.q[c], ax0) - b0 <= 0.f && dot(F.q[c], -ax0) - b1 <= 0.f && dot(F.q[c], ax1) - b2 <= 0.f &&
+               dot(F.q[c], -ax1) - b3 <= 0.f;
     PROBEF(8, cs.E->stats, STAT_T_AUX1);
     if (inside) {
       float dep[4];
       int n = 0;
 #pragma unroll
       for (int c = 0; c < 4; c++) {
-        dep[c] = -dot(qs[c] - cr, nref);
+        dep[c] = -dot(F.q[c] - cr, nref);
         n += dep[c] >= 0.f ? 1 : 0;
       }
       int slot = cs.reserve(n);
 #pragma unroll
       for (int c = 0; c < 4; c++)
-        if (dep[c] >= 0.f) cs.put(slot++, G1.g, G2.g, -dep[c], qs[c] + nref * (0.5f * dep[c]), nout);
+        if (dep[c] >= 0.f) cs.put(slot++, G1.g, G2.g, -dep[c], F.q[c] + nref * (0.5f * dep[c]), nout);
       PROBEF(8, cs.E->stats, STAT_T_AUX2);
       return;
     }
   }
   int np = 4;
-  poly[0] = q0;
-  poly[1] = q1;
-  poly[2] = q2;
-  poly[3] = q3;
+  poly[0] = F.q[0];
+  poly[1] = F.q[1];
+  poly[2] = F.q[2];
+  poly[3] = F.q[3];
   np = clip_poly(poly, np, tmp, ax0, dot(ax0, cr) + hru);
   np = clip_poly(tmp, np, poly, -ax0, dot(-ax0, cr) + hru);
   np = clip_poly(poly, np, tmp, ax1, dot(ax1, cr) + hrv);
@@ -312,6 +373,121 @@ DEV void box_box(Sink& cs, const Geom& G1, const Geom& G2, V3 hb1, V3 hb2, V3* p
     const float depth = -dot(poly[c] - cr, nref);
     if (depth >= 0.f) cs.put(slot++, G1.g, G2.g, -depth, poly[c] + nref * (0.5f * depth), nout);
   }
+}
+
+// ---- lane-quad form: one pair per 4 consecutive lanes (a DPP quad), 16 pairs per wave pass
+template <int CTRL>
+DEV int qdpp_i(int v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+}
+// the quad's lanes where b holds, as bits 0..3
+DEV int qpop(unsigned m) { return (int)__popc(m); }
+DEV unsigned quad_bits(bool b) {
+  const unsigned long long m = __ballot(b);
+  return (unsigned)(m >> ((threadIdx.x & 63) & ~3)) & 0xFu;
+}
+// one pair on the lane quad (every lane of the quad calls it with the same pair): the SAT and the
+// face setup redundantly, then the incident corners one per lane ("inside" case) or the
+// Sutherland-Hodgman clip with polygon vertices ql and ql + 4 per lane and plane (quad prefix
+// counts keep the sequential vertex order, and every vertex and intersection is computed with the
+// sequential form's expression), contacts put with the keys and slots box_box gives them (the
+// same contact list, in the same order).  poly, tmp: 8 V3 each of the quad's LDS scratch.
+template <class Sink>
+DEV void box_box_quad(Sink& cs, const Geom& G1, const Geom& G2, V3 hb1, V3 hb2, V3* poly, V3* tmp) {
+  CLK_DECL;
+  const int ql = threadIdx.x & 3;
+  const unsigned below = (1u << ql) - 1u;
+  BoxSat S;
+  box_sat(G1, G2, hb1, hb2, S);
+  if (S.sep) return;  // (quad-uniform from here on: every lane has the same pair)
+  PROBEF(8, cs.E->stats, STAT_T_AUX0);
+  if (box_edge_contact(S)) {
+    if (ql == 0) box_edge(cs, G1, G2, S);
+    return;
+  }
+  BoxFace F;
+  box_face(G1, G2, S, F);
+  const V3 cr = F.cr, nref = F.nref, nout = F.nout;
+  const V3 pa[4] = {F.ax0, -F.ax0, F.ax1, -F.ax1};
+  const float pb[4] = {dot(F.ax0, cr) + F.hru, dot(-F.ax0, cr) + F.hru, dot(F.ax1, cr) + F.hrv, dot(-F.ax1, cr) + F.hrv};
+  const V3 qc = ql == 0 ? F.q[0] : (ql == 1 ? F.q[1] : (ql == 2 ? F.q[2] : F.q[3]));
+  const bool in_c = dot(qc, pa[0]) - pb[0] <= 0.f && dot(qc, pa[1]) - pb[1] <= 0.f && dot(qc, pa[2]) - pb[2] <= 0.f &&
+                    dot(qc, pa[3]) - pb[3] <= 0.f;
+  PROBEF(8, cs.E->stats, STAT_T_AUX1);
+  if (quad_bits(in_c) == 0xFu) {  // incident face inside the reference face: the 4 corners
+    const float dep = -dot(qc - cr, nref);
+    const unsigned km = quad_bits(dep >= 0.f);
+    int slot = ql == 0 ? cs.reserve(qpop(km)) : 0;
+    slot = qdpp_i<0x00>(slot);  // quad_perm [0,0,0,0]: lane 0's reservation
+    if (dep >= 0.f) {
+      const int rank = qpop(km & below);
+      cs.put_at(slot + rank, rank, G1.g, G2.g, -dep, qc + nref * (0.5f * dep), nout);
+    }
+    PROBEF(8, cs.E->stats, STAT_T_AUX2);
+    return;
+  }
+  // clip: 4 planes, the polygon in the quad's LDS scratch, vertex k in lane k & 3 (slot k >> 2)
+  poly[ql] = qc;
+  __builtin_amdgcn_wave_barrier();
+  int np = 4;
+  V3* src = poly;
+  V3* dst = tmp;
+#pragma unroll
+  for (int st = 0; st < 4; st++) {
+    V3 p[2], q[2];
+    float dp[2], dq[2];
+    bool keep[2], crs[2];
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int k = ql + 4 * h;
+      const bool have = k < np;
+      p[h] = src[have ? k : 0];
+      q[h] = src[have ? (k + 1 == np ? 0 : k + 1) : 0];
+      dp[h] = dot(p[h], pa[st]) - pb[st];
+      dq[h] = dot(q[h], pa[st]) - pb[st];
+      keep[h] = have && dp[h] <= 0.f;
+      crs[h] = have && ((dp[h] < 0.f && dq[h] > 0.f) || (dp[h] > 0.f && dq[h] < 0.f));
+    }
+    const unsigned k0 = quad_bits(keep[0]), c0 = quad_bits(crs[0]), k1 = quad_bits(keep[1]), c1 = quad_bits(crs[1]);
+    const int tot0 = qpop(k0) + qpop(c0);
+    int pos[2] = {qpop(k0 & below) + qpop(c0 & below), tot0 + qpop(k1 & below) + qpop(c1 & below)};
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      if (keep[h]) dst[pos[h]] = p[h];
+      if (crs[h]) {
+        const float t = dp[h] / (dp[h] - dq[h]);
+        dst[pos[h] + (keep[h] ? 1 : 0)] = p[h] + (q[h] - p[h]) * t;
+      }
+    }
+    np = tot0 + qpop(k1) + qpop(c1);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    V3* sw = src;
+    src = dst;
+    dst = sw;
+  }
+  PROBEF(8, cs.E->stats, STAT_T_AUX3);
+  float dep[2];
+  bool kv[2];
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+    const int k = ql + 4 * h;
+    dep[h] = k < np ? -dot(src[k] - cr, nref) : -1.f;
+    kv[h] = k < np && dep[h] >= 0.f;
+  }
+  const unsigned m0 = quad_bits(kv[0]), m1 = quad_bits(kv[1]);
+  int slot = ql == 0 ? cs.reserve(qpop(m0) + qpop(m1)) : 0;
+  slot = qdpp_i<0x00>(slot);
+  const int r[2] = {qpop(m0 & below), qpop(m0) + qpop(m1 & below)};
+#pragma unroll
+  for (int h = 0; h < 2; h++)
+    if (kv[h]) {
+      const int k = ql + 4 * h;
+      cs.put_at(slot + r[h], r[h], G1.g, G2.g, -dep[h], src[k] + nref * (0.5f * dep[h]), nout);
+    }
 }
 
 // ---------------------------------------------------------------- GJK + EPA (wave-cooperative)

@@ -126,6 +126,9 @@ static __shared__ EnvSh g_E;
 // dynamics beside the collision prune, which only touches [0, COL_WORK)) and the observation of
 // the step end.  The Newton Hessian staging tile and Cholesky transpose live in E.con instead
 // (contacts are dead once the rows exist; the last substep stores them to HBM first).
+#ifndef MMX_BOXBOX_QUAD  // box-box narrowphase on lane quads (1) or one pair per lane (0)
+#define MMX_BOXBOX_QUAD 1
+#endif
 #define COL_GX 0      // [NGEOM][GXS] world pose (x3, R9), rbound, type, -, -, box half extents (3), -
 #define GXS 20
 #define COL_CAND 944  // [COL_LIST] candidate pairs after the sphere test, then grouped by class
@@ -672,7 +675,9 @@ struct WaveSink {
   bool ro;
   float mu0, mu1, mu2, dim;
   int bodies;  // geom bodies packed above the 16-bit order key: b1 << 16 | b2 << 24
+  int key0;
   DEV WaveSink(EnvSh* e, int p, bool st, int g1, int g2) : E(e), key(p * 8), store(st) {
+    key0 = p * 8;
     bodies = (MMX_geom_body[g1] << 16) | (MMX_geom_body[g2] << 24);
     const int c1 = MMX_geom_class[g1], c2 = MMX_geom_class[g2];
     ro = (c1 == 1 && c2 == 2) || (c1 == 2 && c2 == 1);
@@ -682,6 +687,13 @@ struct WaveSink {
     dim = (float)max(MMX_geom_condim[g1], MMX_geom_condim[g2]);
   }
   DEV void add(int g1, int g2, float dist, V3 pos, V3 nrm) { put(reserve(1), g1, g2, dist, pos, nrm); }
+  // contact `order` of the pair (its key = pair * 8 + order, as the sequential put would give it)
+  // into a reserved slot: the lane-group form of the box-box narrowphase puts a pair's contacts
+  // from several lanes at once
+  DEV void put_at(int slot, int order, int g1, int g2, float dist, V3 pos, V3 nrm) {
+    key = key0 + order;
+    put(slot, g1, g2, dist, pos, nrm);
+  }
   // n consecutive contact slots with one LDS atomic (a pair's corners / clipped points are
   // counted first, then reserved together); returns the first slot, MMX_MAXCON when none is kept
   DEV int reserve(int n) {
@@ -938,6 +950,21 @@ DEV void collide_pairs(EnvSh& E, bool only_ro, int which) {
     }
     SYNC();
     PROBE(5, stats, STAT_T_AUX0);
+#if MMX_BOXBOX_QUAD
+    // box-box, one pair per lane quad (16 pairs per pass): the clip's vertices split over the quad
+    V3* poly = reinterpret_cast<V3*>(scr + COL_WORK + COL_POLY * (LANE >> 2));
+    for (int k0 = 0; k0 < n1; k0 += WG / 4) {
+      const int k = k0 + (LANE >> 2);
+      if (k < n1) {
+        const int p = cand[n0 + k];
+        int g1, g2;
+        pair_geoms(gx, p, g1, g2);
+        const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
+        WaveSink cs(&E, p, !only_ro, g1, g2);
+        box_box_quad(cs, A, B, geom_half(gx, g1), geom_half(gx, g2), poly, poly + 8);
+      }
+    }
+#else
     V3* poly = reinterpret_cast<V3*>(scr + COL_WORK + COL_POLY * min(LANE, COL_PLANES - 1));
     for (int k0 = 0; k0 < n1; k0 += COL_PLANES) {  // box-box
       const int k = k0 + LANE;
@@ -950,6 +977,7 @@ DEV void collide_pairs(EnvSh& E, bool only_ro, int which) {
         box_box(cs, A, B, geom_half(gx, g1), geom_half(gx, g2), poly, poly + 8);
       }
     }
+#endif
     SYNC();
     PROBE(5, stats, STAT_T_AUX1);
   }

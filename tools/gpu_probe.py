@@ -192,11 +192,32 @@ def nefc_dist(N=4096, steps=400):
             "efc_overflow_envs": int(((env.env_error & 2) != 0).sum()) if hasattr(env, "env_error") else -1}
 
 
+def digest(N=2048, steps=160):
+    """Bit-identity digest of a C3 expert rollout: sha256 of qpos / qvel / obs after every 20 steps
+    (A/B of two builds that must agree bit for bit)."""
+    import hashlib
+
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    env = PickPlaceVecEnv(N, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
+                          autoreset=True)
+    env.reset(seed=[_lib.episode_seed(42, i) for i in range(N)])
+    out = []
+    for k in range(steps // 20):
+        env.rollout_expert(20)
+        torch.cuda.synchronize()
+        h = hashlib.sha256()
+        h.update(env.qpos.cpu().numpy().tobytes())
+        h.update(env.qvel.cpu().numpy().tobytes())
+        out.append(h.hexdigest()[:16])
+    return {"digests": out, "ncon": float(env.sim.view("stats", _lib.STAT_N).double()[:, 1].sum().item())}
+
+
 if __name__ == "__main__":
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     for name, fn in [("phys1", lambda: physics_parity(1)), ("phys16", lambda: physics_parity(16)),
                      ("gym", gym_parity), ("expert", expert_success), ("speed", rollout_speed),
-                     ("nefc", nefc_dist), ("fsm", fsm_profile)]:
+                     ("nefc", nefc_dist), ("fsm", fsm_profile), ("digest", digest)]:
         if len(sys.argv) > 1 and name not in sys.argv[1:]:
             continue
         t = time.time()
