@@ -391,7 +391,8 @@ DEV unsigned quad_bits(bool b) {
 // Sutherland-Hodgman clip with polygon vertices ql and ql + 4 per lane and plane (quad prefix
 // counts keep the sequential vertex order, and every vertex and intersection is computed with the
 // sequential form's expression), contacts put with the keys and slots box_box gives them (the
-// same contact list, in the same order).  poly, tmp: 8 V3 each of the quad's LDS scratch.
+// same contact list in the same order; tools/contact_ab.py: positions and depths bit-identical,
+// normals within 1 ulp).  poly, tmp: 8 V3 each of the quad's LDS scratch.
 template <class Sink>
 DEV void box_box_quad(Sink& cs, const Geom& G1, const Geom& G2, V3 hb1, V3 hb2, V3* poly, V3* tmp) {
   CLK_DECL;

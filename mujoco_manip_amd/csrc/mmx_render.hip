@@ -77,7 +77,12 @@ static constexpr int kBigCache = MMR_BIG_CACHE;  // per band; a full queue sends
 #define MMR_BPW 2
 #endif
 static constexpr int kBPW = MMR_BPW;  // bands per workgroup: vertex and triangle setup shared by them
-static_assert(kBPW >= 1 && kBPW <= 4, "nbig holds 2 counters per band");
+static_assert(kBPW >= 1 && kBPW <= 4, "nbig holds 3 counters per band");
+#ifndef MMR_TINY
+#define MMR_TINY 64  // small boxes up to this many pixels queue from the front, the others from the back
+#endif
+static constexpr int kTiny = MMR_TINY;  // (a wave's 8-lane groups then walk boxes of similar size)
+static constexpr int kNbig = 12;        // [2 kb]: large, [2 kb + 1]: small (front), [8 + kb]: small (back)
 #ifndef MMR_TPW
 #define MMR_TPW 2
 #endif
@@ -126,11 +131,14 @@ DEV void rend_edge_plane(float xa, float ya, int ia, float xb, float yb, int ib,
 // out of a column walk without changing a bit)
 DEV float rend_edge_x(const RTri& T, int k, float x) { return fmaf(T.A[k], x, T.C[k]); }
 DEV float rend_edge_at(const RTri& T, int k, float x, float y) { return fmaf(T.B[k], y, rend_edge_x(T, k, x)); }
+// depth key from the scaled inverse depth q of a covered pixel
+DEV uint32_t rend_key_q(int t, float q) {
+  const uint32_t d = 1u + (uint32_t)(fminf(fmaxf(q, 0.f), 1.f) * 1048574.f);  // 1 .. 2^20 - 1 (0 = empty)
+  return (d << 12) | (uint32_t)t;
+}
 // depth key from the edge values of a covered pixel
 DEV uint32_t rend_key(const RTri& T, int t, float e0, float e1, float e2, float q0) {
-  const float q = fminf(fmaxf(fmaf(e0, T.w[0], fmaf(e1, T.w[1], fmaf(e2, T.w[2], q0))), 0.f), 1.f);
-  const uint32_t d = 1u + (uint32_t)(q * 1048574.f);  // 1 .. 2^20 - 1 (0 = empty)
-  return (d << 12) | (uint32_t)t;
+  return rend_key_q(t, fmaf(e0, T.w[0], fmaf(e1, T.w[1], fmaf(e2, T.w[2], q0))));
 }
 
 // camera-space vertex -> screen (sx, sy, 1 / depth, 1) or (0, 0, 0, 0) behind the near plane
@@ -184,63 +192,57 @@ DEV uint32_t rend_cover(const RTri& T, int t, int px, int py, float q0) {
   return rend_key(T, t, e0, e1, e2, q0);
 }
 
-// shading of 4 horizontally adjacent pixels (px .. px + 3, py) from their depth keys: flat face
-// light and material from tinfo / mrgb, the floor's checker where no triangle covers the pixel and
-// its ray meets the floor, the sky gradient elsewhere; RGB u8 (3 dwords) and segment ids (1 dword)
-DEV void shade4(const uint32_t* keys, int px0, int py, int Sz, float half, float f, const M3& cR, const V3& cx,
-                const V3& l_top, const V3& lp_cam, const uint32_t* tinfo, const float* mrgb, uint32_t* rgb_out,
-                uint32_t* seg_out, int nvalid) {
-  {
-    uint32_t rgbw[3] = {0u, 0u, 0u}, segw = 0u;
-    for (int u = 0; u < 4; u++) {
-      const int px = px0 + u;
-      const uint32_t key = keys[u];
-      const V3 dw = mul(cR, V3{(px + 0.5f - half) / f, -(py + 0.5f - half) / f, -1.f});  // world ray
-      float col[3];
-      int sid = 0;
-      const float s0 = -cx.z / dw.z;  // ray parameter at the floor plane z = 0
-      const float fx = cx.x + s0 * dw.x, fy = cx.y + s0 * dw.y;
-      if (key == 0u && dw.z < 0.f && fabsf(fx) <= MMR_FLOOR_HALF && fabsf(fy) <= MMR_FLOOR_HALF) {
-        // floor: checker (0.1 m squares) under the same lights as a face, evaluated per pixel
-        const float* mt = mrgb + 8 * MMR_FLOOR_MAT;
-        const V3 pc = mulT(cR, V3{fx, fy, 0.f} - cx);  // camera frame; the normal is l_top
-        const float light = fminf(0.3f + 0.6f * fmaxf(l_top.z, 0.f) + 0.8f +
-                                  0.4f * fmaxf(dot(l_top, normalize(lp_cam - pc)), 0.f), 3.99f);
-        sid = (int)mt[7];
-        const bool alt = ((int)floorf(fx / mt[6]) + (int)floorf(fy / mt[6])) & 1;
-        for (int k = 0; k < 3; k++) col[k] = fminf((alt ? mt[3 + k] : mt[k]) * light, 1.f);
-      } else if (key == 0u) {  // skybox gradient (rgb1 top -> rgb2 bottom, scene.xml:17-18)
-        const float sky = 0.5f * (dw.z * rsqrtf(dot(dw, dw)) + 1.f);
-        col[0] = 0.3f * sky; col[1] = 0.5f * sky; col[2] = 0.7f * sky;
-      } else {
-        const uint32_t ti = tinfo[key & 4095];
-        const float* mt = mrgb + 8 * (ti & 255);
-        const float light = (float)(ti >> 16) * (1.f / 16384.f);
-        sid = (int)mt[7];
-        bool alt = false;
-        if (mt[6] > 0.f) {  // floor checker: the ray meets the plane z = 0
-          const float s0 = -cx.z / dw.z;
-          alt = ((int)floorf((cx.x + s0 * dw.x) / mt[6]) + (int)floorf((cx.y + s0 * dw.y) / mt[6])) & 1;
-        }
-        for (int k = 0; k < 3; k++) col[k] = fminf((alt ? mt[3 + k] : mt[k]) * light, 1.f);
-      }
-      for (int k = 0; k < 3; k++) {
-        const uint32_t v8 = (uint32_t)(col[k] * 255.f + 0.5f);
-        const int byte = 3 * u + k;
-        rgbw[byte >> 2] |= v8 << (8 * (byte & 3));
-      }
-      segw |= (uint32_t)sid << (8 * u);
+// RGB8 of a colour in [0, 1]^3 (rounded) and a segment id, packed r | g << 8 | b << 16 | seg << 24
+DEV uint32_t rend_pack(float r, float g, float b, uint32_t sid) {
+  return (uint32_t)(r * 255.f + 0.5f) | ((uint32_t)(g * 255.f + 0.5f) << 8) | ((uint32_t)(b * 255.f + 0.5f) << 16) |
+         (sid << 24);
+}
+// shading of 4 horizontally adjacent pixels (px .. px + 3, py) from their depth keys: a covered
+// pixel takes its triangle's packed colour (tinfo: flat face light x material, set up once per
+// triangle), an uncovered one the floor's checker where its ray meets the floor (per pixel: the
+// floor's normal is world z, so its headlight / directional terms are constants of the camera and
+// the point light's cosine is 1.5 / |(0.5, 0.5, 1.5) - p|), the sky gradient elsewhere; RGB u8
+// (3 dwords) and segment ids (1 dword)
+DEV void shade4(const uint32_t* keys, int px0, int py, float half, float f, const M3& cR, const V3& cx,
+                float floor_light0, const uint32_t* tinfo, const float* mrgb, uint32_t* rgb_out, uint32_t* seg_out,
+                int nvalid) {
+  uint32_t pix[4];
+  // world ray of the first pixel; the next ones step by the camera's x axis / f
+  const float rf = 1.f / f;
+  const V3 dx = col(cR, 0) * rf;
+  V3 dw = mul(cR, V3{(px0 + 0.5f - half) * rf, -(py + 0.5f - half) * rf, -1.f});
+  for (int u = 0; u < 4; u++, dw = dw + dx) {
+    const uint32_t key = keys[u];
+    if (key != 0u) {
+      pix[u] = tinfo[key & 4095];
+      continue;
     }
-    if (nvalid == 4) {  // the image side is a multiple of 16: 4 whole pixels, dword-aligned
-      rgb_out[0] = rgbw[0]; rgb_out[1] = rgbw[1]; rgb_out[2] = rgbw[2];
-      seg_out[0] = segw;
-    } else {  // other sides: byte stores of the pixels inside the image
-      unsigned char* rb = reinterpret_cast<unsigned char*>(rgb_out);
-      unsigned char* sb = reinterpret_cast<unsigned char*>(seg_out);
-      for (int u = 0; u < nvalid; u++) {
-        for (int k = 0; k < 3; k++) rb[3 * u + k] = (unsigned char)(rgbw[(3 * u + k) >> 2] >> (8 * ((3 * u + k) & 3)));
-        sb[u] = (unsigned char)(segw >> (8 * u));
-      }
+    const float s0 = -cx.z / dw.z;  // ray parameter at the floor plane z = 0
+    const float fx = cx.x + s0 * dw.x, fy = cx.y + s0 * dw.y;
+    if (dw.z < 0.f && fabsf(fx) <= MMR_FLOOR_HALF && fabsf(fy) <= MMR_FLOOR_HALF) {
+      const float* mt = mrgb + 8 * MMR_FLOOR_MAT;  // checker (0.1 m squares) under the face lights
+      const float ddx = 0.5f - fx, ddy = 0.5f - fy;
+      const float light = fminf(floor_light0 + 0.6f * rsqrtf(fmaf(ddx, ddx, fmaf(ddy, ddy, 2.25f))), 3.99f);
+      const bool alt = ((int)floorf(fx / mt[6]) + (int)floorf(fy / mt[6])) & 1;
+      const float* c = alt ? mt + 3 : mt;
+      pix[u] = rend_pack(fminf(c[0] * light, 1.f), fminf(c[1] * light, 1.f), fminf(c[2] * light, 1.f), (uint32_t)mt[7]);
+    } else {  // skybox gradient (rgb1 top -> rgb2 bottom, scene.xml:17-18)
+      const float sky = 0.5f * (dw.z * rsqrtf(dot(dw, dw)) + 1.f);
+      pix[u] = rend_pack(0.3f * sky, 0.5f * sky, 0.7f * sky, 0u);
+    }
+  }
+  const uint32_t rgbw[3] = {(pix[0] & 0xFFFFFFu) | (pix[1] << 24), ((pix[1] >> 8) & 0xFFFFu) | (pix[2] << 16),
+                            ((pix[2] >> 16) & 0xFFu) | (pix[3] << 8)};
+  const uint32_t segw = (pix[0] >> 24) | ((pix[1] >> 24) << 8) | ((pix[2] >> 24) << 16) | (pix[3] & 0xFF000000u);
+  if (nvalid == 4) {  // the image side is a multiple of 16: 4 whole pixels, dword-aligned
+    rgb_out[0] = rgbw[0]; rgb_out[1] = rgbw[1]; rgb_out[2] = rgbw[2];
+    seg_out[0] = segw;
+  } else {  // other sides: byte stores of the pixels inside the image
+    unsigned char* rb = reinterpret_cast<unsigned char*>(rgb_out);
+    unsigned char* sb = reinterpret_cast<unsigned char*>(seg_out);
+    for (int u = 0; u < nvalid; u++) {
+      for (int k = 0; k < 3; k++) rb[3 * u + k] = (unsigned char)(rgbw[(3 * u + k) >> 2] >> (8 * ((3 * u + k) & 3)));
+      sb[u] = (unsigned char)(segw >> (8 * u));
     }
   }
 }
@@ -252,8 +254,8 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
   float* bpose = reinterpret_cast<float*>(vs + MMR_NVERT);                        // [19][12]
   uint32_t* zb = reinterpret_cast<uint32_t*>(bpose + 19 * 12);                    // [rows][Zs]
   unsigned short* bigq = reinterpret_cast<unsigned short*>(zb + kZbWords);        // [kBPW][kMaxBig]
-  int* nbig = reinterpret_cast<int*>(bigq + kBPW * kMaxBig);                      // [8]: large, small per band
-  float* cam = reinterpret_cast<float*>(nbig + 8);                                // R (9), p (3)
+  int* nbig = reinterpret_cast<int*>(bigq + kBPW * kMaxBig);                      // [kNbig] queue counters
+  float* cam = reinterpret_cast<float*>(nbig + kNbig);                            // R (9), p (3)
   uint32_t* tinfo = reinterpret_cast<uint32_t*>(cam + 12);                        // [MMR_NTRI]
   float* mrgb = reinterpret_cast<float*>(tinfo + MMR_NTRI);                       // [MMR_NMAT][8]
   unsigned short* smallq = reinterpret_cast<unsigned short*>(mrgb + 8 * MMR_NMAT); // [kBPW][MMR_NTRI]
@@ -286,7 +288,7 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
       for (int k = 0; k < 3; k++) o[9 + k] = b == 0 ? 0.f : MMX_body_pos[3 * b + k];
     }
   }
-  if (tid < 8) nbig[tid] = 0;
+  if (tid < kNbig) nbig[tid] = 0;
   if (tid == 32) {
     const int c = ci == 0 ? MMX_CAM_OVERHEAD : MMX_CAM_WRIST;
     const M3 lq = qmat(Q4{MMX_cam_quat[4 * c], MMX_cam_quat[4 * c + 1], MMX_cam_quat[4 * c + 2], MMX_cam_quat[4 * c + 3]});
@@ -336,6 +338,7 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
   const float iz_lo = 1.f / zfar, iz_scale = 1.f / (1.f / znear - 1.f / zfar), q0 = -iz_lo * iz_scale;
   const V3 l_top = mulT(cR, V3{0.f, 0.f, 1.f});  // toward the directional light (dir 0 0 -1)
   const V3 lp_cam = mulT(cR, V3{0.5f, 0.5f, 1.5f} - cx);
+  const float floor_light0 = 0.3f + 0.6f * fmaxf(l_top.z, 0.f) + 0.8f;  // the floor's headlight + directional
   // the floor's triangles [0, MMR_FLOOR_TRIS) are not rasterised: it lies below everything, so a
   // pixel no triangle covers shows the floor where its ray meets z = 0 inside the plane, else sky
   // Each triangle is set up once for the workgroup's rows (cull, box, face light) and queued per
@@ -352,7 +355,11 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
       const V3 pc = V3{(a.x + b.x + cc.x) * (1.f / 3.f), (a.y + b.y + cc.y) * (1.f / 3.f), (a.z + b.z + cc.z) * (1.f / 3.f)};
       const float light = 0.3f + 0.6f * fmaxf(n.z, 0.f) + 0.8f * fmaxf(dot(n, l_top), 0.f) +
                           0.4f * fmaxf(dot(n, normalize(lp_cam - pc)), 0.f);
-      tinfo[t] = ((uint32_t)(fminf(light, 3.99f) * 16384.f) << 16) | MMR_tri_mat[t];
+      // the face's packed colour (light in steps of 2^-14; no rasterised material has a checker:
+      // the floor, the only one, is shaded per pixel, tools/compile_render.py)
+      const float lq = (float)(uint32_t)(fminf(light, 3.99f) * 16384.f) * (1.f / 16384.f);
+      const float* mt = mrgb + 8 * MMR_tri_mat[t];
+      tinfo[t] = rend_pack(fminf(mt[0] * lq, 1.f), fminf(mt[1] * lq, 1.f), fminf(mt[2] * lq, 1.f), (uint32_t)mt[7]);
     }
     for (int kb = 0; kb < kBPW; kb++) {
       const int r0 = rowA + kb * rows;
@@ -361,7 +368,8 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
       const int area = (T.bx1 - T.bx0 + 1) * (by1 - by0 + 1);
       int k = area > kSmallArea ? atomicAdd(nbig + 2 * kb, 1) : kMaxBig;
       if (k < kMaxBig) bigq[kb * kMaxBig + k] = (unsigned short)t;
-      else smallq[kb * MMR_NTRI + atomicAdd(nbig + 2 * kb + 1, 1)] = (unsigned short)t;
+      else if (area <= kTiny) smallq[kb * MMR_NTRI + atomicAdd(nbig + 2 * kb + 1, 1)] = (unsigned short)t;
+      else smallq[kb * MMR_NTRI + MMR_NTRI - 1 - atomicAdd(nbig + 8 + kb, 1)] = (unsigned short)t;
     }
   }
   const int tcols = Sg >> 4;
@@ -382,24 +390,28 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
   for (int q = tid; q < min((MMR_SKIP & 2) ? 0 : nbig[2 * kb], kBigCache); q += RWG)
     rend_setup(vs, bigq[kb * kMaxBig + q], Sz, row0, row1, iz_scale, bigs[q]);
   {  // small triangles: one per 8-lane group, walked column by column
-    const int ns = (MMR_SKIP & 1) ? 0 : nbig[2 * kb + 1];
+    const int nsf = nbig[2 * kb + 1], ns = (MMR_SKIP & 1) ? 0 : nsf + nbig[8 + kb];
+    // queue entry q: the tiny boxes [0, nsf) from the front, then the others from the back
+    const unsigned short* sq = smallq + kb * MMR_NTRI;
+    auto sq_at = [&](int q) { return (int)sq[q < nsf ? q : MMR_NTRI - 1 - (q - nsf)]; };
     const int grp = tid / kGroup, gl = tid % kGroup;
     // one triangle ahead: the next triangle's vertex ids (table loads) are in flight while this
     // one is scanned
-    int tn = grp < ns ? smallq[kb * MMR_NTRI + grp] : MMR_FLOOR_TRIS;
+    int tn = grp < ns ? sq_at(grp) : MMR_FLOOR_TRIS;
     int an = MMR_tri[3 * tn], bn = MMR_tri[3 * tn + 1], cn = MMR_tri[3 * tn + 2];
     for (int q = grp; q < ns; q += RWG / kGroup) {
       int t = tn;
       const int a = an, b = bn, c = cn;
       if (MMR_PF && q + RWG / kGroup < ns) {
-        tn = smallq[kb * MMR_NTRI + q + RWG / kGroup];
+        tn = sq_at(q + RWG / kGroup);
         an = MMR_tri[3 * tn]; bn = MMR_tri[3 * tn + 1]; cn = MMR_tri[3 * tn + 2];
       }
       RTri T;
       if (MMR_PF) rend_setup_abc(vs, a, b, c, Sz, row0, row1, iz_scale, T);
-      else rend_setup(vs, t = smallq[kb * MMR_NTRI + q], Sz, row0, row1, iz_scale, T);
+      else rend_setup(vs, t = sq_at(q), Sz, row0, row1, iz_scale, T);
       const int w = T.bx1 - T.bx0 + 1;
       const float rw = 1.f / (float)w;
+      const float qB = fmaf(T.B[0], T.w[0], fmaf(T.B[1], T.w[1], T.B[2] * T.w[2]));  // dq / dy
 #ifdef MMR_CLOCK_STATS  // (global atomics: distorts the MMR_CLOCK times)
       if (gl == 0) {
         atomicAdd(&g_rclk[6], 1ull);
@@ -439,11 +451,14 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
 #else
           const int pylo = T.by0, pyhi = T.by1;
 #endif
+          // q is affine in y along the column: q = qB y + qx (one FMA per pixel)
+          const float qx = fmaf(ex0, T.w[0], fmaf(ex1, T.w[1], fmaf(ex2, T.w[2], q0)));
           uint32_t* zc = zb + (pylo + rph - row0) * Zs + px;
-          for (int py = pylo + rph; py <= pyhi; py += rstep, zc += rstep * Zs) {
-            const float y = py + 0.5f;
+          const float ystep = (float)rstep;
+          float y = (float)(pylo + rph) + 0.5f;
+          for (int py = pylo + rph; py <= pyhi; py += rstep, zc += rstep * Zs, y += ystep) {
             const float e0 = fmaf(T.B[0], y, ex0), e1 = fmaf(T.B[1], y, ex1), e2 = fmaf(T.B[2], y, ex2);
-            if (fmaxf(e0, fmaxf(e1, e2)) <= 0.f) atomicMax(zc, rend_key(T, t, e0, e1, e2, q0));
+            if (fmaxf(e0, fmaxf(e1, e2)) <= 0.f) atomicMax(zc, rend_key_q(t, fmaf(qB, y, qx)));
           }
         }
       }
@@ -509,7 +524,7 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
       const int nvalid = whole ? 4 : min(4, Sz - (tx[j] + lx));
       if (nvalid <= 0) continue;
       const size_t p0 = (size_t)py * Sz + tx[j] + lx;  // image pixel of the lane's first pixel
-      shade4(best[j], tx[j] + lx, py, Sz, half, f, cR, cx, l_top, lp_cam, tinfo, mrgb,
+      shade4(best[j], tx[j] + lx, py, half, f, cR, cx, floor_light0, tinfo, mrgb,
              reinterpret_cast<uint32_t*>(img + 3 * p0), reinterpret_cast<uint32_t*>(seg + p0), nvalid);
     }
   }
@@ -529,13 +544,13 @@ extern "C" hipError_t mmx_render_clock(unsigned long long* out, int reset) {
 #endif
 
 static_assert(sizeof(float4) * MMR_NVERT + sizeof(float) * 19 * 12 + sizeof(uint32_t) * kZbWords +
-                  sizeof(unsigned short) * kBPW * kMaxBig + 8 * sizeof(int) + 12 * sizeof(float) +
+                  sizeof(unsigned short) * kBPW * kMaxBig + kNbig * sizeof(int) + 12 * sizeof(float) +
                   sizeof(uint32_t) * MMR_NTRI + sizeof(float) * 8 * MMR_NMAT + sizeof(unsigned short) * kBPW * MMR_NTRI +
                   sizeof(RTri) * kBigCache <= 80 * 1024,
               "render model too large for two workgroups per CU (LDS)");
 extern "C" size_t mmx_render_lds_bytes() {
   return sizeof(float4) * MMR_NVERT + sizeof(float) * 19 * 12 + sizeof(uint32_t) * kZbWords +
-         sizeof(unsigned short) * kBPW * kMaxBig + 8 * sizeof(int) + 12 * sizeof(float) + sizeof(uint32_t) * MMR_NTRI +
+         sizeof(unsigned short) * kBPW * kMaxBig + kNbig * sizeof(int) + 12 * sizeof(float) + sizeof(uint32_t) * MMR_NTRI +
          sizeof(float) * 8 * MMR_NMAT + sizeof(unsigned short) * kBPW * MMR_NTRI + sizeof(RTri) * kBigCache;
 }
 

@@ -275,6 +275,9 @@ def emit(rm, path):
     vbody = [b for b, k in zip(rm["vert_body"], vkeep) if k]
     dtris = vmap[tris[tkeep]].tolist()
     dmat = [m for m, k in zip(rm["tri_mat"], tkeep) if k]
+    # the kernel packs each rasterised face's colour once (flat light x material): a checker
+    # material among the device triangles would need per-pixel shading
+    assert all(rm["materials"][m]["checker"] == 0.0 for m in set(dmat)), "checker material on a rasterised face"
     nv, nt, nm = len(verts), len(dtris), len(rm["materials"])
     L.append(f"#define MMR_NVERT {nv}\n#define MMR_NTRI {nt}\n#define MMR_NMAT {nm}\n")
     L.append(f"#define MMR_FLOOR_TRIS 0\n#define MMR_FLOOR_HALF {FLOOR_HALF!r}f\n#define MMR_FLOOR_MAT 0\n\n")
