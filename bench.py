@@ -357,6 +357,21 @@ def main():
                         "rank_kernel_ms": rank_kern_ms, "solver": solver,
                         "episodes": {"completed": int(eps[0]), "successes": int(eps[1]), "placed": int(eps[2]),
                                      "error_resets": int(eps[3]), "envs_with_error_now": int(errs_now)}})
+    isolated = None
+    if args.image_size:
+        # the render kernel on its own (no step kernels beside it): mmx_forward over the resident
+        # states = the position stage (~0.04 ms for 8192 envs) + one render launch over all N envs
+        env.sim.forward()
+        torch.cuda.synchronize()
+        reps = 10
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            env.sim.forward()
+        torch.cuda.synchronize()
+        fwd_ms = (time.perf_counter() - t1) / reps * 1e3
+        isolated = {"forward_ms": fwd_ms, "envs": N,
+                    "pixels_per_s": N * 2 * args.image_size ** 2 / (fwd_ms * 1e-3),
+                    "note": "mmx_forward (position stage + render of all envs, both cameras) alone on the GPU"}
     values = [args.steps * N * world / w["elapsed"] for w in windows]
     med = windows[int(np.argsort(values)[len(values) // 2])]
     value = args.steps * N * world / med["elapsed"]
@@ -386,7 +401,7 @@ def main():
                   "bound": "valu", "hbm_achieved_GBs": r_achieved, "hbm_frac": r_achieved / HBM_PEAK_GBS,
                   "share_of_kernel_time": med["render_ms"] / (med["render_ms"] + kern_ms),
                   "pixels_per_s": lanes * envs_per_launch * 2 * S * S / (med["render_ms"] * 1e-3),
-                  "valu": None if rpmc is None else rpmc.get("valu"),
+                  "valu": None if rpmc is None else rpmc.get("valu"), "isolated": isolated,
                   "note": "HBM is not the render kernel's roof (it writes 4 B per pixel); VALU issue is "
                           "(valu: SQ counters of tools/render_pmc.sh for this configuration)"}
     if rank == 0:

@@ -23,6 +23,10 @@ def main():
         for r in csv.DictReader(open(f, newline="")):
             if "mmx_render_kernel" not in r.get("Kernel_Name", ""):
                 continue
+            # the bench's per-step launches only (2048 envs x 2 cameras x 512 lanes); its isolated
+            # render timing (mmx_forward over all 8192 envs) launches 4x larger grids
+            if int(r.get("Grid_Size") or 0) != a.wg_per_dispatch * 512:
+                continue
             d = (pas, int(r.get("Dispatch_Id") or r.get("Correlation_Id")))
             per.setdefault(d, {}).setdefault(r["Counter_Name"], 0.0)
             per[d][r["Counter_Name"]] += float(r["Counter_Value"])
