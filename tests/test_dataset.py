@@ -183,6 +183,59 @@ def test_writer_splits_data_files(tmp_path):
         np.testing.assert_array_equal(frames[ep.index]["observation.state"], ep.frames["observation.state"])
 
 
+def test_threaded_writer_matches_inline_and_keeps_png_uncompressed(tmp_path):
+    """The background-thread writer (generate()'s) writes the same dataset as the inline one; PNG
+    bytes take no dictionary encoding and the requested compression (here NONE), numeric columns
+    keep snappy."""
+    import pyarrow.parquet as pq
+
+    rng = np.random.default_rng(3)
+    feats = {k: v for k, v in D.FEATURES.items() if k in ("observation.state", "action.joint_pos")}
+    feats.update({k: dict(D.FEATURES[k], shape=(8, 8, 3)) for k in D.IMAGE_KEYS})
+    eps = _synthetic_episodes(rng, feats, n_eps=5)
+    out = {}
+    for mode in (False, True):
+        root = str(tmp_path / f"ds{int(mode)}")
+        w = D.LeRobotWriter(root, "u/ds", feats, threaded=mode, image_compression="NONE" if mode else "SNAPPY")
+        for ep in eps:
+            w.add_episode(ep)
+        info = w.close()
+        out[mode] = (info, D.read_lerobot_v3(root)[2], root)
+    assert out[False][0] == out[True][0]
+    for ep in eps:
+        a, b = out[False][1][ep.index], out[True][1][ep.index]
+        assert set(a) == set(b)
+        for k in a:
+            if isinstance(a[k], np.ndarray):
+                np.testing.assert_array_equal(a[k], b[k])
+            else:
+                assert a[k] == b[k]
+        for k in D.IMAGE_KEYS:  # (read back decoded)
+            np.testing.assert_array_equal(np.stack(list(b[k])), np.stack([D.png_decode(x) for x in ep.frames[k]]))
+    md = pq.ParquetFile(os.path.join(out[True][2], "data", "chunk-000", "file-000.parquet")).metadata
+    comp = {md.row_group(0).column(i).path_in_schema: md.row_group(0).column(i).compression
+            for i in range(md.num_columns)}
+    enc = {md.row_group(0).column(i).path_in_schema: md.row_group(0).column(i).encodings
+           for i in range(md.num_columns)}
+    for k in D.IMAGE_KEYS:
+        assert comp[f"{k}.bytes"] == "UNCOMPRESSED"
+        assert not any("DICTIONARY" in e for e in enc[f"{k}.bytes"])
+    assert comp["observation.state.list.element"] == "SNAPPY"
+
+
+def test_threaded_writer_reports_errors(tmp_path):
+    rng = np.random.default_rng(4)
+    feats = {"observation.state": D.FEATURES["observation.state"]}
+    eps = _synthetic_episodes(rng, feats, n_eps=2)
+    bad = D.Episode(2, "not_an_object", BINS[0], None, length=eps[0].length, frames=dict(eps[0].frames))
+    bad.frames["observation.state"] = np.zeros((1, 3), np.float32)  # wrong shape: fails in the thread
+    w = D.LeRobotWriter(str(tmp_path / "ds"), "ds", feats, threaded=True)
+    for ep in eps + [bad]:
+        w.add_episode(ep)
+    with pytest.raises(Exception):
+        w.close()
+
+
 # ----------------------------------------------------------------------------------------- GPU
 def _oracle_episode(seed, task, feats, reward_type="staged", randomize=True):
     """The reference run_episode loop (generate_dataset.py:83-198) on the fp64 oracle."""
