@@ -1342,9 +1342,12 @@ DEV float row_bcast(float v, int k) {
 }
 
 // J_i . x for a block-format row (slots past the row's width hold zeros)
+#ifndef MMX_ROWDOT_BASES
+#define MMX_ROWDOT_BASES 1  // 0: per-slot index select (A/B switch)
+#endif
 DEV float row_dot16(const EnvSh& E, int i, const float* x) {
   const int h = E.hdr[i], b0 = h & 15, b1 = (h >> 4) & 15;
-  const int d0 = blk_d0(b0), n0 = blk_size(b0), d1 = b1 == BLK_NONE ? 0 : blk_d0(b1);
+  const int n0 = blk_size(b0), o0 = blk_d0(b0), o1 = (b1 == BLK_NONE ? 0 : blk_d0(b1)) - n0;
   float jv[16];
 #pragma unroll
   for (int q = 0; q < 4; q++) {
@@ -1354,11 +1357,22 @@ DEV float row_dot16(const EnvSh& E, int i, const float* x) {
     jv[4 * q + 2] = v.z;
     jv[4 * q + 3] = v.w;
   }
+  // slot k holds dof k + o0 below n0 and dof k + o1 from n0 on (n0 = 9 for an arm block, 6 for a
+  // cube), so slots 0..5 read from one base, 6..8 from the base n0 selects, 9..11 from the second
+  // one: LDS reads with immediate offsets instead of a per-slot index select.  Slots 12..14 are
+  // clamped to dof 26 (past the row's width they hold zeros; the clamp keeps the read in x).
+  const float* x0 = x + o0;
+  const float* x1 = x + o1;
+  const float* x2 = n0 == 9 ? x0 : x1;
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < 15; k++) {
-    const int idx = min(k < n0 ? d0 + k : d1 + k - n0, 26);
-    s = fmaf(jv[k], x[idx], s);
+#if MMX_ROWDOT_BASES
+    const float v = k < 6 ? x0[k] : (k < 9 ? x2[k] : (k < 12 ? x1[k] : x[min(o1 + k, 26)]));
+#else
+    const float v = x[min(k < n0 ? o0 + k : o1 + k, 26)];
+#endif
+    s = fmaf(jv[k], v, s);
   }
   return s;
 }
@@ -1475,6 +1489,33 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 #ifndef MMX_HESS_PIPE
 #define MMX_HESS_PIPE 0  // 1: software-pipelined trips (next trip's loads issued before the MFMAs)
 #endif
+// gather one row type's staged 16 x 16 tile into the dof lanes' Hessian rows: dof lane d reads row
+// sd of the tile; the type's two blocks land on static columns of hrow (uniform branches over the
+// 4 possible blocks keep every register index static); slot 15 is the type's gradient
+DEV void tile_gather(const float* G, int t, int bd, int od, float* hrow, float& gacc) {
+  const int b0 = kTB0[t], b1 = kTB1[t];
+  const int n0 = blk_size(b0);
+  const int sd = bd == b0 ? od : (bd == b1 ? n0 + od : -1);
+  if (sd >= 0) {
+    const float* Gr = G + 16 * sd;
+#pragma unroll
+    for (int B = 0; B < 4; B++) {
+      const int nb = B == 0 ? 9 : 6, dB = B == 0 ? 0 : 9 + 6 * (B - 1);
+      if (B == b0) {
+#pragma unroll
+        for (int k = 0; k < nb; k++) hrow[dB + k] += Gr[k];
+      } else if (B == b1) {
+#pragma unroll
+        for (int k = 0; k < nb; k++) hrow[dB + k] += Gr[n0 + k];
+      }
+    }
+    gacc += Gr[15];
+  }
+}
+#ifndef HESS_TILES
+#define HESS_TILES 1  // row types staged per barrier round (E.con holds up to three 16 x 16 tiles; 3: -1.3 % in the A/B, the unrolled rounds grow the substep's save area)
+#endif
+static_assert(HESS_TILES * 256 <= MMX_MAXCON * CON_F, "Hessian staging tiles exceed E.con");
 DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
   float* stats = E.stats;
   CLK_DECL;
@@ -1487,101 +1528,102 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
   for (int i = 0; i < 27; i++) hrow[i] = d < 9 ? (i < 9 ? E.M9[d][i] : 0.f) : (i == d ? E.Mc[d - 9] : 0.f);
   float gacc = 0.f;
   PROBE(6, stats, STAT_T_AUX3);
-  for (int t = 0; t < NTYPE; t++) {
-    const int r0 = E.tbase[t], r1 = E.tbase[t + 1];
-    if (r1 <= r0) continue;
+  // The non-empty row types go in rounds of up to HESS_TILES: each type's tile is staged in its
+  // own 16 x 16 slot of E.con (free until the Cholesky), then one barrier, then the dof lanes
+  // gather every tile of the round (in type order, so the sums are the same as one type at a time)
+  unsigned tmask = 0;  // non-empty row types (uniform)
+  for (int t = 0; t < NTYPE; t++) tmask |= E.tbase[t + 1] > E.tbase[t] ? 1u << t : 0u;
+  tmask = __builtin_amdgcn_readfirstlane(tmask);
+  while (tmask) {
+    int tys[HESS_TILES];
+#pragma unroll
+    for (int j = 0; j < HESS_TILES; j++) {
+      tys[j] = tmask ? __builtin_ctz(tmask) : -1;
+      tmask &= tmask - 1u;
+    }
+#pragma unroll
+    for (int j = 0; j < HESS_TILES; j++) {
+      if (tys[j] < 0) break;
+      const int t = tys[j];
+      const int r0 = E.tbase[t], r1 = E.tbase[t + 1];
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
-    // MMX_HESS_U MFMA steps (one 4-row group each) per trip, loads first; the steps alternate
-    // between the two accumulators, so each sums the same groups in the same order for any
-    // MMX_HESS_U.  Types span whole groups (tbase and MMX_LDSEFC are multiples of 4), so every step
-    // is full.  The LDS groups and the (rare) HBM overflow groups run in separate loops: one
-    // address space per loop, no generic (flat) loads in the hot one.
-    const float m_[4] = {rk == 0 ? 1.f : 0.f, rk == 1 ? 1.f : 0.f, rk == 2 ? 1.f : 0.f, rk == 3 ? 1.f : 0.f};
-    const float c15 = col == 15 ? 1.f : 0.f;  // slot 15 carries g, not C B
-    auto groups = [&](auto from_lds, int g_begin, int g_end) {
-      constexpr bool LDS = decltype(from_lds)::value;
-      float jg_[MMX_HESS_U][4], nc_[MMX_HESS_U][4], dr_[MMX_HESS_U];
-      auto load_trip = [&](int s0) {
-#pragma unroll
-        for (int u = 0; u < MMX_HESS_U; u++) {
-          const int g0 = min(s0 + 4 * u, g_end - 4), r = g0 + rk;
-          if (LDS) {
-            const float4 n4 = *reinterpret_cast<const float4*>(&E.NC[g0]);  // one broadcast read
-            nc_[u][0] = n4.x; nc_[u][1] = n4.y; nc_[u][2] = n4.z; nc_[u][3] = n4.w;
-#pragma unroll
-            for (int m = 0; m < 4; m++) jg_[u][m] = E.J[g0 + m][col];  // slot 15 holds g
-            dr_[u] = E.D[r];
-          } else {
-#pragma unroll
-            for (int m = 0; m < 4; m++) {
-              jg_[u][m] = ovf_j(E, g0 + m)[col];
-              nc_[u][m] = *ovf_nc(E, g0 + m);
+      // MMX_HESS_U MFMA steps (one 4-row group each) per trip, loads first; the steps alternate
+      // between the two accumulators, so each sums the same groups in the same order for any
+      // MMX_HESS_U.  Types span whole groups (tbase and MMX_LDSEFC are multiples of 4), so every step
+      // is full.  The LDS groups and the (rare) HBM overflow groups run in separate loops: one
+      // address space per loop, no generic (flat) loads in the hot one.
+      const float m_[4] = {rk == 0 ? 1.f : 0.f, rk == 1 ? 1.f : 0.f, rk == 2 ? 1.f : 0.f, rk == 3 ? 1.f : 0.f};
+      const float c15 = col == 15 ? 1.f : 0.f;  // slot 15 carries g, not C B
+      auto groups = [&](auto from_lds, int g_begin, int g_end) {
+        constexpr bool LDS = decltype(from_lds)::value;
+        float jg_[MMX_HESS_U][4], nc_[MMX_HESS_U][4], dr_[MMX_HESS_U];
+        auto load_trip = [&](int s0) {
+  #pragma unroll
+          for (int u = 0; u < MMX_HESS_U; u++) {
+            const int g0 = min(s0 + 4 * u, g_end - 4), r = g0 + rk;
+            if (LDS) {
+              const float4 n4 = *reinterpret_cast<const float4*>(&E.NC[g0]);  // one broadcast read
+              nc_[u][0] = n4.x; nc_[u][1] = n4.y; nc_[u][2] = n4.z; nc_[u][3] = n4.w;
+  #pragma unroll
+              for (int m = 0; m < 4; m++) jg_[u][m] = E.J[g0 + m][col];  // slot 15 holds g
+              dr_[u] = E.D[r];
+            } else {
+  #pragma unroll
+              for (int m = 0; m < 4; m++) {
+                jg_[u][m] = ovf_j(E, g0 + m)[col];
+                nc_[u][m] = *ovf_nc(E, g0 + m);
+              }
+              dr_[u] = *ovf_d(E, r);
             }
-            dr_[u] = *ovf_d(E, r);
+          }
+        };
+  #if MMX_HESS_PIPE  // the next trip's loads in flight during this trip's math and MFMAs
+        if (g_begin < g_end) load_trip(g_begin);
+  #endif
+        for (int s0 = g_begin; s0 < g_end; s0 += 4 * MMX_HESS_U) {
+          float a[MMX_HESS_U], b[MMX_HESS_U];
+  #if !MMX_HESS_PIPE
+          load_trip(s0);
+  #endif
+  #pragma unroll
+          for (int u = 0; u < MMX_HESS_U; u++) {
+            // arithmetic selects over the lane's row rk (0 / 1 masks): no divergent branches
+            const float live = s0 + 4 * u < g_end ? 1.f : 0.f;  // uniform
+            const float* jg = jg_[u];
+            const float* nc = nc_[u];
+            const float own = fmaf(m_[0], jg[0], fmaf(m_[1], jg[1], fmaf(m_[2], jg[2], m_[3] * jg[3])));
+            const float ncr = fmaf(m_[1], nc[1], fmaf(m_[2], nc[2], m_[3] * nc[3]));  // C_nk of row rk (0 for n)
+            const float s123 = fmaf(nc[1], jg[1], fmaf(nc[2], jg[2], nc[3] * jg[3]));
+            const float cpl = fmaf(ncr, jg[0], m_[0] * s123);
+            a[u] = live * own;  // (slot 15 only feeds G's unused row 15)
+            b[u] = live * fmaf(c15, own - fmaf(dr_[u], own, cpl), fmaf(dr_[u], own, cpl));
+          }
+  #if MMX_HESS_PIPE
+          if (s0 + 4 * MMX_HESS_U < g_end) load_trip(s0 + 4 * MMX_HESS_U);
+  #endif
+  #pragma unroll
+          for (int u = 0; u < MMX_HESS_U; u++) {
+            if (u & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[u], acc1, 0, 0, 0);
+            else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[u], acc0, 0, 0, 0);
           }
         }
       };
-#if MMX_HESS_PIPE  // the next trip's loads in flight during this trip's math and MFMAs
-      if (g_begin < g_end) load_trip(g_begin);
-#endif
-      for (int s0 = g_begin; s0 < g_end; s0 += 4 * MMX_HESS_U) {
-        float a[MMX_HESS_U], b[MMX_HESS_U];
-#if !MMX_HESS_PIPE
-        load_trip(s0);
-#endif
-#pragma unroll
-        for (int u = 0; u < MMX_HESS_U; u++) {
-          // arithmetic selects over the lane's row rk (0 / 1 masks): no divergent branches
-          const float live = s0 + 4 * u < g_end ? 1.f : 0.f;  // uniform
-          const float* jg = jg_[u];
-          const float* nc = nc_[u];
-          const float own = fmaf(m_[0], jg[0], fmaf(m_[1], jg[1], fmaf(m_[2], jg[2], m_[3] * jg[3])));
-          const float ncr = fmaf(m_[1], nc[1], fmaf(m_[2], nc[2], m_[3] * nc[3]));  // C_nk of row rk (0 for n)
-          const float s123 = fmaf(nc[1], jg[1], fmaf(nc[2], jg[2], nc[3] * jg[3]));
-          const float cpl = fmaf(ncr, jg[0], m_[0] * s123);
-          a[u] = live * own;  // (slot 15 only feeds G's unused row 15)
-          b[u] = live * fmaf(c15, own - fmaf(dr_[u], own, cpl), fmaf(dr_[u], own, cpl));
-        }
-#if MMX_HESS_PIPE
-        if (s0 + 4 * MMX_HESS_U < g_end) load_trip(s0 + 4 * MMX_HESS_U);
-#endif
-#pragma unroll
-        for (int u = 0; u < MMX_HESS_U; u++) {
-          if (u & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[u], acc1, 0, 0, 0);
-          else acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[u], acc0, 0, 0, 0);
-        }
+      const int split = min(max(r0, MMX_LDSEFC), r1);
+      groups(std::true_type{}, r0, split);
+      if (split < r1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the overflow rows' stores (ovf_fence)
+        groups(std::false_type{}, split, r1);
       }
-    };
-    const int split = min(max(r0, MMX_LDSEFC), r1);
-    groups(std::true_type{}, r0, split);
-    if (split < r1) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the overflow rows' stores (ovf_fence)
-      groups(std::false_type{}, split, r1);
+      PROBE(6, stats, STAT_T_AUX0);
+      // stage: lane l holds G[4 (l >> 4) + q][l & 15]
+#pragma unroll
+      for (int q = 0; q < 4; q++) G[256 * j + 16 * (4 * rk + q) + col] = acc0[q] + acc1[q];
     }
-    PROBE(6, stats, STAT_T_AUX0);
-    // stage: lane l holds G[4 (l >> 4) + q][l & 15]
-#pragma unroll
-    for (int q = 0; q < 4; q++) G[16 * (4 * rk + q) + col] = acc0[q] + acc1[q];
     SYNC();
-    // gather: dof lane d reads row sd of the tile; the type's two blocks land on static columns
-    // of hrow (uniform branches over the 4 possible blocks keep every register index static)
-    const int b0 = kTB0[t], b1 = kTB1[t];
-    const int n0 = blk_size(b0);
-    const int sd = bd == b0 ? od : (bd == b1 ? n0 + od : -1);
-    if (sd >= 0) {
-      const float* Gr = G + 16 * sd;
 #pragma unroll
-      for (int B = 0; B < 4; B++) {
-        const int nb = B == 0 ? 9 : 6, dB = B == 0 ? 0 : 9 + 6 * (B - 1);
-        if (B == b0) {
-#pragma unroll
-          for (int k = 0; k < nb; k++) hrow[dB + k] += Gr[k];
-        } else if (B == b1) {
-#pragma unroll
-          for (int k = 0; k < nb; k++) hrow[dB + k] += Gr[n0 + k];
-        }
-      }
-      gacc += Gr[15];
+    for (int j = 0; j < HESS_TILES; j++) {
+      if (tys[j] < 0) break;
+      tile_gather(G + 256 * j, tys[j], bd, od, hrow, gacc);
     }
     SYNC();
     PROBE(6, stats, STAT_T_AUX1);
@@ -1611,6 +1653,17 @@ DEV float hess_grad_delta(EnvSh& E, float* hrow, const unsigned long long* gm) {
   const float m_[4] = {rk == 0 ? 1.f : 0.f, rk == 1 ? 1.f : 0.f, rk == 2 ? 1.f : 0.f, rk == 3 ? 1.f : 0.f};
   const float c15 = col == 15 ? 1.f : 0.f;
   float gacc = 0.f;
+  int nst = 0, tyslots = 0;  // tiles staged in this round and their row types (4 bits each)
+  auto flush = [&]() {
+    if (nst == 0) return;
+    SYNC();
+#pragma unroll
+    for (int j = 0; j < HESS_TILES; j++)
+      if (j < nst) tile_gather(G + 256 * j, (tyslots >> (4 * j)) & 15, bd, od, hrow, gacc);
+    SYNC();
+    nst = 0;
+    tyslots = 0;
+  };
   for (int t = 0; t < NTYPE; t++) {
     const int r0 = E.tbase[t], r1 = E.tbase[t + 1];
     if (r1 <= r0) continue;
@@ -1639,29 +1692,13 @@ DEV float hess_grad_delta(EnvSh& E, float* hrow, const unsigned long long* gm) {
       }
     }
     if (!any) continue;
+    // stage into the round's next tile; a full round (or the last type) is gathered in type order
 #pragma unroll
-    for (int q = 0; q < 4; q++) G[16 * (4 * rk + q) + col] = acc[q];
-    SYNC();
-    const int b0 = kTB0[t], b1 = kTB1[t];
-    const int n0 = blk_size(b0);
-    const int sd = bd == b0 ? od : (bd == b1 ? n0 + od : -1);
-    if (sd >= 0) {
-      const float* Gr = G + 16 * sd;
-#pragma unroll
-      for (int B = 0; B < 4; B++) {
-        const int nb = B == 0 ? 9 : 6, dB = B == 0 ? 0 : 9 + 6 * (B - 1);
-        if (B == b0) {
-#pragma unroll
-          for (int k = 0; k < nb; k++) hrow[dB + k] += Gr[k];
-        } else if (B == b1) {
-#pragma unroll
-          for (int k = 0; k < nb; k++) hrow[dB + k] += Gr[n0 + k];
-        }
-      }
-      gacc += Gr[15];
-    }
-    SYNC();
+    for (int q = 0; q < 4; q++) G[256 * nst + 16 * (4 * rk + q) + col] = acc[q];
+    tyslots |= t << (4 * nst);
+    if (++nst == HESS_TILES) flush();
   }
+  flush();
   return nd >= 0 ? gacc : 0.f;
 }
 

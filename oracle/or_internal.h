@@ -57,6 +57,7 @@ struct or_env {
   int solver_iter;
   double solver_tol;       /* Newton: relative gradient tolerance (default 1e-13: parity tests) */
   int solver_maxiter;      /* iteration cap (default 200) */
+  double solver_mj_tol;    /* MuJoCo's opt.tolerance convergence tests, 0 = off (parity tests) */
   long solver_calls, solver_iters_total;
   /* gym episode state */
   or_pcg64 rng;

@@ -447,11 +447,21 @@ static int cmp_dbl_idx(const void* a, const void* b) {
   return (x[0] > y[0]) - (x[0] < y[0]);
 }
 
+/* Primal Newton with exact line search (MuJoCo's default solver, mj_solNewton), warm-started from
+ * the cheaper of qacc_warmstart and qacc_smooth.  Convergence: the relative gradient test
+ * |g| / (1 + |qfrc_smooth|) < solver_tol (the parity tests' fully converged solve, 1e-13), and, when
+ * solver_mj_tol > 0, MuJoCo's own tests at opt.tolerance: after an iteration, stop when its cost
+ * decrease or the gradient norm, both scaled by 1 / (meaninertia * nv) (mj_setConst's
+ * stat.meaninertia: the mean diagonal of qM at qpos0), is below the tolerance (MuJoCo records the
+ * two per iteration as mjSolverStat.improvement / .gradient). */
 static void solve_newton(or_env* e) {
   int n = e->nefc;
   double x[NV];
-  if (cost_at(e, e->qacc_ws) < cost_at(e, e->qacc_smooth)) memcpy(x, e->qacc_ws, sizeof(x));
+  const double c_ws = cost_at(e, e->qacc_ws), c_s = cost_at(e, e->qacc_smooth);
+  if (c_ws < c_s) memcpy(x, e->qacc_ws, sizeof(x));
   else memcpy(x, e->qacc_smooth, sizeof(x));
+  const double mjscale = 1.0 / (OM_MEANINERTIA * NV);
+  double cost_old = c_ws < c_s ? c_ws : c_s;
   double r[OR_MAXEFC], s[OR_MAXEFC], bp[OR_MAXEFC][2];
   double res = 0;
   int it;
@@ -482,6 +492,7 @@ static void solve_newton(or_env* e) {
     }
     res = sqrt(gn) / (1 + sqrt(sc));
     if (res < e->solver_tol) break;
+    if (e->solver_mj_tol > 0 && it > 0 && mjscale * sqrt(gn) < e->solver_mj_tol) break;
     if (chol_factor(H, NV) != 0) break;
     double p[NV];
     for (int d = 0; d < NV; d++) p[d] = -g[d];
@@ -537,6 +548,12 @@ static void solve_newton(or_env* e) {
       step += alpha * alpha * p[d] * p[d];
     }
     if (sqrt(step) < 1e-15) { it++; break; }
+    if (e->solver_mj_tol > 0) {
+      const double c = cost_at(e, x);
+      const double improvement = mjscale * (cost_old - c);
+      cost_old = c;
+      if (improvement < e->solver_mj_tol) { it++; break; }
+    }
   }
   e->solver_res = res;
   e->solver_iter = it;
@@ -669,6 +686,7 @@ void or_set_solver(or_env* e, double tol, int maxiter) {
   e->solver_tol = tol;
   e->solver_maxiter = maxiter;
 }
+void or_set_solver_mj(or_env* e, double mj_tol) { e->solver_mj_tol = mj_tol; }
 void or_solver_stats(or_env* e, long* calls, long* iters) {
   *calls = e->solver_calls;
   *iters = e->solver_iters_total;

@@ -430,6 +430,7 @@ or_env* or_create(int action_mode, int reward_type, int max_episode_steps, int r
   e->fixed_obj = e->fixed_bin = -1;
   e->solver_tol = 1e-13;
   e->solver_maxiter = 200;
+  e->solver_mj_tol = 0;
   or_pcg64_seed(&e->rng, 0);
   or_reset_keyframe(e);
   return e;

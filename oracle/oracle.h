@@ -73,6 +73,11 @@ double or_solver_residual(or_env* e);
 /* Newton tolerance / iteration cap (defaults 1e-13 / 200 for the parity tests; MuJoCo's defaults
  * are 1e-8 / 100, which the CPU baseline uses) and (solves, iterations) counted since creation */
 void or_set_solver(or_env* e, double tol, int maxiter);
+/* MuJoCo's convergence tests at opt.tolerance mj_tol (0 = off, the default): after each Newton
+ * iteration stop when scale * (cost decrease) < mj_tol or scale * |gradient| < mj_tol, scale =
+ * 1 / (meaninertia * nv) (mj_solNewton, recorded per iteration in mjSolverStat.improvement /
+ * .gradient) */
+void or_set_solver_mj(or_env* e, double mj_tol);
 void or_solver_stats(or_env* e, long* calls, long* iters);
 /* constraint rows of the last solve: type (0 equality, 1 limit, 2 contact edge), pos, R, aref;
  * returns nefc (NULL skips a field; arrays hold OR_MAXEFC) */

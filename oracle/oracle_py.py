@@ -68,6 +68,7 @@ def lib():
         L.or_solver_residual.argtypes = [C.c_void_p]
         L.or_get_qacc.argtypes = [C.c_void_p, dp]
         L.or_set_solver.argtypes = [C.c_void_p, C.c_double, C.c_int]
+        L.or_set_solver_mj.argtypes = [C.c_void_p, C.c_double]
         L.or_solver_stats.argtypes = [C.c_void_p, C.POINTER(C.c_long), C.POINTER(C.c_long)]
         L.or_get_efc.restype = C.c_int
         L.or_get_efc.argtypes = [C.c_void_p, ip, dp, dp, dp]
@@ -277,6 +278,11 @@ class OracleEnv:
         """Newton tolerance / iteration cap (defaults: the parity tests' 1e-13 / 200; MuJoCo's own
         defaults are 1e-8 / 100)."""
         lib().or_set_solver(self.ptr, float(tol), int(maxiter))
+
+    def set_solver_mj(self, mj_tol=1e-8):
+        """MuJoCo's convergence tests at opt.tolerance (improvement / scaled gradient after each
+        iteration); 0 turns them off (the parity tests' default)."""
+        lib().or_set_solver_mj(self.ptr, float(mj_tol))
 
     def solver_stats(self):
         """(solves, Newton iterations) since creation."""

@@ -574,6 +574,9 @@ def invweights(model):
             dinv[da] = Minv[da, da]
     model["body_invweight0"] = binv
     model["dof_invweight0"] = dinv.tolist()
+    # mj_setConst's m->stat.meaninertia: the mean diagonal of qM (armature included) at qpos0; the
+    # Newton solver's convergence tests scale by 1 / (meaninertia * nv)
+    model["meaninertia"] = float(np.trace(M) / model["nv"])
 
 
 # --------------------------------------------------------------------------- emit
@@ -715,6 +718,7 @@ def emit_header(model, path, real, prefix, guard):
     L.append(c_array(f"{P}dof_jnt", "int", dof_jnt))
     L.append(c_array(f"{P}dof_invweight0", R, model["dof_invweight0"]))
     L.append(c_array(f"{P}qpos0", R, model["qpos0"]))
+    L.append(f"#define {P}MEANINERTIA {model['meaninertia']:.17g}\n")
     L.append(c_array(f"{P}key_qpos", R, model["key_qpos"]))
     L.append(c_array(f"{P}key_ctrl", R, model["key_ctrl"]))
     # geoms (colliding only, renumbered)
