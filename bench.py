@@ -220,9 +220,11 @@ def launch_ranks(n: int, cmd: list[str] | None = None, poll_s: float = 0.2, grac
 
 
 # ----------------------------------------------------------------------------- PMC evidence
-def pmc_evidence(workload: str, envs: int, spl: int, lanes: int) -> dict | None:
+def pmc_evidence(workload: str, envs: int, lanes: int) -> dict | None:
     """Counter evidence recorded by tools/profile.sh for THIS configuration (same workload, envs
-    per GPU, env steps per launch and concurrent launches); None when absent or different."""
+    per GPU and concurrent launches; the counters are per env step, which the launch length -- the
+    record is loaded and stored once per launch, 2.5 KB of ~100 KB per env step -- barely moves);
+    None when absent or different."""
     f = os.path.join(REPO, "profiles", f"pmc_{workload}.json")
     if not os.path.exists(f):
         return None
@@ -231,8 +233,7 @@ def pmc_evidence(workload: str, envs: int, spl: int, lanes: int) -> dict | None:
     except (OSError, ValueError):
         return None
     c = rec.get("config", {})
-    if (c.get("workload"), c.get("envs_per_gpu"), c.get("env_steps_per_launch"), c.get("lanes")) != \
-            (workload, envs, spl, lanes):
+    if (c.get("workload"), c.get("envs_per_gpu"), c.get("lanes")) != (workload, envs, lanes):
         return None
     return rec
 
@@ -304,11 +305,10 @@ def main():
     env.rollout_expert(args.warmup)
     torch.cuda.synchronize()
 
-    spl = env.sim.rollout_steps_per_launch
     lanes = env.sim.rollout_lanes
-    launches = -(-args.steps // spl)
+    launches = env.sim.rollout_launches(args.steps)  # per lane (launch lengths within one of each other)
     # the sim launches on torch's current stream and forks its `lanes` concurrent env ranges from
-    # it (each range: one mmx_env_step_kernel launch per spl env steps on its own stream, joined
+    # it (each range: `launches` mmx_env_step_kernel launches of ~steps / launches env steps on its own stream, joined
     # back at the end): events on that stream bracket the K env steps of every range, so
     # kern_ms is the span over which one launch of each range (N envs in total) ran side by side
     stream = torch.cuda.current_stream(dev)
@@ -333,7 +333,7 @@ def main():
         env.sim.kernel_timing(False)
         kt = env.sim.kernel_times()
         span_ms = ev0.elapsed_time(ev1) / launches  # the rollout's span per launch round
-        # the step kernel's average launch duration (each launch: envs_per_launch envs x spl steps)
+        # the step kernel's average launch duration (each launch: envs_per_launch envs x ~steps / launches steps)
         kern_ms = kt["step_ms"] / max(kt["step_launches"], 1)
         render_ms = kt["render_ms"] / kt["render_launches"] if kt["render_launches"] else None
         eps = (env._epi[:, cnt].sum(0).double() - epi0).tolist()
@@ -376,8 +376,8 @@ def main():
     med = windows[int(np.argsort(values)[len(values) // 2])]
     value = args.steps * N * world / med["elapsed"]
     solver, kern_ms = med["solver"], med["kern_ms"]
-    # spl env steps of the batch = `lanes` concurrent mmx_env_step_kernel dispatches of N / lanes
-    # envs x spl steps each; they run side by side for the whole span, so a dispatch lasts ~kern_ms
+    # a launch round = `lanes` concurrent mmx_env_step_kernel dispatches of N / lanes envs x
+    # steps / launches env steps each; they run side by side for the whole span, so a dispatch lasts ~kern_ms
     # (rocprof's per-dispatch average agrees) and the chip-level rate is lanes x one dispatch's
     # bytes / kern_ms.  nefc is the mean rows per substep counted on device in the same window.
     envs_per_launch = N / lanes
@@ -395,7 +395,7 @@ def main():
         S = args.image_size
         rbytes = envs_per_launch * (2 * S * S * 4 + 14 * 12 * 4)
         r_achieved = lanes * rbytes / (med["render_ms"] * 1e-3) / 1e9
-        rpmc = pmc_evidence("render", N, 1, lanes)
+        rpmc = pmc_evidence("render", N, lanes)
         render = {"kernel": "mmx_render_kernel", "kernel_ms": med["render_ms"], "concurrent_launches": lanes,
                   "envs_per_launch": envs_per_launch, "image_size": S, "bytes_per_launch": rbytes,
                   "bound": "valu", "hbm_achieved_GBs": r_achieved, "hbm_frac": r_achieved / HBM_PEAK_GBS,
@@ -405,7 +405,7 @@ def main():
                   "note": "HBM is not the render kernel's roof (it writes 4 B per pixel); VALU issue is "
                           "(valu: SQ counters of tools/render_pmc.sh for this configuration)"}
     if rank == 0:
-        pmc = pmc_evidence(args.workload, N, spl, lanes)
+        pmc = pmc_evidence(args.workload, N, lanes)
         traffic = None if pmc is None else pmc["hbm_bytes_per_env_step"] * envs_per_launch * steps_per_launch
         workload = (f"C2: PickPlaceGymEnv.step x {N} envs/GPU, fixed task (obj_red, bin_red), keyframe start (no "
                     "randomisation), staged reward, FSM expert abs_pos, autoreset" if c2 else

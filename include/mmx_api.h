@@ -128,13 +128,19 @@ int mmx_expert_plan(mmx_sim* sim, int32_t n_steps, float* action_dev_out);
  * Requires action_mode == MMX_ACTION_ABS_POS. */
 int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps);
 
+/* Launches per rollout lane that mmx_rollout_expert(sim, n_env_steps) makes: a launch runs
+ * min(steps_per_launch, ceil(n / 8)) consecutive steps (1 with cameras) and the n steps are cut into
+ * launches of near-equal length, so a short rollout still spreads over several launch rounds (the
+ * drain at the end of a call then costs a fraction of a short launch).  0 for a null sim or n <= 0. */
+int mmx_rollout_launches(const mmx_sim* sim, int32_t n_env_steps);
+
 /* Number of independent env ranges a multi-step rollout runs concurrently (one internal stream
  * each, forked from and joined back to cfg.stream; env MMX_STREAMS overrides the default of one
  * range per 1024 envs, at most 4).  Single-step calls always run as one launch on cfg.stream. */
 int mmx_rollout_lanes(const mmx_sim* sim);
 
-/* Env steps one mmx_env_step_kernel launch runs per env in mmx_rollout_expert: 1 with cameras
- * (every step is rendered), else up to 16 (env MMX_FUSE overrides).  A fused launch runs its
+/* Upper bound of the env steps one mmx_env_step_kernel launch runs per env in mmx_rollout_expert: 1
+ * with cameras (every step is rendered), else 16 (env MMX_FUSE overrides).  A fused launch runs its
  * envs' steps back to back inside each workgroup; the trajectories are bit-identical to one
  * launch per step.  0 for a null sim. */
 int mmx_rollout_steps_per_launch(const mmx_sim* sim);

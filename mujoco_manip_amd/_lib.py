@@ -55,7 +55,7 @@ class MMXBuffers(C.Structure):
 EXPORTED = ("mmx_config_default", "mmx_create", "mmx_destroy", "mmx_last_error", "mmx_reset", "mmx_step",
             "mmx_expert_plan", "mmx_rollout_expert", "mmx_physics_step", "mmx_forward", "mmx_get_buffers",
             "mmx_synchronize", "mmx_get_state", "mmx_set_state", "mmx_episode_seed", "mmx_rollout_lanes",
-            "mmx_rollout_steps_per_launch", "mmx_expert_physics", "mmx_eval_reward", "mmx_kernel_timing",
+            "mmx_rollout_steps_per_launch", "mmx_rollout_launches", "mmx_expert_physics", "mmx_eval_reward", "mmx_kernel_timing",
             "mmx_kernel_times", "mmx_png_bound", "mmx_png_scratch", "mmx_png_encode", "mmx_png_pack")
 
 _lib = None
@@ -89,6 +89,8 @@ def load(build_if_missing: bool = True):
     L.mmx_rollout_lanes.restype = C.c_int
     L.mmx_rollout_steps_per_launch.argtypes = [vp]
     L.mmx_rollout_steps_per_launch.restype = C.c_int
+    L.mmx_rollout_launches.argtypes = [vp, C.c_int32]
+    L.mmx_rollout_launches.restype = C.c_int
     L.mmx_forward.argtypes = [vp]
     L.mmx_expert_physics.argtypes = [vp, C.c_int32]
     L.mmx_eval_reward.argtypes = [vp, vp, vp, vp, vp, C.c_int32]
@@ -284,6 +286,10 @@ class Sim:
     @property
     def rollout_steps_per_launch(self) -> int:
         return int(self.L.mmx_rollout_steps_per_launch(self.ptr))
+
+    def rollout_launches(self, n_env_steps: int) -> int:
+        """Launches per rollout lane that rollout_expert(n_env_steps) makes."""
+        return int(self.L.mmx_rollout_launches(self.ptr, int(n_env_steps)))
 
     def physics_step(self, n: int = 1, with_ik: bool = False):
         self._check(self.L.mmx_physics_step(self.ptr, n, int(with_ik)), "mmx_physics_step")

@@ -344,9 +344,10 @@ def test_rollout_lanes_bit_identical(monkeypatch):
 
 
 def test_fused_rollout_bit_identical(monkeypatch):
-    """Several env steps per launch (mmx_rollout_steps_per_launch) change nothing but timing:
-    state, episode records, observations, rewards, flags and solver stats match one launch per
-    step bit for bit, incl. autoresets inside a fused launch and a ragged last chunk (40 = 5 x 7 + 5)."""
+    """Several env steps per launch (mmx_rollout_steps_per_launch, mmx_rollout_launches) change
+    nothing but timing: state, episode records, observations, rewards, flags and solver stats match
+    one launch per step bit for bit, incl. autoresets inside a fused launch and launches of unequal
+    length (43 steps at a cap of 7 or 32: 8 launches of min(cap, ceil(43 / 8)) = 6 -> 6,6,6,5,5,5,5,5)."""
     import oracle_py as O
     from mujoco_manip_amd import _lib
     from mujoco_manip_amd.vec_env import PickPlaceVecEnv
@@ -359,8 +360,10 @@ def test_fused_rollout_bit_identical(monkeypatch):
         env = PickPlaceVecEnv(12, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
                               autoreset=True, image_size=0, max_episode_steps=25)
         assert env.sim.rollout_steps_per_launch == int(fuse)
+        assert env.sim.rollout_launches(43) == (43 if fuse == "1" else 8)
+        assert env.sim.rollout_launches(512) == -(-512 // min(int(fuse), 64))
         env.reset(seed=seeds)
-        env.rollout_expert(40)
+        env.rollout_expert(43)
         torch.cuda.synchronize()
         q, v, _, _ = env.sim.get_state()
         s = env.sim

@@ -70,9 +70,9 @@ def main():
                 open(os.path.join(dst, f"{tag}_bench_trace.json"), "w").write(lines[-1])
             line = line or json.loads(lines[-1])
     rf = line["roofline"]
-    lanes, spl, epl = rf["concurrent_launches"], int(rf["env_steps_per_launch"]), rf["envs_per_launch"]
-    n_timed = lanes * (-(-a.timed_steps // spl))  # dispatches of the timed window (the last ones)
-    unit = epl * spl  # env steps per dispatch
+    lanes, spl, epl = rf["concurrent_launches"], rf["env_steps_per_launch"], rf["envs_per_launch"]
+    n_timed = lanes * int(round(a.timed_steps / spl))  # dispatches of the timed window (the last ones)
+    unit = epl * spl  # env steps per dispatch (mean: launch lengths differ by at most one step)
     fetch = timed_mean(per_dispatch(os.path.join(a.prof, "fetch"), ["FETCH_SIZE"]), n_timed)["FETCH_SIZE"]
     write = timed_mean(per_dispatch(os.path.join(a.prof, "write"), ["WRITE_SIZE"]), n_timed)["WRITE_SIZE"]
     sq_names = ["SQ_WAVE_CYCLES", "SQ_WAVES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_VALU", "SQ_INSTS_VALU",
