@@ -236,6 +236,14 @@ DEV int row_type(int b0, int b1) {
   return b0 == 0 ? (b1 == BLK_NONE ? 0 : b1) : (b0 == 1 ? (b1 == BLK_NONE ? 4 : 3 + b1) : (b0 == 2 ? (b1 == BLK_NONE ? 7 : 8) : 9));
 }
 DEV bool arm_anc(int d, int b) { return d <= 6 ? (b >= d + 2 && b <= 11) : (d == 7 ? b == 10 : b == 11); }
+// the arm dofs on body b's root path as a 9-bit mask (bit d = arm_anc(d, b)): the chain dofs
+// 0..min(b - 2, 6), plus finger dof 7 / 8 for the finger bodies 10 / 11
+DEV unsigned anc_mask(int b) {
+  return b >= 2 && b <= 11 ? ((1u << min(b - 1, 7)) - 1u) | (b == 10 ? 0x80u : 0u) | (b == 11 ? 0x100u : 0u) : 0u;
+}
+#ifndef MMX_CROW_FAST
+#define MMX_CROW_FAST 1  // contact rows: ancestor masks and per-body columns (0: per-dof tests, A/B)
+#endif
 DEV V3 body_x(const EnvSh& E, int b) {
   if (MMX_body_static[b]) return V3{0.f, 0.f, 0.f};
   const int s = body_slot(b);
@@ -1087,18 +1095,57 @@ DEV float contact_row(EnvSh& E, int row, int c, int rr) {
     rb0 = rb1;
     rb1 = t;
   }
+#if MMX_CROW_FAST
+  // arm block: coefficient +1 / -1 / 0 of dof d from the two bodies' ancestor-dof masks
+  const unsigned am1 = anc_mask(b1), am2 = anc_mask(b2);
+#endif
   float vel = 0.f;
   float arm[9];
   // u . (v_d + w_d x p) + w . w_d = u . v_d + w_d . (p x u + w): one cross product per row
   const V3 pu = cross(p, u) + w;
 #pragma unroll
   for (int d = 0; d < 9; d++) {  // body 2 counts +, body 1 counts -
+#if MMX_CROW_FAST
+    const float coef = (float)((int)((am2 >> d) & 1u) - (int)((am1 >> d) & 1u));
+#else
     const float coef = (arm_anc(d, b2) ? 1.f : 0.f) - (arm_anc(d, b1) ? 1.f : 0.f);
+#endif
     const SV sd = load_S(E, d);
     arm[d] = coef * (dot(u, sd.v) + dot(sd.w, pu));
     vel = fmaf(arm[d], E.qvel[d], vel);
   }
   float cubeA[6], cubeB[6];  // blocks rb0 (when a cube) and rb1
+#if MMX_CROW_FAST
+  // each body's free-body columns (zero unless it is a cube), velocity summed in body order; block
+  // A (rb0) is body 1's unless body 1 is not rb0
+  float cvs[2][6];
+#pragma unroll
+  for (int side = 0; side < 2; side++) {
+    const int b = side ? b2 : b1, blk = side ? k2 : k1;
+#pragma unroll
+    for (int j = 0; j < 6; j++) cvs[side][j] = 0.f;
+    if (blk > 0) {
+      const float sg = side ? 1.f : -1.f;
+      const V3 x = body_x(E, b);
+      const M3 R = body_R(E, b);
+      cvs[side][0] = sg * u.x;
+      cvs[side][1] = sg * u.y;
+      cvs[side][2] = sg * u.z;
+      const V3 ru = cross(p - x, u) + w;  // u . (r_k x (p - x)) + w . r_k = r_k . ((p - x) x u + w)
+#pragma unroll
+      for (int k = 0; k < 3; k++) cvs[side][3 + k] = sg * dot(col(R, k), ru);
+      const int d0 = blk_d0(blk);
+#pragma unroll
+      for (int j = 0; j < 6; j++) vel = fmaf(cvs[side][j], E.qvel[d0 + j], vel);
+    }
+  }
+  const bool swap = k1 != rb0;
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+    cubeA[j] = swap ? cvs[1][j] : cvs[0][j];
+    cubeB[j] = swap ? cvs[0][j] : cvs[1][j];
+  }
+#else
 #pragma unroll
   for (int j = 0; j < 6; j++) {
     cubeA[j] = 0.f;
@@ -1125,6 +1172,7 @@ DEV float contact_row(EnvSh& E, int row, int c, int rr) {
       }
     }
   }
+#endif
   float jv[16];
   const bool armrow = rb0 == 0;
 #pragma unroll
