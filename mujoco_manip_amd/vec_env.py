@@ -5,8 +5,9 @@ same constructor keywords, same 5 action modes, same numeric observation keys an
 types.  Differences, all documented in DESIGN.md:
   * observations are torch tensors on the GPU ([N, ...]); with image_size > 0 the
     `image_overhead` / `image_wrist` keys are uint8 [N, S, S, 3] from the batched HIP rasteriser
-    (mmx_render.hip: per-body hull geometry, flat-lit with the scene's lights, no shadows or
-    specular; DESIGN.md §8), image_size = 0 skips them;
+    (mmx_render.hip: the Panda's visual parts reduced to convex pieces and clustered meshes per
+    part, flat-lit with the scene's lights, no shadows or specular), image_size = 0
+    skips them;
   * reset(seed=s) seeds env i with s + i (gymnasium vector convention); a list gives one
     seed per env;
   * with autoreset=True an env that terminated/truncated (or whose FSM expert finished: reported
