@@ -241,6 +241,9 @@ DEV bool arm_anc(int d, int b) { return d <= 6 ? (b >= d + 2 && b <= 11) : (d ==
 DEV unsigned anc_mask(int b) {
   return b >= 2 && b <= 11 ? ((1u << min(b - 1, 7)) - 1u) | (b == 10 ? 0x80u : 0u) | (b == 11 ? 0x100u : 0u) : 0u;
 }
+#ifndef MMX_TYPE_BALLOT
+#define MMX_TYPE_BALLOT 1  // row-type bases from per-type ballots (0: packed prefix scans, A/B)
+#endif
 #ifndef MMX_CROW_FAST
 #define MMX_CROW_FAST 1  // contact rows: ancestor masks and per-body columns (0: per-dof tests, A/B)
 #endif
@@ -1225,11 +1228,31 @@ DEV void make_constraints_wave(EnvSh& E) {
   }
   // single rows (equality + limits), then per type the contact groups
   const int acnt = (LANE == 0 ? 1 : 0) + nlim;
+#if MMX_TYPE_BALLOT
+  // acnt <= 3: its two bits as ballots give the exclusive prefix and the total without a scan
+  const unsigned long long a0 = __ballot(acnt & 1), a1 = __ballot(acnt & 2);
+  const int nsingle_raw = __popcll(a0) + 2 * __popcll(a1);
+  const int arow = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(a0 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)a0, 0u)) +
+                   2 * (int)__builtin_amdgcn_mbcnt_hi((unsigned)(a1 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)a1, 0u));
+#else
   const int aincl = wave_scan_incl(acnt);
   const int nsingle_raw = __builtin_amdgcn_readlane(aincl, 63);
-  const int nsingle = (nsingle_raw + 3) & ~3;
   const int arow = aincl - acnt;
+#endif
+  const int nsingle = (nsingle_raw + 3) & ~3;
   int brow = 0, base = 0;
+#if MMX_TYPE_BALLOT
+  // per type: one ballot of the contacts (lanes) of that type; a lane's rows start at the type's
+  // base plus 4 x the contacts of its type in lower lanes (mbcnt), so no prefix scans
+#pragma unroll
+  for (int t = 0; t < NTYPE; t++) {
+    const unsigned long long m = __ballot(tc == t);
+    const int first = base + (t == 0 ? nsingle : 0);  // type 0: the single rows come first
+    if (tc == t) brow = first + 4 * (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+    if (LANE == 0) E.tbase[t] = min(base, MMX_MAXEFC);
+    base = first + 4 * __popcll(m);
+  }
+#else
   // per-type prefix counts of contact rows, three 10-bit fields per 32-bit scan (<= MAXEFC < 1024)
 #pragma unroll
   for (int t0 = 0; t0 < NTYPE; t0 += 3) {
@@ -1253,9 +1276,15 @@ DEV void make_constraints_wave(EnvSh& E) {
       base = first + ((tot >> (10 * f)) & 1023);
     }
   }
+#endif
   const int total = base;
   const int nefc = min(total, MMX_MAXEFC);
+#if MMX_TYPE_BALLOT
+  const int nefc_mj = nsingle_raw + __popcll(__ballot(nedge & 1)) + 2 * __popcll(__ballot(nedge & 2)) +
+                      4 * __popcll(__ballot(nedge & 4));  // nedge <= 6
+#else
   const int nefc_mj = nsingle_raw + (int)wave_sum((float)nedge);
+#endif
   if (LANE == 0) {
     E.tbase[NTYPE] = nefc;
     E.nefc = nefc;
@@ -1582,17 +1611,22 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
   unsigned tmask = 0;  // non-empty row types (uniform)
   for (int t = 0; t < NTYPE; t++) tmask |= E.tbase[t + 1] > E.tbase[t] ? 1u << t : 0u;
   tmask = __builtin_amdgcn_readfirstlane(tmask);
+  int nst = 0, tyslots = 0;  // tiles staged in this round and their row types (4 bits each)
+  auto flush = [&]() {
+    if (nst == 0) return;
+    SYNC();
+#pragma unroll
+    for (int j = 0; j < HESS_TILES; j++)
+      if (j < nst) tile_gather(G + 256 * j, (tyslots >> (4 * j)) & 15, bd, od, hrow, gacc);
+    SYNC();
+    nst = 0;
+    tyslots = 0;
+    PROBE(6, stats, STAT_T_AUX1);
+  };
   while (tmask) {
-    int tys[HESS_TILES];
-#pragma unroll
-    for (int j = 0; j < HESS_TILES; j++) {
-      tys[j] = tmask ? __builtin_ctz(tmask) : -1;
+    {
+      const int t = __builtin_ctz(tmask);
       tmask &= tmask - 1u;
-    }
-#pragma unroll
-    for (int j = 0; j < HESS_TILES; j++) {
-      if (tys[j] < 0) break;
-      const int t = tys[j];
       const int r0 = E.tbase[t], r1 = E.tbase[t + 1];
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
       // MMX_HESS_U MFMA steps (one 4-row group each) per trip, loads first; the steps alternate
@@ -1665,17 +1699,12 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
       PROBE(6, stats, STAT_T_AUX0);
       // stage: lane l holds G[4 (l >> 4) + q][l & 15]
 #pragma unroll
-      for (int q = 0; q < 4; q++) G[256 * j + 16 * (4 * rk + q) + col] = acc0[q] + acc1[q];
+      for (int q = 0; q < 4; q++) G[256 * nst + 16 * (4 * rk + q) + col] = acc0[q] + acc1[q];
+      tyslots |= t << (4 * nst);
+      if (++nst == HESS_TILES) flush();
     }
-    SYNC();
-#pragma unroll
-    for (int j = 0; j < HESS_TILES; j++) {
-      if (tys[j] < 0) break;
-      tile_gather(G + 256 * j, tys[j], bd, od, hrow, gacc);
-    }
-    SYNC();
-    PROBE(6, stats, STAT_T_AUX1);
   }
+  flush();
   PROBE(6, stats, STAT_T_AUX2);
   return nd >= 0 ? gacc + mdx : 0.f;
 }
