@@ -747,12 +747,16 @@ DEV Geom geom_lds(const float* gx, int g) {
   for (int k = 0; k < 9; k++) G.R.m[k] = o[3 + k];
   return G;
 }
-// geoms of pair p ordered by type (plane first), as the narrowphase dispatch expects
-// (MMX_pair_packed is MMX_bodypair_geoms pre-sorted by the model compiler)
-DEV void pair_geoms(const float* gx, int p, int& g1, int& g2) {
-  const int pk = MMX_pair_packed[p];
-  g1 = pk & 255;
-  g2 = pk >> 8;
+// MMX_pair_packed[p]: the geoms of pair p ordered by type (plane first), as the narrowphase dispatch
+// expects (pre-sorted by the model compiler).  A candidate entry carries the pair index and both geom ids (p | g1 << 12 | g2 << 18), so the
+// passes after the sphere test decode them from LDS instead of gathering MMX_pair_packed (a
+// per-lane global-memory load) again.  Classes go above bit 24 (collide_prune's regrouping).
+static_assert(MMX_NPAIR < 4096 && MMX_NGEOM <= 64, "candidate entry packing");
+DEV int cand_pack(int p, int pk) { return p | ((pk & 255) << 12) | ((pk >> 8) << 18); }
+DEV void cand_unpack(int e, int& p, int& g1, int& g2) {
+  p = e & 4095;
+  g1 = (e >> 12) & 63;
+  g2 = (e >> 18) & 63;
 }
 DEV bool robot_obstacle(int g1, int g2) {
   const int c1 = MMX_geom_class[g1], c2 = MMX_geom_class[g2];
@@ -843,11 +847,20 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
   int nc = 0;
   if (use_list) {  // uniform: the list's pairs only (<= MMX_CAND_CAP, pair order)
     const int n = E.ncand;
-    for (int k0 = 0; k0 < n; k0 += WG) {
-      const int k = k0 + LANE;
-      const int p = k < n ? (int)E.cand[k] : 0;
-      const bool keep = k < n && sphere_test(p, MMX_pair_packed[p], 0.f);
-      nc = wave_compact(keep, cand, nc, p);
+    constexpr int NLP = (MMX_CAND_CAP + WG - 1) / WG;
+    int lp[NLP], lk[NLP];  // every pass's pair-table gather in flight at once
+#pragma unroll
+    for (int q = 0; q < NLP; q++) {
+      const int k = q * WG + LANE;
+      lp[q] = k < n ? (int)E.cand[k] : 0;
+      lk[q] = WG * q < n ? MMX_pair_packed[lp[q]] : 0;
+    }
+#pragma unroll
+    for (int q = 0; q < NLP; q++) {
+      if (WG * q >= n) break;  // uniform
+      const int k = q * WG + LANE;
+      const bool keep = k < n && sphere_test(lp[q], lk[q], 0.f);
+      nc = wave_compact(keep, cand, nc, cand_pack(lp[q], lk[q]));
     }
   } else {
   // all pairs: unrolled so the pair-table loads issue together
@@ -873,7 +886,7 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
     const unsigned long long m = km[q];
     if ((m >> LANE) & 1ull) {
       const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-      cand[nc + pos] = q * WG + LANE;
+      cand[nc + pos] = cand_pack(q * WG + LANE, pg[q]);
     }
     nc += __popcll(m);
     if (rebuild) {  // the inflated set -> the persistent list (pair order)
@@ -902,8 +915,8 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
     if (q * WG < nc) {
       if (k < nc) {
         p = cand[k];
-        int g1, g2;
-        pair_geoms(gx, p, g1, g2);
+        int pp, g1, g2;
+        cand_unpack(p, pp, g1, g2);
         const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
         if (A.type == GT_PLANE) c = 0;
         else if (obb_overlap(A, B, geom_half(gx, g1), geom_half(gx, g2))) c = (A.type == GT_BOX && B.type == GT_BOX) ? 1 : 2;
@@ -911,16 +924,16 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
 #pragma unroll
       for (int t = 0; t < 3; t++) ncls[t] += __popcll(__ballot(c == t));
     }
-    ce[q] = p | (c << 12);
+    ce[q] = p | (c << 24);  // (p: the packed candidate entry, 24 bits)
   }
   SYNC();
   int base[3] = {0, ncls[0], ncls[0] + ncls[1]};
 #pragma unroll
   for (int q = 0; q < NCP; q++) {
     if (q * WG < nc) {
-      const int c = ce[q] >> 12;
+      const int c = ce[q] >> 24;
 #pragma unroll
-      for (int t = 0; t < 3; t++) base[t] = wave_compact(c == t, cand, base[t], ce[q] & 4095);
+      for (int t = 0; t < 3; t++) base[t] = wave_compact(c == t, cand, base[t], ce[q] & 0xFFFFFF);
     }
   }
   if (LANE == 0) {
@@ -951,9 +964,8 @@ DEV void collide_pairs(EnvSh& E, bool only_ro, int which) {
   const int n0 = E.ncls[0], n1 = E.ncls[1], n2 = E.ncls[2];
   if (which & 1) {
     for (int k = LANE; k < n0; k += WG) {  // plane-box / plane-convex
-      const int p = cand[k];
-      int g1, g2;
-      pair_geoms(gx, p, g1, g2);
+      int p, g1, g2;
+      cand_unpack(cand[k], p, g1, g2);
       const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
       WaveSink cs(&E, p, !only_ro, g1, g2);
       if (B.type == GT_BOX) plane_box(cs, A, B, geom_half(gx, g2));
@@ -967,9 +979,8 @@ DEV void collide_pairs(EnvSh& E, bool only_ro, int which) {
     for (int k0 = 0; k0 < n1; k0 += WG / 4) {
       const int k = k0 + (LANE >> 2);
       if (k < n1) {
-        const int p = cand[n0 + k];
-        int g1, g2;
-        pair_geoms(gx, p, g1, g2);
+        int p, g1, g2;
+        cand_unpack(cand[n0 + k], p, g1, g2);
         const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
         WaveSink cs(&E, p, !only_ro, g1, g2);
         box_box_quad(cs, A, B, geom_half(gx, g1), geom_half(gx, g2), poly, poly + 8);
@@ -980,9 +991,8 @@ DEV void collide_pairs(EnvSh& E, bool only_ro, int which) {
     for (int k0 = 0; k0 < n1; k0 += COL_PLANES) {  // box-box
       const int k = k0 + LANE;
       if (LANE < COL_PLANES && k < n1) {
-        const int p = cand[n0 + k];
-        int g1, g2;
-        pair_geoms(gx, p, g1, g2);
+        int p, g1, g2;
+        cand_unpack(cand[n0 + k], p, g1, g2);
         const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
         WaveSink cs(&E, p, !only_ro, g1, g2);
         box_box(cs, A, B, geom_half(gx, g1), geom_half(gx, g2), poly, poly + 8);
@@ -994,9 +1004,8 @@ DEV void collide_pairs(EnvSh& E, bool only_ro, int which) {
   }
   if (which & 2) {
     for (int k = 0; k < n2; k++) {  // GJK / EPA
-      const int p = cand[n0 + n1 + k];
-      int g1, g2;
-      pair_geoms(gx, p, g1, g2);
+      int p, g1, g2;
+      cand_unpack(cand[n0 + n1 + k], p, g1, g2);
       const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
       WaveSink cs(&E, p, !only_ro, g1, g2);
       convex_convex(cs, A, B, scr + COL_EPA);
