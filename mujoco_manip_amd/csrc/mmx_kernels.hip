@@ -241,6 +241,9 @@ DEV bool arm_anc(int d, int b) { return d <= 6 ? (b >= d + 2 && b <= 11) : (d ==
 DEV unsigned anc_mask(int b) {
   return b >= 2 && b <= 11 ? ((1u << min(b - 1, 7)) - 1u) | (b == 10 ? 0x80u : 0u) | (b == 11 ? 0x100u : 0u) : 0u;
 }
+#ifndef MMX_DPP_FOLD
+#define MMX_DPP_FOLD 1  // DPP reads in the update_dpp form the combiner folds into VOP2 ops (0: mov_dpp, A/B)
+#endif
 #ifndef MMX_TYPE_BALLOT
 #define MMX_TYPE_BALLOT 1  // row-type bases from per-type ballots (0: packed prefix scans, A/B)
 #endif
@@ -264,9 +267,16 @@ DEV SV load_S(const EnvSh& E, int d) { return SV{V3{E.S[d][0], E.S[d][1], E.S[d]
 // ---------------------------------------------------------------- wave primitives
 // wave64 sum: DPP butterflies inside each row of 16 lanes, then the four row sums in a fixed
 // order (bit-identical in every lane, no LDS traffic)
+// (update_dpp with old = 0 and bound_ctrl: every control used here reads a valid lane, so the value
+// is the same as mov_dpp's, but LLVM's DPP combiner only folds this form into the consuming VOP2
+// op: v_add_f32_dpp instead of v_mov_b32_dpp + v_add_f32)
 template <int CTRL>
 DEV float dpp_f(float v) {
+#if MMX_DPP_FOLD
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
+#else
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+#endif
 }
 DEV float wave_sum(float v) {
   v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
@@ -1410,7 +1420,11 @@ __host__ __device__ constexpr int newton_lane(int d) { return d < 9 ? d : 16 * (
 // DPP row_newbcast:K, the value of lane K of each 16-lane row in every lane of that row
 template <int K>
 DEV float row_bcast_t(float v) {
+#if MMX_DPP_FOLD
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + K, 0xF, 0xF, true));
+#else
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + K, 0xF, 0xF, false));
+#endif
 }
 // k is a constant of a fully unrolled loop at every call: the switch folds to one DPP move
 DEV float row_bcast(float v, int k) {
