@@ -29,16 +29,21 @@
 
 #define WG 64  // lanes of the wave that runs a phase
 // lane within the wave; WAVE_ID: which of the env-step kernel's two waves (0 or 1)
-#ifdef MMX_LANE_OPAQUE  // experiment: lane id re-materialised per use (nothing lane-indexed hoists)
+// Lane id re-materialised per use (an opaque copy of threadIdx.x): nothing lane-derived (lane masks,
+// per-lane dof / row indices) is hoisted to a function's entry and kept live across it.  In the
+// Newton solver, where the substep's register peak sits, that frees registers: the substep's
+// callee-saved save area 592 -> 436 B per lane and most SGPR spills go, for fewer instructions
+// overall (C3 +2.4 % in the A/B); applied everywhere it costs more re-materialisation than it saves
+// (-0.6 %).  MMX_LANE_OPAQUE_SECTIONS selects the sections by bit (LANE_SECTION below).
 DEV int lane_opaque() {
   int t = (int)threadIdx.x;
   asm volatile("" : "+v"(t));
   return t & 63;
 }
-#define LANE lane_opaque()
-#else
-#define LANE ((int)(threadIdx.x & 63))
+#ifndef MMX_LANE_OPAQUE_SECTIONS
+#define MMX_LANE_OPAQUE_SECTIONS 0x10  // bit 0 kinematics, 1 dynamics, 2 collision, 3 constraints, 4 solver, 5 integrate, 6 IK
 #endif
+#define LANE ((int)(threadIdx.x & 63))
 #define WAVE_ID ((int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6))
 // SYNC: wave-local LDS ordering (a phase runs on ONE wave: its lanes exchange data through LDS,
 // whose operations a wave issues and completes in order, so no s_barrier / waitcnt is needed,
@@ -319,6 +324,12 @@ DEV void tri_index(int e, int& a, int& b) {
   b = e - aa * (aa + 1) / 2;
 }
 
+#undef LANE
+#if (MMX_LANE_OPAQUE_SECTIONS >> 0) & 1
+#define LANE lane_opaque()
+#else
+#define LANE ((int)(threadIdx.x & 63))
+#endif
 // ============================================================================ kinematics (lane 0)
 // mj_kinematics + arm motion subspaces (world-origin Plucker).  All joint anchors of this model
 // sit at the body origin (jnt_pos = 0).  Also refreshes the IK's kinematics cache.
@@ -441,6 +452,12 @@ DEV void kinematics_wave(EnvSh& E) {
   SYNC();
 }
 
+#undef LANE
+#if (MMX_LANE_OPAQUE_SECTIONS >> 1) & 1
+#define LANE lane_opaque()
+#else
+#define LANE ((int)(threadIdx.x & 63))
+#endif
 // ============================================================================ dynamics
 DEV RI body_inertia(const EnvSh& E, int b) {
   const V3 x = body_x(E, b);
@@ -664,6 +681,12 @@ DEV void dynamics_wave(EnvSh& E) {
   PROBE(11, stats, STAT_T_AUX3);
 }
 
+#undef LANE
+#if (MMX_LANE_OPAQUE_SECTIONS >> 2) & 1
+#define LANE lane_opaque()
+#else
+#define LANE ((int)(threadIdx.x & 63))
+#endif
 // ============================================================================ collision (wave)
 DEV Geom geom_pose(const EnvSh& E, int g) {
   Geom G;
@@ -1054,6 +1077,12 @@ DEV void collide_wave(EnvSh& E, bool only_ro) {
   if (!only_ro) collide_sort(E);
 }
 
+#undef LANE
+#if (MMX_LANE_OPAQUE_SECTIONS >> 3) & 1
+#define LANE lane_opaque()
+#else
+#define LANE ((int)(threadIdx.x & 63))
+#endif
 // ============================================================================ constraints (wave)
 // Soft-constraint reference terms of a row: K, B from solref, impedance from solimp (MuJoCo
 // mj_makeImpedance); D = 1 / R with R = (1 - imp) / imp * diag.
@@ -1397,6 +1426,12 @@ DEV void make_constraints_wave(EnvSh& E) {
   PROBE(3, stats, STAT_T_AUX2);
 }
 
+#undef LANE
+#if (MMX_LANE_OPAQUE_SECTIONS >> 4) & 1
+#define LANE lane_opaque()
+#else
+#define LANE ((int)(threadIdx.x & 63))
+#endif
 // ============================================================================ Newton solver (wave)
 // Primal Newton with exact line search (MuJoCo's default solver): minimise
 //   0.5 (x - xs)' M (x - xs) + sum_i s_i(J_i x - aref_i),  s_i = 0.5 D_i r^2 on active rows.
@@ -2236,6 +2271,12 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid, int& exit) 
   return it;
 }
 
+#undef LANE
+#if (MMX_LANE_OPAQUE_SECTIONS >> 5) & 1
+#define LANE lane_opaque()
+#else
+#define LANE ((int)(threadIdx.x & 63))
+#endif
 // ============================================================================ implicitfast + advance (wave)
 // Arm: (M - h qDeriv) qacc = qfrc_smooth + qfrc_constraint with qfrc_constraint = M (x - qacc_s),
 // qDeriv = -(damping + actuator kv where the force is unclamped), solved by a register Cholesky
@@ -2294,6 +2335,12 @@ DEV void integrate_wave(EnvSh& E) {
 
 // ============================================================================ implicitfast + advance (lane 0)
 
+#undef LANE
+#if (MMX_LANE_OPAQUE_SECTIONS >> 6) & 1
+#define LANE lane_opaque()
+#else
+#define LANE ((int)(threadIdx.x & 63))
+#endif
 // ============================================================================ IK (lane 0)
 DEV void orientation_error(const M3& Rc, V3& err) {  // controller.py:21-43, atan2 form for fp32
   float Em[9];
@@ -2469,6 +2516,8 @@ DEV void ik_wave(EnvSh& E) {
   SYNC();
 }
 
+#undef LANE
+#define LANE ((int)(threadIdx.x & 63))
 // ============================================================================ one mj_step
 DEV void mj_step_wave(int max_iter, float tol, EnvSh& E, float* con_dst) {
   float* stats = E.stats;
