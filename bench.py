@@ -15,7 +15,9 @@ the line reports the median window (all windows listed under "repeats").
 Multi-GPU: one process per GPU, weak scaling (4096 envs per rank), no data-path collective.
 Under torchrun the ranks come from the environment; `--gpus N` without torchrun starts the N
 rank processes itself (before anything touches a GPU) and relays rank 0's line.  Collectives:
-barrier, all_reduce(MAX) of the window time, all_reduce(SUM) of the episode counters.
+barrier, all_reduce(MAX) of the window time, all_reduce(SUM) of the episode counters, and after
+each window (untimed) an all_gather_into_tensor of every env's 16-byte episode record to rank 0
+(per-rank summaries in the line's `rank_envs`).
 """
 from __future__ import annotations
 
@@ -267,7 +269,7 @@ def main():
     if args.workload == "c2" and args.envs_per_gpu == 4096:
         args.envs_per_gpu = 1024
 
-    from mujoco_manip_amd.shard import dist_env, shard_seeds
+    from mujoco_manip_amd.shard import dist_env, env_stats_record, gather_env_stats, shard_seeds, summarize_env_stats
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
@@ -352,9 +354,14 @@ def main():
             rank_kern_ms = rk.tolist()
         else:
             rank_kern_ms = [kern_ms]
+        # SURVEY §8(e)'s logging collective, outside the timed region: every env's episode record
+        # (return, length, counters, FSM phase; 16 B per env) gathered to rank 0
+        rec = env_stats_record(env)
+        gathered = gather_env_stats(rec if cdev.type == "cuda" else rec.cpu(), dist, world)
+        env_summary = summarize_env_stats(gathered, world) if rank == 0 else None
         windows.append({"elapsed": elapsed, "kern_ms": kern_ms, "span_ms": span_ms, "render_ms": render_ms,
                         "launch_counts": [kt["step_launches"], kt["render_launches"]],
-                        "rank_kernel_ms": rank_kern_ms, "solver": solver,
+                        "rank_kernel_ms": rank_kern_ms, "solver": solver, "rank_envs": env_summary,
                         "episodes": {"completed": int(eps[0]), "successes": int(eps[1]), "placed": int(eps[2]),
                                      "error_resets": int(eps[3]), "envs_with_error_now": int(errs_now)}})
     isolated = None
@@ -444,6 +451,9 @@ def main():
             "render": render,
             "cpu_baseline": cpu,
             "solver": solver,
+            # per-rank summaries of the per-env episode records gathered to rank 0 after the median
+            # window (all_gather_into_tensor over the default group: RCCL on N GPUs)
+            "rank_envs": med["rank_envs"],
         }
         print(json.dumps(line), flush=True)
     if dist:

@@ -156,11 +156,13 @@ int mmx_kernel_times(mmx_sim* sim, float* step_ms, int32_t* step_launches, float
 
 /* Batched PNG encoder (dataset emission, generate_dataset.py:250-260: LeRobot embeds image
  * features as PNG files).  Encodes n RGB8 images (device, image i at rgb_dev + i * img_stride,
- * rows of 3 * width bytes, height <= 1024) into complete PNG files: image i's file is written at
+ * rows of 3 * width bytes, height <= 1024, width <= MMX_PNG_MAX_WIDTH: the encoder's row-above match
+ * uses deflate distance 3 * width + 1, capped at 32768) into complete PNG files: image i's file is written at
  * out_dev + i * out_stride (out_stride >= mmx_png_bound(width, height)) and its byte size to
  * sizes_dev[i] (int32).  scratch_dev: n * mmx_png_scratch(width, height) bytes of device memory.
  * mmx_png_pack copies the n files back to back into packed_dev at offsets_dev[i] (int64, device).
  * Asynchronous on the sim's stream; bounds return -1 for unsupported sizes. */
+#define MMX_PNG_MAX_WIDTH 10922
 int64_t mmx_png_bound(int32_t width, int32_t height);
 int64_t mmx_png_scratch(int32_t width, int32_t height);
 int mmx_png_encode(mmx_sim* sim, const uint8_t* rgb_dev, int64_t img_stride, int32_t n, int32_t width,

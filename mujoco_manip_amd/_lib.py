@@ -17,6 +17,7 @@ from . import _build
 
 NQ, NV, NU, NOBS = 30, 27, 8, 85
 MAXCON, CON_F = 64, 13
+PNG_MAX_WIDTH = 10922  # include/mmx_api.h MMX_PNG_MAX_WIDTH
 EPI_N, EPF_N, KIN_N, STAT_N = 18, 28, 63, 19
 EPI_FIELDS = ("obj", "bin", "step_count", "flags", "fsm_state", "fsm_task_index", "fsm_settle", "fsm_gripper_open",
               "fsm_has_target", "env_error", "ncon", "nefc", "episodes", "rng_has32", "successes", "placed", "error_resets",
@@ -253,10 +254,27 @@ class Sim:
         assert c == 3 and images.dtype == torch.uint8 and images.is_cuda
         if n == 0:
             return torch.empty(0, dtype=torch.uint8, device=images.device), np.zeros(1, np.int64)
-        imgs = images.contiguous()
         bound, scr = int(self.L.mmx_png_bound(W, H)), int(self.L.mmx_png_scratch(W, H))
         if bound < 0:
             raise ValueError(f"unsupported image size {W} x {H}")
+        # the encoder runs on the sim's stream: the buffers, the size scan and the read-back are
+        # ordered on that stream too (and the caller's stream waits for the result), whatever
+        # stream the caller is on
+        cur = torch.cuda.current_stream(images.device)
+        sst = (torch.cuda.ExternalStream(self.cfg.stream, device=images.device) if self.cfg.stream
+               else torch.cuda.default_stream(images.device))
+        sst.wait_stream(cur)
+        with torch.cuda.stream(sst):
+            imgs = images.contiguous()
+            images.record_stream(sst)
+            packed, offs = self._png_encode_on_stream(imgs, n, H, W, bound, scr, max_batch)
+        cur.wait_stream(sst)
+        packed.record_stream(cur)
+        return packed, offs
+
+    def _png_encode_on_stream(self, imgs, n, H, W, bound, scr, max_batch):
+        import torch
+
         dev = imgs.device
         parts, offs = [], [0]
         for b0 in range(0, n, max_batch):

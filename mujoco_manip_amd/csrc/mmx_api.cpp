@@ -167,6 +167,7 @@ T* dalloc(mmx_sim* sim, size_t count) {
 }  // namespace
 
 namespace {
+static constexpr size_t kTimingPoolPresize = 2048;
 // an event of the timing pool recorded on `st` (its index), or SIZE_MAX when the pool cannot grow
 size_t timing_mark(mmx_sim* sim, hipStream_t st) {
   if (sim->ev_used == sim->ev_pool.size()) {
@@ -417,6 +418,13 @@ int mmx_kernel_timing(mmx_sim* sim, int32_t enable) {
     sim->ev_used = 0;
     sim->t_step.clear();
     sim->t_render.clear();
+    // pre-size the pool, so no hipEventCreate runs between the launches of a timed window (2 events
+    // per launch: a C5 window of 128 env steps on 4 lanes records 2048)
+    while (sim->ev_pool.size() < kTimingPoolPresize) {
+      hipEvent_t ev;
+      if (hipEventCreate(&ev) != hipSuccess) break;
+      sim->ev_pool.push_back(ev);
+    }
   }
   sim->timing = enable != 0;
   return MMX_OK;
@@ -500,17 +508,21 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
 
 int mmx_rollout_lanes(const mmx_sim* sim) { return sim ? sim->nlanes : 0; }
 
+// the row-above match uses deflate distance 3 W + 1, which deflate caps at 32768: W <= 10922
+static bool png_size_ok(int32_t width, int32_t height) {
+  return width > 0 && height > 0 && height <= 1024 && width <= MMX_PNG_MAX_WIDTH;
+}
 int64_t mmx_png_bound(int32_t width, int32_t height) {
-  return width > 0 && height > 0 && height <= 1024 ? mmx_png_bound_bytes(width, height) : -1;
+  return png_size_ok(width, height) ? mmx_png_bound_bytes(width, height) : -1;
 }
 int64_t mmx_png_scratch(int32_t width, int32_t height) {
-  return width > 0 && height > 0 && height <= 1024 ? mmx_png_scratch_bytes(width, height) : -1;
+  return png_size_ok(width, height) ? mmx_png_scratch_bytes(width, height) : -1;
 }
 
 int mmx_png_encode(mmx_sim* sim, const uint8_t* rgb_dev, int64_t img_stride, int32_t n, int32_t width, int32_t height,
                    uint8_t* out_dev, int64_t out_stride, int32_t* sizes_dev, void* scratch_dev) {
-  if (!sim || n < 0 || (n > 0 && (!rgb_dev || !out_dev || !sizes_dev || !scratch_dev)) || width <= 0 || height <= 0 ||
-      height > 1024 || img_stride < 3LL * width * height || out_stride < mmx_png_bound_bytes(width, height))
+  if (!sim || n < 0 || (n > 0 && (!rgb_dev || !out_dev || !sizes_dev || !scratch_dev)) || !png_size_ok(width, height) ||
+      img_stride < 3LL * width * height || out_stride < mmx_png_bound_bytes(width, height))
     return sim ? fail(sim, MMX_EINVAL, "mmx_png_encode: bad arguments") : MMX_EINVAL;
   DeviceGuard guard(sim);
   return hip_check(sim, mmx_launch_png(rgb_dev, img_stride, n, width, height, out_dev, out_stride, sizes_dev,

@@ -229,6 +229,20 @@ def episode_seeds(seed: int, num_episodes: int) -> list[int]:
     return [_lib.episode_seed(seed, e) for e in range(num_episodes)]
 
 
+def rank_episodes(num_episodes: int, rank: int = 0, world_size: int = 1) -> list[int]:
+    """Global episode indices a rank generates when the dataset is sharded over `world_size`
+    processes (one per GPU): e = rank (mod world_size).  An episode keeps its global
+    seed and task (generate_dataset.py:263-277), so the frames do not depend on the rank count."""
+    if not (0 <= rank < world_size):
+        raise ValueError(f"bad shard: rank {rank} of {world_size}")
+    return list(range(rank, int(num_episodes), world_size))
+
+
+def shard_dir(path: str, rank: int, world_size: int) -> str:
+    """Where rank `rank` of `world_size` writes its LeRobot shard inside the dataset directory."""
+    return os.path.join(path, f"shard-{rank:03d}-of-{world_size:03d}")
+
+
 class _PinnedRing:
     """Pinned host staging for the per-step frame copies: device tensors are copied with
     non_blocking=True on a side stream that waits for the producing stream, an event marks
@@ -284,13 +298,23 @@ def _raw_image_stats(frames_u8: list) -> dict:
             "_sum": x.sum(0).tolist(), "_sumsq": (x * x).sum(0).tolist(), "_n": int(len(x))}
 
 
-def _frame_image_stats(imgs):
+def _frame_image_stats(imgs, chunk=256):
     """Per-frame channel statistics of uint8 images [k, H, W, 3] on the device: min, max, sum and
-    sum of squares of the pixel values scaled to [0, 1] -> float64 [k, 4, 3]."""
+    sum of squares of the pixel values scaled to [0, 1] -> float64 [k, 4, 3].  Min / max on the
+    uint8 values, sums exact in integers (int32 values, int64 sums) and scaled at the end, in
+    chunks of `chunk` images (no float64 copy of the frames)."""
     import torch
 
-    x = imgs.reshape(imgs.shape[0], -1, 3).to(torch.float64) * (1.0 / 255.0)
-    return torch.stack([x.amin(1), x.amax(1), x.sum(1), (x * x).sum(1)], 1)
+    k = imgs.shape[0]
+    x = imgs.reshape(k, -1, 3)
+    out = torch.empty((k, 4, 3), dtype=torch.float64, device=imgs.device)
+    out[:, 0] = x.amin(1).to(torch.float64) * (1.0 / 255.0)
+    out[:, 1] = x.amax(1).to(torch.float64) * (1.0 / 255.0)
+    for a in range(0, k, chunk):
+        xi = x[a:a + chunk].to(torch.int32)
+        out[a:a + chunk, 2] = xi.sum(1, dtype=torch.int64).to(torch.float64) * (1.0 / 255.0)
+        out[a:a + chunk, 3] = (xi * xi).sum(1, dtype=torch.int64).to(torch.float64) * (1.0 / (255.0 * 255.0))
+    return out
 
 
 def _merge_image_stats(fs: np.ndarray, npx: int) -> dict:
@@ -307,8 +331,10 @@ def _merge_image_stats(fs: np.ndarray, npx: int) -> dict:
 
 def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type="staged", randomize_objects=False,
                      seed=0, spawn_x_range=(-0.20, 0.20), spawn_y_range=(0.30, 0.45), num_envs=1024, device=0,
-                     max_gym_steps=5000, on_step=None, sink=None, image_size=IMAGE_SIZE):
-    """Run `num_episodes` reference run_episode loops (generate_dataset.py:83-198) side by side.
+                     max_gym_steps=5000, on_step=None, sink=None, image_size=IMAGE_SIZE, episode_ids=None):
+    """Run `num_episodes` reference run_episode loops (generate_dataset.py:83-198) side by side,
+    or, with `episode_ids`, only those episodes of the `num_episodes`-episode job (a rank's shard,
+    rank_episodes): each keeps its global index, seed and task.
 
     Streaming: each step's frames (active slots only) are gathered on the device, copied to pinned
     host memory on a side stream and split into their episodes on the host.  Camera frames are
@@ -324,8 +350,13 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
 
     from .vec_env import PickPlaceVecEnv
 
-    E = int(num_episodes)
-    seeds = episode_seeds(seed, E) if randomize_objects else None
+    seeds = episode_seeds(seed, int(num_episodes)) if randomize_objects else None
+    ids = list(range(int(num_episodes))) if episode_ids is None else [int(g) for g in episode_ids]
+    if any(not 0 <= g < int(num_episodes) for g in ids):
+        raise ValueError(f"episode ids must lie in [0, {num_episodes})")
+    E = len(ids)
+    if E == 0:
+        return ([] if sink is None else None), seeds
     N = max(1, min(int(num_envs), E))
     use_images = bool(set(feature_keys) & set(IMAGE_KEYS))
     env = PickPlaceVecEnv(N, tasks=[tuple(t) for t in task_list], action_mode="abs_pos", reward_type=reward_type,
@@ -339,7 +370,8 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
     img_feats = [(cam, f) for cam, f in enumerate(IMAGE_KEYS) if f in feature_keys]
     npx = image_size * image_size
 
-    eps = [Episode(e, *task_list[e % len(task_list)], seeds[e] if seeds else None) for e in range(E)]
+    # local position e <-> global episode ids[e]: slots and rows are indexed locally
+    eps = [Episode(g, *task_list[g % len(task_list)], seeds[g] if seeds else None) for g in ids]
     rows = [dict() for _ in range(E)]  # episode -> "_rows": [(step id, row)], image key -> [PNG bytes]
     slot_ep = np.full(N, -1, np.int64)
     next_ep = 0
@@ -471,7 +503,7 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
                     frame[k] = enc[k]
         frame["_fsm"] = fsm_view.index_select(0, idx)
         if on_step is not None:
-            on_step(act_slots, slot_ep[act_slots].copy(), env)
+            on_step(act_slots, np.asarray(ids, np.int64)[slot_ep[act_slots]], env)
         env.step(action)
         if need_reward:
             frame["next.reward"] = env._rc.index_select(0, idx)
@@ -509,7 +541,7 @@ class LeRobotWriter:
 
     def __init__(self, root: str, repo_id: str, features: dict, *, fps=CONTROL_FPS, robot_type="franka_panda",
                  chunks_size=1000, data_files_size_in_mb=100, threaded=False, queue_depth=64,
-                 image_compression="SNAPPY"):
+                 image_compression="SNAPPY", keep_image_sums=False):
         import pyarrow as pa
         import pyarrow.parquet  # noqa: F401  (imported here, not on the first episode)
 
@@ -530,6 +562,9 @@ class LeRobotWriter:
         self.img_acc = {}  # feature -> [min, max, sum, sumsq, pixels, frames]
         self.n_episodes = 0
         self.image_compression = image_compression
+        # shards keep each episode's raw image sums in meta/episodes, so merge_shards rebuilds the
+        # dataset statistics bit for bit
+        self.keep_image_sums = keep_image_sums
         # threaded: episodes go through a bounded queue to one writer thread (the reference writes
         # with background threads too, generate_dataset.py:260); parquet encoding and the file write
         # release the GIL, so they overlap the collection loop.  Episode order is kept.
@@ -663,6 +698,9 @@ class LeRobotWriter:
             for name in ("min", "max", "mean", "std"):
                 row[f"stats/{k}/{name}"] = st[name]
             row[f"stats/{k}/count"] = [int(ep.length)]
+            if self.keep_image_sums:
+                row[f"stats/{k}/_sum"], row[f"stats/{k}/_sumsq"] = list(st["_sum"]), list(st["_sumsq"])
+                row[f"stats/{k}/_n"] = int(st["_n"])
             mn = np.array([c[0][0] for c in st["min"]])
             mx = np.array([c[0][0] for c in st["max"]])
             acc = self.img_acc.get(k)
@@ -764,32 +802,126 @@ def read_lerobot_v3(root: str):
 
 
 # ----------------------------------------------------------------------------- entry point
+def _features_at(feats: dict, image_size: int) -> dict:
+    """The feature schema with the image features at the rendered size (features.py:11-20 states
+    224 x 224; the renderer takes any size)."""
+    return {k: (dict(v, shape=(image_size, image_size, 3)) if v["dtype"] == "image" else v) for k, v in feats.items()}
+
+
 def generate(repo_id, num_episodes=100, root="./datasets", task=None, tasks="all", reward_type="staged",
              randomize_objects=False, seed=0, spawn_x_range=(-0.20, 0.20), spawn_y_range=(0.30, 0.45),
-             features=None, num_envs=1024, device=0, image_size=IMAGE_SIZE):
+             features=None, num_envs=1024, device=0, image_size=IMAGE_SIZE, rank=0, world_size=1):
     """generate_dataset.main (generate_dataset.py:201-333) with the episodes batched on the GPU and
-    streamed to the LeRobot writer as they finish."""
+    streamed to the LeRobot writer as they finish.
+
+    Sharded (world_size > 1, one process per GPU): rank r generates the episodes
+    e = r (mod world_size) with their global seeds and tasks and writes them as a LeRobot dataset
+    of its own in `<root>/<repo_id>/shard-RRR-of-WWW` (local episode indices 0..n-1, the global
+    ones in its metadata.json under "shard"); merge_shards then writes the dataset a single
+    process would have written.  Returns (path written, info)."""
     if not repo_id:
         raise ValueError("repo_id is required (e.g. repo_id=user/pick-place)")
     task_list = resolve_tasks(task, tasks)
-    feats = resolve_features(features, reward_type)
+    feats = _features_at(resolve_features(features, reward_type), image_size)
     path = os.path.join(root, repo_id)
-    writer = LeRobotWriter(path, repo_id, feats, threaded=True)
+    ids = rank_episodes(num_episodes, rank, world_size)
+    out = path if world_size == 1 else shard_dir(path, rank, world_size)
+    writer = LeRobotWriter(out, repo_id, feats, threaded=True, keep_image_sums=world_size > 1)
+    local = []
+
+    def sink(ep):  # shard-local episode numbering (a LeRobot dataset counts from 0)
+        local.append(ep.index)
+        ep.index = len(local) - 1
+        writer.add_episode(ep)
+
     _, seeds = collect_episodes(num_episodes, task_list, set(feats), reward_type=reward_type,
                                 randomize_objects=randomize_objects, seed=seed, spawn_x_range=spawn_x_range,
-                                spawn_y_range=spawn_y_range, num_envs=num_envs, device=device, sink=writer.add_episode,
-                                image_size=image_size)
+                                spawn_y_range=spawn_y_range, num_envs=num_envs, device=device, sink=sink,
+                                image_size=image_size, episode_ids=ids)
     cfg = {"repo_id": repo_id, "num_episodes": int(num_episodes), "root": root,
            "task": list(task) if task is not None else None, "tasks": tasks, "reward_type": reward_type,
            "randomize_objects": bool(randomize_objects), "seed": int(seed), "spawn_x_range": list(spawn_x_range),
            "spawn_y_range": list(spawn_y_range), "push_to_hub": False, "private": True,
            "features": list(features) if features is not None else None}
+    if image_size != IMAGE_SIZE:
+        cfg["image_size"] = int(image_size)
     if seeds is not None:
         cfg["episode_seeds"] = [int(s) for s in seeds]
+    md = cfg if world_size == 1 else dict(cfg, shard={"rank": int(rank), "world_size": int(world_size),
+                                                      "global_episode_index": local})
+    info = writer.close(extra_info={"generation_config": md})
+    with open(os.path.join(out, "metadata.json"), "w") as f:
+        json.dump(md, f, indent=2)
+    return out, info
+
+
+def _shard_episodes(sdir: str, feats: dict, global_ids: list, seeds):
+    """Episodes of one shard in its (global-index increasing) order, read file by file: Episode
+    objects with their global index, PNG bytes as stored and the image statistics the writer kept."""
+    import pyarrow.parquet as pq
+
+    info = json.load(open(os.path.join(sdir, "meta", "info.json")))
+    rows = pq.read_table(os.path.join(sdir, "meta", "episodes", "chunk-000", "file-000.parquet")).to_pylist()
+    by_task = {make_task_string(o, b): (o, b) for o in OBJECTS for b in BINS}
+    cur_key, tab, epi = None, None, None
+    for row in sorted(rows, key=lambda r: r["episode_index"]):
+        key = (row["data/chunk_index"], row["data/file_index"])
+        if key != cur_key:
+            cur_key = key
+            tab = pq.read_table(os.path.join(sdir, info["data_path"].format(chunk_index=key[0], file_index=key[1])))
+            epi = tab.column("episode_index").to_numpy()
+        sel = np.where(epi == row["episode_index"])[0]
+        g = int(global_ids[row["episode_index"]])
+        obj, bin_ = by_task[row["tasks"][0]]
+        ep = Episode(g, obj, bin_, int(seeds[g]) if seeds else None, length=int(row["length"]))
+        part = tab.take(sel)
+        for k, f in feats.items():
+            col = part.column(k).combine_chunks()
+            if f["dtype"] == "float32":
+                ep.frames[k] = np.asarray(col.flatten(), np.float32).reshape(len(sel), -1)
+            elif f["dtype"] == "string":
+                ep.frames[k] = col.to_pylist()
+            else:
+                ep.frames[k] = col.field("bytes").to_pylist()
+                ep.image_stats[k] = {n: row[f"stats/{k}/{n}"] for n in ("min", "max", "mean", "std", "_sum", "_sumsq",
+                                                                        "_n")}
+        yield ep
+
+
+def merge_shards(path: str, remove_shards: bool = False):
+    """Merge the LeRobot shards a sharded generate() wrote under `path` into the dataset one
+    process would have written there (episodes in global order, global indices, the same
+    statistics and metadata bit for bit).  Streams: one data file per shard is held at a time."""
+    import heapq
+    import shutil
+
+    sdirs = sorted(d for d in (os.path.join(path, x) for x in os.listdir(path)) if os.path.basename(d).startswith("shard-"))
+    if not sdirs:
+        raise ValueError(f"no shards under {path}")
+    mds = [json.load(open(os.path.join(d, "metadata.json"))) for d in sdirs]
+    world = mds[0]["shard"]["world_size"]
+    if len(sdirs) != world or sorted(m["shard"]["rank"] for m in mds) != list(range(world)):
+        raise ValueError(f"expected {world} shards, found ranks {[m['shard']['rank'] for m in mds]}")
+    cfg = {k: v for k, v in mds[0].items() if k != "shard"}
+    feats = _features_at(resolve_features(cfg["features"], cfg["reward_type"]), cfg.get("image_size", IMAGE_SIZE))
+    seeds = cfg.get("episode_seeds")
+    writer = LeRobotWriter(path, cfg["repo_id"], feats, threaded=True)
+    streams = [_shard_episodes(d, feats, m["shard"]["global_episode_index"], seeds) for d, m in zip(sdirs, mds)]
+    n = 0
+    for ep in heapq.merge(*streams, key=lambda e: e.index):
+        if ep.index != n:
+            raise ValueError(f"episode {n} missing from the shards (next is {ep.index})")
+        writer.add_episode(ep)
+        n += 1
+    if n != cfg["num_episodes"]:
+        raise ValueError(f"shards hold {n} of {cfg['num_episodes']} episodes")
     info = writer.close(extra_info={"generation_config": cfg})
     with open(os.path.join(path, "metadata.json"), "w") as f:
         json.dump(cfg, f, indent=2)
-    return path, info
+    if remove_shards:
+        for d in sdirs:
+            shutil.rmtree(d)
+    return info
 
 
 def main(argv=None):
@@ -805,10 +937,41 @@ def main(argv=None):
     ap.add_argument("--spawn-x-range", type=float, nargs=2, default=(-0.20, 0.20))
     ap.add_argument("--spawn-y-range", type=float, nargs=2, default=(0.30, 0.45))
     ap.add_argument("--features", nargs="*", default=None)
-    ap.add_argument("--num-envs", type=int, default=1024)
+    ap.add_argument("--num-envs", type=int, default=1024, help="parallel envs per GPU")
+    ap.add_argument("--image-size", type=int, default=IMAGE_SIZE)
+    ap.add_argument("--no-merge", action="store_true", help="sharded run: keep the per-rank shards only")
+    ap.add_argument("--dist-backend", default=None, help="sharded run: collective backend (default nccl = RCCL)")
     a = ap.parse_args(argv)
+    # one process per GPU under torchrun (RANK / LOCAL_RANK / WORLD_SIZE): each rank writes its
+    # shard, a gather of the per-rank summaries (the only collective) tells rank 0 they are done
+    rank, local_rank, world = (int(os.environ.get(k, d)) for k, d in (("RANK", 0), ("LOCAL_RANK", 0), ("WORLD_SIZE", 1)))
+    import time
+
+    t0 = time.perf_counter()
     path, info = generate(a.repo_id, a.num_episodes, a.root, a.task, a.tasks, a.reward_type, a.randomize_objects,
-                          a.seed, a.spawn_x_range, a.spawn_y_range, a.features, a.num_envs)
+                          a.seed, a.spawn_x_range, a.spawn_y_range, a.features, a.num_envs, device=local_rank,
+                          image_size=a.image_size, rank=rank, world_size=world)
+    summary = [float(info["total_episodes"]), float(info["total_frames"]), time.perf_counter() - t0]
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+
+        backend = a.dist_backend or ("nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group(backend)
+        dev = torch.device("cuda", local_rank) if backend == "nccl" else torch.device("cpu")
+        mine = torch.tensor(summary, dtype=torch.float64, device=dev)
+        every = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(every, mine)
+        dist.destroy_process_group()
+        if rank != 0:
+            return
+        per_rank = [t.cpu().tolist() for t in every]
+        print(json.dumps({"shards": [{"rank": r, "episodes": int(e), "frames": int(f), "seconds": round(s, 3)}
+                                     for r, (e, f, s) in enumerate(per_rank)]}))
+        if a.no_merge:
+            return
+        info = merge_shards(os.path.join(a.root, a.repo_id))
+        path = os.path.join(a.root, a.repo_id)
     print(f"Dataset saved to {path}: {info['total_episodes']} episodes, {info['total_frames']} frames")
 
 

@@ -39,9 +39,13 @@ def decode_targets(mode: str, actions, T_init):
 
 
 def episode_setup(metadata, episode_index: int):
-    """replay_actions.py:74-100: (seed or None, (obj, bin) or None, spawn_x, spawn_y)."""
+    """replay_actions.py:74-100: (seed or None, (obj, bin) or None, spawn_x, spawn_y).  A shard of a
+    sharded generation (dataset.generate with world_size > 1) numbers its episodes locally: the
+    global index its seed and task belong to is in metadata["shard"]."""
     spawn_x, spawn_y = (-0.20, 0.20), (0.30, 0.45)
     seed, task = None, None
+    if metadata is not None and "shard" in metadata:
+        episode_index = int(metadata["shard"]["global_episode_index"][episode_index])
     if metadata is not None:
         seeds = metadata.get("episode_seeds")
         if seeds and episode_index < len(seeds):

@@ -16,7 +16,7 @@ sys.path.insert(0, REPO)
 def main():
     n, steps, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
     from mujoco_manip_amd import _lib
-    from mujoco_manip_amd.shard import dist_env, shard_seeds
+    from mujoco_manip_amd.shard import dist_env, env_stats_record, gather_env_stats, shard_seeds
     from mujoco_manip_amd.vec_env import PickPlaceVecEnv
 
     rank, _, world = dist_env()
@@ -31,8 +31,9 @@ def main():
     local = torch.from_numpy(np.concatenate([q, v, epi.view(np.float32)], 1))
     gathered = [torch.zeros_like(local) for _ in range(world)]
     dist.all_gather(gathered, local)
+    stats = gather_env_stats(env_stats_record(env).cpu(), dist, world)  # the bench's logging gather
     if rank == 0:
-        np.savez(out, rows=torch.cat(gathered).numpy())
+        np.savez(out, rows=torch.cat(gathered).numpy(), stats=stats.numpy())
     dist.destroy_process_group()
     env.close()
 

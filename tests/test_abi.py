@@ -75,6 +75,7 @@ def test_state_layout_constants_match_header():
     assert enum_count("STAT_NEFC", "STAT_N") == _lib.STAT_N == len(_lib.STAT_FIELDS)
     hdr = open(os.path.join(REPO, "include", "mmx_api.h")).read()
     assert f"[N][{_lib.MAXCON}][{_lib.CON_F}]" in hdr and f"[N][{_lib.STAT_N}]" in hdr
+    assert f"#define MMX_PNG_MAX_WIDTH {_lib.PNG_MAX_WIDTH}" in hdr and 3 * _lib.PNG_MAX_WIDTH + 1 <= 32768
 
 
 def test_obs_layout_covers_reference_keys():

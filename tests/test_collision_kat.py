@@ -114,6 +114,34 @@ def scene_cube_on_cube(m):
     return q, [dict(pair=ordered(m, a, b, [0, 0, 1]), depth=d, pts=pts)]
 
 
+def scene_cube_on_cube_turned(m):
+    """Green cube centred on the red one, turned 45 deg about z, 0.7 mm deep: the overlap of the
+    two squares is a regular octagon (the turned square's edges |x| + |y| = h sqrt 2 cut the
+    lower one's |x| = h, |y| = h at (sqrt 2 - 1) h): 8 contacts at its corners."""
+    q = parked(m)
+    x0, y0, z0, d = -0.6, -0.3, 0.9, 0.0007
+    put_cube(q, 0, [x0, y0, z0])
+    put_cube(q, 1, [x0, y0, z0 + 2 * H - d], axis_rot([0, 0, 1], np.pi / 4))
+    s = (np.sqrt(2) - 1) * H
+    pts = [[x0 + a, y0 + b, z0 + H - d / 2] for a, b in ((H, s), (H, -s), (-H, s), (-H, -s), (s, H), (-s, H),
+                                                         (s, -H), (-s, -H))]
+    return q, [dict(pair=ordered(m, m.find("obj_red", "box"), m.find("obj_green", "box"), [0, 0, 1]), depth=d,
+                    pts=pts)]
+
+
+def scene_cube_edge_on_edge(m):
+    """Red cube turned 45 deg about x (top edge along x), green cube above it turned 45 deg about
+    y (bottom edge along y), the edges crossing 0.9 mm deep: the edge-edge axis (z) is the
+    separating-axis minimum, one contact at the midpoint of the edges' closest points."""
+    q = parked(m)
+    x0, y0, z0, d = 0.5, 0.9, 0.7, 0.0009
+    r2 = H * np.sqrt(2)
+    put_cube(q, 0, [x0, y0, z0], axis_rot([1, 0, 0], np.pi / 4))
+    put_cube(q, 1, [x0, y0, z0 + 2 * r2 - d], axis_rot([0, 1, 0], np.pi / 4))
+    return q, [dict(pair=ordered(m, m.find("obj_red", "box"), m.find("obj_green", "box"), [0, 0, 1]), depth=d,
+                    pts=[[x0, y0, z0 + r2 - d / 2]])]
+
+
 def scene_cube_edge_on_table(m):
     """A cube turned 45 deg about x, balanced on its lower edge on the tabletop 0.8 mm deep: two
     contacts at the edge's end corners, normal +z (table -> cube)."""
@@ -209,7 +237,7 @@ def scene_cube_against_leg(m):
                     depth=d, pts=pts, convex=True)]
 
 
-BOX_SCENES = [scene_cube_on_cube, scene_cube_edge_on_table, scene_cube_in_bin_corner, scene_pad_clamp,
+BOX_SCENES = [scene_cube_on_cube, scene_cube_on_cube_turned, scene_cube_edge_on_edge, scene_cube_edge_on_table, scene_cube_in_bin_corner, scene_pad_clamp,
               scene_cube_tilted_on_floor, scene_cube_against_leg]
 
 

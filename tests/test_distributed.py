@@ -81,6 +81,51 @@ def test_two_rank_sharding_matches_single_process():
     np.testing.assert_array_equal(gathered, single)
 
 
+def _stats_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mujoco_manip_amd.shard import gather_env_stats, summarize_env_stats
+
+    local = _synthetic_records(range(rank * 3, rank * 3 + 3))
+    got = gather_env_stats(local, dist, world)
+    if rank == 0:
+        q.put((got.numpy(), summarize_env_stats(got, world)))
+    dist.destroy_process_group()
+
+
+def _synthetic_records(env_ids):
+    """Per-env episode records as env_stats_record packs them, a function of the global env id."""
+    rows = []
+    for g in env_ids:
+        ret = np.array([0.25 * g - 1.0], np.float32).view(np.int32)[0]
+        rows.append([ret, 10 + g, g % 2, (g % 11) | ((g % 3) << 8) | ((g % 2) << 20)])
+    return torch.tensor(rows, dtype=torch.int32)
+
+
+def test_two_rank_env_stats_gather_matches_single_process():
+    """SURVEY §8(e)'s logging collective: the per-env episode records (16 B per env) gathered to
+    rank 0 over the default group equal one process's records, and the per-rank summaries follow."""
+    from mujoco_manip_amd.shard import summarize_env_stats, unpack_env_stats
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stats_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got, summ = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+    single = _synthetic_records(range(6))
+    np.testing.assert_array_equal(got, single.numpy())
+    u = unpack_env_stats(single)
+    assert summ[1]["successes"] == int(u["successes"][3:].sum()) and summ[0]["envs"] == 3
+    assert summ == summarize_env_stats(single, 2)
+    assert abs(summ[0]["mean_return"] - np.mean([-1.0, -0.75, -0.5])) < 1e-7
+    assert sum(summ[0]["fsm_phase_hist"]) == 3 and summ[1]["placed"] == sum(g % 3 for g in range(3, 6))
+
+
 def test_shard_ranges_and_seeds():
     from mujoco_manip_amd import _lib
     from mujoco_manip_amd.shard import shard_range, shard_seeds
@@ -138,7 +183,7 @@ def test_two_rank_hip_rollout_matches_single_process(tmp_path):
                               env=dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2",
                                        MASTER_ADDR="127.0.0.1", MASTER_PORT=port)) for r in range(2)]
     assert [p.wait(timeout=240) for p in procs] == [0, 0]
-    ranks = np.load(out)["rows"]
+    ranks, stats = np.load(out)["rows"], np.load(out)["stats"]
     env = PickPlaceVecEnv(2 * n, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
                           image_size=0, autoreset=True)
     env.reset(seed=[_lib.episode_seed(42, g) for g in range(2 * n)])
@@ -147,3 +192,6 @@ def test_two_rank_hip_rollout_matches_single_process(tmp_path):
     q, v, _, _ = env.sim.get_state()
     epi = env.sim.view("episode_i", _lib.EPI_N, "<i4").cpu().numpy()
     np.testing.assert_array_equal(ranks, np.concatenate([q, v, epi.view(np.float32)], 1))
+    from mujoco_manip_amd.shard import env_stats_record
+
+    np.testing.assert_array_equal(stats, env_stats_record(env).cpu().numpy())  # §8(e) gather

@@ -103,3 +103,37 @@ def test_png_rendered_frames_compress(sim):
     print(f"mean PNG {sz.mean():.0f} B, compression {ratio:.1f}x")
     assert ratio > 3.0
     env.close()
+
+
+def test_png_width_limit(sim):
+    """The row-above match's deflate distance 3 W + 1 must stay <= 32768: the widest accepted
+    image (W = 10922) round-trips, one pixel wider is rejected up front."""
+    from mujoco_manip_amd import _lib
+
+    rng = np.random.default_rng(7)
+    im = rng.integers(0, 256, (1, 3, _lib.PNG_MAX_WIDTH, 3), dtype=np.uint8)
+    im[0, 1] = im[0, 0]  # a whole row repeated: the match at the maximum distance
+    _check(sim, im)
+    assert sim.L.mmx_png_bound(_lib.PNG_MAX_WIDTH + 1, 2) == -1
+    with pytest.raises(ValueError, match="unsupported image size"):
+        sim.png_encode(torch.zeros((1, 2, _lib.PNG_MAX_WIDTH + 1, 3), dtype=torch.uint8, device="cuda"))
+
+
+def test_png_encode_from_another_stream(sim):
+    """png_encode called under another current stream: the encoder runs on the sim's
+    stream, its inputs produced on the caller's stream are waited for, and the caller's stream sees
+    the finished files; the bytes equal an encode on the default stream."""
+    rng = np.random.default_rng(8)
+    host = rng.integers(0, 256, (6, 48, 64, 3), dtype=np.uint8)
+    want, woffs = sim.png_encode(torch.as_tensor(host).cuda())
+    want = want.cpu().numpy()
+    other = torch.cuda.Stream()
+    with torch.cuda.stream(other):
+        big = torch.randn(4096, 4096, device="cuda")
+        for _ in range(4):  # keep the caller's stream busy before the images exist
+            big = big @ big * 1e-3
+        imgs = torch.as_tensor(host).cuda(non_blocking=True) + (big[0, 0] * 0).to(torch.uint8)
+        packed, offs = sim.png_encode(imgs)
+        got = packed.cpu().numpy()  # ordered on the caller's stream
+    np.testing.assert_array_equal(offs, woffs)
+    np.testing.assert_array_equal(got, want)

@@ -1,0 +1,10 @@
+"""Small helpers shared by the multi-process tests."""
+import socket
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
