@@ -159,7 +159,7 @@ DEV int clip_poly(const V3* in, int n, V3* out, V3 a, float b) {
 DEV V3 sel3(V3 a0, V3 a1, V3 a2, int k) { return k == 0 ? a0 : (k == 1 ? a1 : a2); }
 DEV float self3(float a0, float a1, float a2, int k) { return k == 0 ? a0 : (k == 1 ? a1 : a2); }
 
-// box-box, split in the parts the lane-per-pair (box_box) and lane-quad (box_box_quad) forms share:
+// box-box, split in parts (used by the lane-quad form box_box_quad below):
 // the 15-axis SAT, the edge-edge contact and the face-contact setup (reference / incident faces).
 struct BoxSat {
   V3 A[3], B[3], d;
@@ -312,69 +312,6 @@ DEV void box_face(const Geom& G1, const Geom& G2, const BoxSat& S, BoxFace& F) {
   F.nout = ref1 ? nref : -nref;
 }
 
-// box-box, one pair per lane: 15-axis SAT; face contacts clip the incident face against the
-// reference face (<= 8 points), edge-edge contacts give one point at the midpoint of the closest
-// points.  poly, tmp: 8 V3 each of per-lane LDS scratch (a quad clipped by 4 half-planes has <= 8
-// corners).
-template <class Sink>
-DEV void box_box(Sink& cs, const Geom& G1, const Geom& G2, V3 hb1, V3 hb2, V3* poly, V3* tmp) {
-  CLK_DECL;
-  BoxSat S;
-  box_sat(G1, G2, hb1, hb2, S);
-  if (S.sep) return;
-  PROBEF(8, cs.E->stats, STAT_T_AUX0);
-  if (box_edge_contact(S)) {
-    box_edge(cs, G1, G2, S);
-    return;
-  }
-  BoxFace F;
-  box_face(G1, G2, S, F);
-  const V3 cr = F.cr, nref = F.nref, ax0 = F.ax0, ax1 = F.ax1, nout = F.nout;
-  const float hru = F.hru, hrv = F.hrv;
-  {  // incident face entirely inside the reference face (a cube resting on a larger box): the
-     // clip below would return the 4 corners unchanged, in order
-    const float b0 = dot(ax0, cr) + hru, b1 = dot(-ax0, cr) + hru, b2 = dot(ax1, cr) + hrv, b3 = dot(-ax1, cr) + hrv;
-    bool inside = true;
-#pragma unroll
-    for (int c = 0; c < 4; c++)
-      inside = inside && dot(F.q[c], ax0) - b0 <= 0.f && dot(F.q[c], -ax0) - b1 <= 0.f && dot(F.q[c], ax1) - b2 <= 0.f &&
-               dot(F.q[c], -ax1) - b3 <= 0.f;
-    PROBEF(8, cs.E->stats, STAT_T_AUX1);
-    if (inside) {
-      float dep[4];
-      int n = 0;
-#pragma unroll
-      for (int c = 0; c < 4; c++) {
-        dep[c] = -dot(F.q[c] - cr, nref);
-        n += dep[c] >= 0.f ? 1 : 0;
-      }
-      int slot = cs.reserve(n);
-#pragma unroll
-      for (int c = 0; c < 4; c++)
-        if (dep[c] >= 0.f) cs.put(slot++, G1.g, G2.g, -dep[c], F.q[c] + nref * (0.5f * dep[c]), nout);
-      PROBEF(8, cs.E->stats, STAT_T_AUX2);
-      return;
-    }
-  }
-  int np = 4;
-  poly[0] = F.q[0];
-  poly[1] = F.q[1];
-  poly[2] = F.q[2];
-  poly[3] = F.q[3];
-  np = clip_poly(poly, np, tmp, ax0, dot(ax0, cr) + hru);
-  np = clip_poly(tmp, np, poly, -ax0, dot(-ax0, cr) + hru);
-  np = clip_poly(poly, np, tmp, ax1, dot(ax1, cr) + hrv);
-  np = clip_poly(tmp, np, poly, -ax1, dot(-ax1, cr) + hrv);
-  PROBEF(8, cs.E->stats, STAT_T_AUX3);
-  int n = 0;
-  for (int c = 0; c < np; c++) n += -dot(poly[c] - cr, nref) >= 0.f ? 1 : 0;
-  int slot = cs.reserve(n);
-  for (int c = 0; c < np; c++) {
-    const float depth = -dot(poly[c] - cr, nref);
-    if (depth >= 0.f) cs.put(slot++, G1.g, G2.g, -depth, poly[c] + nref * (0.5f * depth), nout);
-  }
-}
-
 // ---- lane-quad form: one pair per 4 consecutive lanes (a DPP quad), 16 pairs per wave pass
 template <int CTRL>
 DEV int qdpp_i(int v) {
@@ -390,9 +327,10 @@ DEV unsigned quad_bits(bool b) {
 // face setup redundantly, then the incident corners one per lane ("inside" case) or the
 // Sutherland-Hodgman clip with polygon vertices ql and ql + 4 per lane and plane (quad prefix
 // counts keep the sequential vertex order, and every vertex and intersection is computed with the
-// sequential form's expression), contacts put with the keys and slots box_box gives them (the
-// same contact list in the same order; tools/contact_ab.py: positions and depths bit-identical,
-// normals within 1 ulp).  poly, tmp: 8 V3 each of the quad's LDS scratch.
+// sequential clip's expression), contacts put with the keys and slots the sequential clip gives
+// them (the same contact list in the same order as the r02 lane-per-pair form, checked on 24,576
+// C3 states in r03: positions and depths bit-identical, normals within 1 ulp; the oracle's box_box
+// is that sequential form).  poly, tmp: 8 V3 each of the quad's LDS scratch.
 template <class Sink>
 DEV void box_box_quad(Sink& cs, const Geom& G1, const Geom& G2, V3 hb1, V3 hb2, V3* poly, V3* tmp) {
   CLK_DECL;

@@ -28,26 +28,22 @@
 #include "mmx_state.h"
 
 #define WG 64  // lanes of the wave that runs a phase
-// lane within the wave; WAVE_ID: which of the env-step kernel's two waves (0 or 1)
+// lane within the wave (a workgroup is one wave: one env)
 // Lane id re-materialised per use (an opaque copy of threadIdx.x): nothing lane-derived (lane masks,
 // per-lane dof / row indices) is hoisted to a function's entry and kept live across it.  In the
 // Newton solver, where the substep's register peak sits, that frees registers: the substep's
 // callee-saved save area 592 -> 436 B per lane and most SGPR spills go, for fewer instructions
 // overall (C3 +2.4 % in the A/B); applied everywhere it costs more re-materialisation than it saves
-// (-0.6 %).  MMX_LANE_OPAQUE_SECTIONS selects the sections by bit (LANE_SECTION below).
+// (-0.6 %), and in the constraint / collision / integrate + IK sections as well -0.8 to -1.7 %.
 DEV int lane_opaque() {
   int t = (int)threadIdx.x;
   asm volatile("" : "+v"(t));
   return t & 63;
 }
-#ifndef MMX_LANE_OPAQUE_SECTIONS
-#define MMX_LANE_OPAQUE_SECTIONS 0x10  // bit 0 kinematics, 1 dynamics, 2 collision, 3 constraints, 4 solver, 5 integrate, 6 IK
-#endif
 #define LANE ((int)(threadIdx.x & 63))
-#define WAVE_ID ((int)__builtin_amdgcn_readfirstlane(threadIdx.x >> 6))
 // SYNC: wave-local LDS ordering (a phase runs on ONE wave: its lanes exchange data through LDS,
 // whose operations a wave issues and completes in order, so no s_barrier / waitcnt is needed,
-// only a compiler fence).  XSYNC: both waves of the env-step workgroup (s_barrier).
+// only a compiler fence).  XSYNC: the workgroup barrier (s_barrier + memory fence) between env steps.
 DEV void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -61,11 +57,6 @@ static constexpr float kHome[7] = {1.5708f, -0.2f, 0.0f, -2.1f, 0.0f, 1.8f, 0.78
 static constexpr int kBinBody[3] = {MMX_BODY_BIN_RED, MMX_BODY_BIN_GREEN, MMX_BODY_BIN_BLUE};
 
 #define NSLOT 14  // arm bodies 1..11 -> slots 0..10, cubes 16..18 -> slots 11..13
-#ifdef MMX_TWO_WAVE
-static constexpr bool kTwoWave = true;
-#else
-static constexpr bool kTwoWave = false;
-#endif
 #ifndef MMX_CAND_CAP
 #define MMX_CAND_CAP 160      // persistent broadphase list entries (pair indices)
 #endif
@@ -127,13 +118,9 @@ static __shared__ EnvSh g_E;
 
 // E.J is the phases' scratch outside the constraint build + Newton solve (rows are rebuilt every
 // substep): the collision layout below, the position stage's chain scan, the IK system, the RNE /
-// composite-inertia / actuator scratch of the dynamics (at COL_WORK: the two-wave step runs the
-// dynamics beside the collision prune, which only touches [0, COL_WORK)) and the observation of
-// the step end.  The Newton Hessian staging tile and Cholesky transpose live in E.con instead
+// composite-inertia / actuator scratch of the dynamics (at COL_WORK) and the observation of the
+// step end.  The Newton Hessian staging tile and Cholesky transpose live in E.con instead
 // (contacts are dead once the rows exist; the last substep stores them to HBM first).
-#ifndef MMX_BOXBOX_QUAD  // box-box narrowphase on lane quads (1) or one pair per lane (0)
-#define MMX_BOXBOX_QUAD 1
-#endif
 #define COL_GX 0      // [NGEOM][GXS] world pose (x3, R9), rbound, type, -, -, box half extents (3), -
 #define GXS 20
 #define COL_CAND 944  // [COL_LIST] candidate pairs after the sphere test, then grouped by class
@@ -142,11 +129,7 @@ static __shared__ EnvSh g_E;
 #define COL_POLY 48                     // them) the EPA polytope, then the contact sort
 // lanes that clip box-box polygons at a time (their polygons fill the rest of the LDS rows)
 #define COL_PLANES ((MMX_LDSEFC * 16 - COL_WORK) / COL_POLY < 32 ? (MMX_LDSEFC * 16 - COL_WORK) / COL_POLY : 32)
-#if MMX_TWO_WAVE  // wave 0's GJK/EPA runs beside wave 1's box-box clipping
-#define COL_EPA (COL_WORK + COL_PLANES * COL_POLY)
-#else  // the GJK/EPA pass follows the box-box pass: the polytope reuses the polygons' space
 #define COL_EPA COL_WORK
-#endif
 static_assert(COL_EPA + EPA_SCRATCH_FLOATS <= MMX_LDSEFC * 16, "box-box polygons + EPA scratch exceed E.J");
 static_assert(COL_WORK + MMX_MAXCON * CON_F <= MMX_LDSEFC * 16, "contact sort exceeds E.J");
 static_assert(COL_PLANES >= 16 && COL_WORK + COL_PLANES * COL_POLY <= MMX_LDSEFC * 16, "box-box polygons exceed E.J");
@@ -246,15 +229,6 @@ DEV bool arm_anc(int d, int b) { return d <= 6 ? (b >= d + 2 && b <= 11) : (d ==
 DEV unsigned anc_mask(int b) {
   return b >= 2 && b <= 11 ? ((1u << min(b - 1, 7)) - 1u) | (b == 10 ? 0x80u : 0u) | (b == 11 ? 0x100u : 0u) : 0u;
 }
-#ifndef MMX_DPP_FOLD
-#define MMX_DPP_FOLD 1  // DPP reads in the update_dpp form the combiner folds into VOP2 ops (0: mov_dpp, A/B)
-#endif
-#ifndef MMX_TYPE_BALLOT
-#define MMX_TYPE_BALLOT 1  // row-type bases from per-type ballots (0: packed prefix scans, A/B)
-#endif
-#ifndef MMX_CROW_FAST
-#define MMX_CROW_FAST 1  // contact rows: ancestor masks and per-body columns (0: per-dof tests, A/B)
-#endif
 DEV V3 body_x(const EnvSh& E, int b) {
   if (MMX_body_static[b]) return V3{0.f, 0.f, 0.f};
   const int s = body_slot(b);
@@ -277,11 +251,7 @@ DEV SV load_S(const EnvSh& E, int d) { return SV{V3{E.S[d][0], E.S[d][1], E.S[d]
 // op: v_add_f32_dpp instead of v_mov_b32_dpp + v_add_f32)
 template <int CTRL>
 DEV float dpp_f(float v) {
-#if MMX_DPP_FOLD
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, true));
-#else
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
-#endif
 }
 DEV float wave_sum(float v) {
   v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
@@ -324,12 +294,6 @@ DEV void tri_index(int e, int& a, int& b) {
   b = e - aa * (aa + 1) / 2;
 }
 
-#undef LANE
-#if (MMX_LANE_OPAQUE_SECTIONS >> 0) & 1
-#define LANE lane_opaque()
-#else
-#define LANE ((int)(threadIdx.x & 63))
-#endif
 // ============================================================================ kinematics (lane 0)
 // mj_kinematics + arm motion subspaces (world-origin Plucker).  All joint anchors of this model
 // sit at the body origin (jnt_pos = 0).  Also refreshes the IK's kinematics cache.
@@ -452,12 +416,6 @@ DEV void kinematics_wave(EnvSh& E) {
   SYNC();
 }
 
-#undef LANE
-#if (MMX_LANE_OPAQUE_SECTIONS >> 1) & 1
-#define LANE lane_opaque()
-#else
-#define LANE ((int)(threadIdx.x & 63))
-#endif
 // ============================================================================ dynamics
 DEV RI body_inertia(const EnvSh& E, int b) {
   const V3 x = body_x(E, b);
@@ -681,12 +639,6 @@ DEV void dynamics_wave(EnvSh& E) {
   PROBE(11, stats, STAT_T_AUX3);
 }
 
-#undef LANE
-#if (MMX_LANE_OPAQUE_SECTIONS >> 2) & 1
-#define LANE lane_opaque()
-#else
-#define LANE ((int)(threadIdx.x & 63))
-#endif
 // ============================================================================ collision (wave)
 DEV Geom geom_pose(const EnvSh& E, int g) {
   Geom G;
@@ -806,11 +758,9 @@ DEV int wave_compact(bool keep, int* list, int base, int val) {
 // Collision in coherent stages: (1) world poses of all geoms into LDS, one lane per geom;
 // (2) bounding-sphere / plane-distance prune of all pairs, compacted with ballots; (3) OBB prune,
 // split by narrowphase class into per-class lists (E.ncls); (4) one pass per class (plane-convex
-// / box lane per pair, box-box lane per pair, GJK/EPA one pair per wave), so lanes of a pass run
-// the same code; (5) deterministic rank sort of the contacts by pair key.  Every prune is
-// conservative, so the contact set equals the all-pairs narrowphase.  (1)-(3), (4) and (5) are
-// separate functions: the two-wave env step runs (4)'s lane-per-pair classes on one wave and the
-// GJK pairs on the other (their contacts meet through the LDS atomic slot counter).
+// / box lane per pair, box-box one pair per lane quad, GJK/EPA one pair per wave), so lanes of a
+// pass run the same code; (5) deterministic rank sort of the contacts by pair key.  Every prune is
+// conservative, so the contact set equals the all-pairs narrowphase.
 DEV void collide_prune(EnvSh& E, bool only_ro) {
   float* stats = E.stats;
   CLK_DECL;
@@ -827,7 +777,7 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
   // for the integrators' second-order terms).  The list is in pair order, so the exact test below
   // keeps the same candidates, in the same order, as the all-pairs pass.
   bool use_list = false;
-  if (!kTwoWave && !only_ro && E.ncand >= 0) {  // (the two-wave step runs the RNE beside this)
+  if (!only_ro && E.ncand >= 0) {
     float vc = 0.f;
     if (LANE < 3) {
       const int da = 9 + 6 * LANE;
@@ -841,7 +791,7 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
     SYNC();
     if (LANE == 0) E.cdisp = use_list ? E.cdisp + inc : E.cdisp;
   }
-  const bool rebuild = !kTwoWave && !only_ro && !use_list;
+  const bool rebuild = !only_ro && !use_list;
   if (LANE < MMX_NGEOM) {
     const Geom G = geom_pose(E, LANE);
     float* o = gx + GXS * LANE;
@@ -1006,7 +956,6 @@ DEV void collide_pairs(EnvSh& E, bool only_ro, int which) {
     }
     SYNC();
     PROBE(5, stats, STAT_T_AUX0);
-#if MMX_BOXBOX_QUAD
     // box-box, one pair per lane quad (16 pairs per pass): the clip's vertices split over the quad
     V3* poly = reinterpret_cast<V3*>(scr + COL_WORK + COL_POLY * (LANE >> 2));
     for (int k0 = 0; k0 < n1; k0 += WG / 4) {
@@ -1019,19 +968,6 @@ DEV void collide_pairs(EnvSh& E, bool only_ro, int which) {
         box_box_quad(cs, A, B, geom_half(gx, g1), geom_half(gx, g2), poly, poly + 8);
       }
     }
-#else
-    V3* poly = reinterpret_cast<V3*>(scr + COL_WORK + COL_POLY * min(LANE, COL_PLANES - 1));
-    for (int k0 = 0; k0 < n1; k0 += COL_PLANES) {  // box-box
-      const int k = k0 + LANE;
-      if (LANE < COL_PLANES && k < n1) {
-        int p, g1, g2;
-        cand_unpack(cand[n0 + k], p, g1, g2);
-        const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
-        WaveSink cs(&E, p, !only_ro, g1, g2);
-        box_box(cs, A, B, geom_half(gx, g1), geom_half(gx, g2), poly, poly + 8);
-      }
-    }
-#endif
     SYNC();
     PROBE(5, stats, STAT_T_AUX1);
   }
@@ -1077,12 +1013,6 @@ DEV void collide_wave(EnvSh& E, bool only_ro) {
   if (!only_ro) collide_sort(E);
 }
 
-#undef LANE
-#if (MMX_LANE_OPAQUE_SECTIONS >> 3) & 1
-#define LANE lane_opaque()
-#else
-#define LANE ((int)(threadIdx.x & 63))
-#endif
 // ============================================================================ constraints (wave)
 // Soft-constraint reference terms of a row: K, B from solref, impedance from solimp (MuJoCo
 // mj_makeImpedance); D = 1 / R with R = (1 - imp) / imp * diag.
@@ -1146,27 +1076,20 @@ DEV float contact_row(EnvSh& E, int row, int c, int rr) {
     rb0 = rb1;
     rb1 = t;
   }
-#if MMX_CROW_FAST
   // arm block: coefficient +1 / -1 / 0 of dof d from the two bodies' ancestor-dof masks
   const unsigned am1 = anc_mask(b1), am2 = anc_mask(b2);
-#endif
   float vel = 0.f;
   float arm[9];
   // u . (v_d + w_d x p) + w . w_d = u . v_d + w_d . (p x u + w): one cross product per row
   const V3 pu = cross(p, u) + w;
 #pragma unroll
   for (int d = 0; d < 9; d++) {  // body 2 counts +, body 1 counts -
-#if MMX_CROW_FAST
     const float coef = (float)((int)((am2 >> d) & 1u) - (int)((am1 >> d) & 1u));
-#else
-    const float coef = (arm_anc(d, b2) ? 1.f : 0.f) - (arm_anc(d, b1) ? 1.f : 0.f);
-#endif
     const SV sd = load_S(E, d);
     arm[d] = coef * (dot(u, sd.v) + dot(sd.w, pu));
     vel = fmaf(arm[d], E.qvel[d], vel);
   }
   float cubeA[6], cubeB[6];  // blocks rb0 (when a cube) and rb1
-#if MMX_CROW_FAST
   // each body's free-body columns (zero unless it is a cube), velocity summed in body order; block
   // A (rb0) is body 1's unless body 1 is not rb0
   float cvs[2][6];
@@ -1196,34 +1119,6 @@ DEV float contact_row(EnvSh& E, int row, int c, int rr) {
     cubeA[j] = swap ? cvs[1][j] : cvs[0][j];
     cubeB[j] = swap ? cvs[0][j] : cvs[1][j];
   }
-#else
-#pragma unroll
-  for (int j = 0; j < 6; j++) {
-    cubeA[j] = 0.f;
-    cubeB[j] = 0.f;
-  }
-#pragma unroll
-  for (int side = 0; side < 2; side++) {
-    const int b = side ? b2 : b1, blk = side ? k2 : k1;
-    if (blk > 0) {
-      const float sg = side ? 1.f : -1.f;
-      const V3 x = body_x(E, b);
-      const M3 R = body_R(E, b);
-      float cv[6] = {sg * u.x, sg * u.y, sg * u.z, 0.f, 0.f, 0.f};
-      const V3 ru = cross(p - x, u) + w;  // u . (r_k x (p - x)) + w . r_k = r_k . ((p - x) x u + w)
-#pragma unroll
-      for (int k = 0; k < 3; k++) cv[3 + k] = sg * dot(col(R, k), ru);
-      const int d0 = blk_d0(blk);
-      const bool toA = blk == rb0;
-#pragma unroll
-      for (int j = 0; j < 6; j++) {
-        cubeA[j] += toA ? cv[j] : 0.f;
-        cubeB[j] += toA ? 0.f : cv[j];
-        vel = fmaf(cv[j], E.qvel[d0 + j], vel);
-      }
-    }
-  }
-#endif
   float jv[16];
   const bool armrow = rb0 == 0;
 #pragma unroll
@@ -1276,20 +1171,13 @@ DEV void make_constraints_wave(EnvSh& E) {
   }
   // single rows (equality + limits), then per type the contact groups
   const int acnt = (LANE == 0 ? 1 : 0) + nlim;
-#if MMX_TYPE_BALLOT
   // acnt <= 3: its two bits as ballots give the exclusive prefix and the total without a scan
   const unsigned long long a0 = __ballot(acnt & 1), a1 = __ballot(acnt & 2);
   const int nsingle_raw = __popcll(a0) + 2 * __popcll(a1);
   const int arow = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(a0 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)a0, 0u)) +
                    2 * (int)__builtin_amdgcn_mbcnt_hi((unsigned)(a1 >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)a1, 0u));
-#else
-  const int aincl = wave_scan_incl(acnt);
-  const int nsingle_raw = __builtin_amdgcn_readlane(aincl, 63);
-  const int arow = aincl - acnt;
-#endif
   const int nsingle = (nsingle_raw + 3) & ~3;
   int brow = 0, base = 0;
-#if MMX_TYPE_BALLOT
   // per type: one ballot of the contacts (lanes) of that type; a lane's rows start at the type's
   // base plus 4 x the contacts of its type in lower lanes (mbcnt), so no prefix scans
 #pragma unroll
@@ -1300,39 +1188,10 @@ DEV void make_constraints_wave(EnvSh& E) {
     if (LANE == 0) E.tbase[t] = min(base, MMX_MAXEFC);
     base = first + 4 * __popcll(m);
   }
-#else
-  // per-type prefix counts of contact rows, three 10-bit fields per 32-bit scan (<= MAXEFC < 1024)
-#pragma unroll
-  for (int t0 = 0; t0 < NTYPE; t0 += 3) {
-    int packed = 0;
-#pragma unroll
-    for (int f = 0; f < 3; f++) {
-      const int t = t0 + f;
-      packed |= (t < NTYPE && tc == t ? 4 : 0) << (10 * f);
-    }
-    const int incl = wave_scan_incl(packed);
-    const int tot = __builtin_amdgcn_readlane(incl, 63);
-#pragma unroll
-    for (int f = 0; f < 3; f++) {
-      const int t = t0 + f;
-      if (t >= NTYPE) break;
-      const int cnt = tc == t ? 4 : 0;
-      const int excl = ((incl >> (10 * f)) & 1023) - cnt;
-      const int first = base + (t == 0 ? nsingle : 0);  // type 0: the single rows come first
-      if (tc == t) brow = first + excl;
-      if (LANE == 0) E.tbase[t] = min(base, MMX_MAXEFC);
-      base = first + ((tot >> (10 * f)) & 1023);
-    }
-  }
-#endif
   const int total = base;
   const int nefc = min(total, MMX_MAXEFC);
-#if MMX_TYPE_BALLOT
   const int nefc_mj = nsingle_raw + __popcll(__ballot(nedge & 1)) + 2 * __popcll(__ballot(nedge & 2)) +
                       4 * __popcll(__ballot(nedge & 4));  // nedge <= 6
-#else
-  const int nefc_mj = nsingle_raw + (int)wave_sum((float)nedge);
-#endif
   if (LANE == 0) {
     E.tbase[NTYPE] = nefc;
     E.nefc = nefc;
@@ -1427,11 +1286,7 @@ DEV void make_constraints_wave(EnvSh& E) {
 }
 
 #undef LANE
-#if (MMX_LANE_OPAQUE_SECTIONS >> 4) & 1
-#define LANE lane_opaque()
-#else
-#define LANE ((int)(threadIdx.x & 63))
-#endif
+#define LANE lane_opaque()  // the Newton solver section (see lane_opaque)
 // ============================================================================ Newton solver (wave)
 // Primal Newton with exact line search (MuJoCo's default solver): minimise
 //   0.5 (x - xs)' M (x - xs) + sum_i s_i(J_i x - aref_i),  s_i = 0.5 D_i r^2 on active rows.
@@ -1455,11 +1310,7 @@ __host__ __device__ constexpr int newton_lane(int d) { return d < 9 ? d : 16 * (
 // DPP row_newbcast:K, the value of lane K of each 16-lane row in every lane of that row
 template <int K>
 DEV float row_bcast_t(float v) {
-#if MMX_DPP_FOLD
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + K, 0xF, 0xF, true));
-#else
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + K, 0xF, 0xF, false));
-#endif
 }
 // k is a constant of a fully unrolled loop at every call: the switch folds to one DPP move
 DEV float row_bcast(float v, int k) {
@@ -1477,9 +1328,6 @@ DEV float row_bcast(float v, int k) {
 }
 
 // J_i . x for a block-format row (slots past the row's width hold zeros)
-#ifndef MMX_ROWDOT_BASES
-#define MMX_ROWDOT_BASES 1  // 0: per-slot index select (A/B switch)
-#endif
 DEV float row_dot16(const EnvSh& E, int i, const float* x) {
   const int h = E.hdr[i], b0 = h & 15, b1 = (h >> 4) & 15;
   const int n0 = blk_size(b0), o0 = blk_d0(b0), o1 = (b1 == BLK_NONE ? 0 : blk_d0(b1)) - n0;
@@ -1502,11 +1350,7 @@ DEV float row_dot16(const EnvSh& E, int i, const float* x) {
   float s = 0.f;
 #pragma unroll
   for (int k = 0; k < 15; k++) {
-#if MMX_ROWDOT_BASES
     const float v = k < 6 ? x0[k] : (k < 9 ? x2[k] : (k < 12 ? x1[k] : x[min(o1 + k, 26)]));
-#else
-    const float v = x[min(k < n0 ? o0 + k : o1 + k, 26)];
-#endif
     s = fmaf(jv[k], v, s);
   }
   return s;
@@ -1618,12 +1462,8 @@ DEV void cost2_wave(const EnvSh& E, const float* xa, const float* xb, const floa
 // dof lanes into their Hessian row (static columns) and gradient.  Returns, in lane j < 27,
 // row j of H = M + J'WJ in hrow[0..27) and g_j = (M (x - xs) + J'W r)_j.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-#ifndef MMX_HESS_U
-#define MMX_HESS_U 2  // groups (MFMA steps) per trip, their loads issued together
-#endif
-#ifndef MMX_HESS_PIPE
-#define MMX_HESS_PIPE 0  // 1: software-pipelined trips (next trip's loads issued before the MFMAs)
-#endif
+// groups (MFMA steps) per trip, their loads issued together (3 or 4: -1.3 / -0.7 % in the r03 A/B)
+#define MMX_HESS_U 2
 // gather one row type's staged 16 x 16 tile into the dof lanes' Hessian rows: dof lane d reads row
 // sd of the tile; the type's two blocks land on static columns of hrow (uniform branches over the
 // 4 possible blocks keep every register index static); slot 15 is the type's gradient
@@ -1647,9 +1487,9 @@ DEV void tile_gather(const float* G, int t, int bd, int od, float* hrow, float& 
     gacc += Gr[15];
   }
 }
-#ifndef HESS_TILES
-#define HESS_TILES 1  // row types staged per barrier round (E.con holds up to three 16 x 16 tiles; 3: -1.3 % in the A/B, the unrolled rounds grow the substep's save area)
-#endif
+// row types staged per barrier round (E.con holds up to three 16 x 16 tiles; 3 measured -1.3 % in the
+// r03 A/B: the unrolled rounds grow the substep's register save area)
+#define HESS_TILES 1
 static_assert(HESS_TILES * 256 <= MMX_MAXCON * CON_F, "Hessian staging tiles exceed E.con");
 DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
   float* stats = E.stats;
@@ -1717,14 +1557,9 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
             }
           }
         };
-  #if MMX_HESS_PIPE  // the next trip's loads in flight during this trip's math and MFMAs
-        if (g_begin < g_end) load_trip(g_begin);
-  #endif
         for (int s0 = g_begin; s0 < g_end; s0 += 4 * MMX_HESS_U) {
           float a[MMX_HESS_U], b[MMX_HESS_U];
-  #if !MMX_HESS_PIPE
           load_trip(s0);
-  #endif
   #pragma unroll
           for (int u = 0; u < MMX_HESS_U; u++) {
             // arithmetic selects over the lane's row rk (0 / 1 masks): no divergent branches
@@ -1738,9 +1573,6 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
             a[u] = live * own;  // (slot 15 only feeds G's unused row 15)
             b[u] = live * fmaf(c15, own - fmaf(dr_[u], own, cpl), fmaf(dr_[u], own, cpl));
           }
-  #if MMX_HESS_PIPE
-          if (s0 + 4 * MMX_HESS_U < g_end) load_trip(s0 + 4 * MMX_HESS_U);
-  #endif
   #pragma unroll
           for (int u = 0; u < MMX_HESS_U; u++) {
             if (u & 1) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[u], b[u], acc1, 0, 0, 0);
@@ -1777,9 +1609,6 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
 // and only the row types holding one are staged and gathered.  LDS rows only (the caller runs the
 // full pass when rows spill to HBM).  Adds into hrow; returns sum B' dC r in lane j < 27.
 #define HESS_LQ (MMX_LDSEFC / WG)  // row slices held in LDS
-#ifndef MMX_NEWTON_DELTA
-#define MMX_NEWTON_DELTA 1  // 0: full Hessian / gradient pass every Newton iteration (A/B switch)
-#endif
 DEV float hess_grad_delta(EnvSh& E, float* hrow, const unsigned long long* gm) {
   float* G = lrow_of(E);
   const int col = LANE & 15, rk = LANE >> 4;
@@ -2053,14 +1882,11 @@ DEV float chol_solve_arrow(EnvSh& E, const float* hrow, float v, int cpl) {
   return j >= 0 ? y : 0.f;
 }
 
-#ifndef MMX_CHOL_BLOCK
-#define MMX_CHOL_BLOCK 1  // 0: the arrow form for every solve (A/B switch)
-#endif
 // H^{-1} v: the block form unless two cubes are coupled (a cube resting on or pushing another)
 DEV float chol_solve(EnvSh& E, const float* hrow, float v, int cpl) {
   float* stats = E.stats;
   CLK_DECL;
-  const bool cube_cube = !MMX_CHOL_BLOCK || (cpl & 0x6AC0) != 0;  // bits 4 x + y with x, y in 1..3, x != y
+  const bool cube_cube = (cpl & 0x6AC0) != 0;  // bits 4 x + y with x, y in 1..3, x != y
   const float y = cube_cube ? chol_solve_arrow(E, hrow, v, cpl)
                             : ((cpl & 0xE) ? chol_block_arm(hrow, v, cpl & 0xE) : chol_block_free(hrow, v));
   // probe set 9: cycles of the uncoupled / arm-coupled / cube-cube solves; AUX3 counts the
@@ -2121,7 +1947,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid, int& exit) 
     // collects its edges' normal parts over the DPP quad.  Delta mode: the same with the change
     // of each edge's weight (+-D where its active state flipped, else 0), and a mask of the
     // groups holding a flipped edge.
-    const bool delta = MMX_NEWTON_DELTA && it > 0 && nefc <= MMX_LDSEFC;  // uniform
+    const bool delta = it > 0 && nefc <= MMX_LDSEFC;  // uniform
     unsigned long long gm[HESS_LQ];
 #pragma unroll
     for (int q = 0; q < HESS_LQ; q++) gm[q] = 0ull;
@@ -2272,11 +2098,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid, int& exit) 
 }
 
 #undef LANE
-#if (MMX_LANE_OPAQUE_SECTIONS >> 5) & 1
-#define LANE lane_opaque()
-#else
 #define LANE ((int)(threadIdx.x & 63))
-#endif
 // ============================================================================ implicitfast + advance (wave)
 // Arm: (M - h qDeriv) qacc = qfrc_smooth + qfrc_constraint with qfrc_constraint = M (x - qacc_s),
 // qDeriv = -(damping + actuator kv where the force is unclamped), solved by a register Cholesky
@@ -2335,12 +2157,6 @@ DEV void integrate_wave(EnvSh& E) {
 
 // ============================================================================ implicitfast + advance (lane 0)
 
-#undef LANE
-#if (MMX_LANE_OPAQUE_SECTIONS >> 6) & 1
-#define LANE lane_opaque()
-#else
-#define LANE ((int)(threadIdx.x & 63))
-#endif
 // ============================================================================ IK (lane 0)
 DEV void orientation_error(const M3& Rc, V3& err) {  // controller.py:21-43, atan2 form for fp32
   float Em[9];
@@ -2516,8 +2332,6 @@ DEV void ik_wave(EnvSh& E) {
   SYNC();
 }
 
-#undef LANE
-#define LANE ((int)(threadIdx.x & 63))
 // ============================================================================ one mj_step
 DEV void mj_step_wave(int max_iter, float tol, EnvSh& E, float* con_dst) {
   float* stats = E.stats;
@@ -3097,83 +2911,16 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_substep_kernel(MMXState S, 
 // the env-step loop (hoisted invariants would pin registers for the whole kernel and serialise
 // the phases' LDS loads); the price is the callee-saved register spill / fill per call.
 //
-// Two waves per env (STEP_WG = 128): after the position stage, wave 0 runs the smooth dynamics
-// (RNE, CRBA, actuation, qacc_smooth) while wave 1 runs the collision prune (geom poses, sphere /
-// OBB tests, class lists); then wave 0 runs the GJK/EPA pairs while wave 1 runs the plane and
-// box-box pairs.  Concurrent phases touch disjoint LDS (M / Ic / bias / qfrc / qacc_s / Lrow
-// scratch vs. contacts / J scratch; contacts from both waves meet through an LDS atomic).
-// Everything else runs on wave 0.  This form (MMX_TWO_WAVE) is register-bound at 4 workgroups
-// per CU (2 x 250 VGPRs per SIMD).  The product build is the single-wave form: the env's LDS
-// footprint (19,232 B with rows past MMX_LDSEFC in HBM) admits 8 workgroups per CU, which beats
-// splitting one env over two waves (measured: 1.11 M env steps/s for two waves at 4 / CU vs 1.21 M
-// single-wave at 5 / CU).  The two-wave form needs -DMMX_LDSEFC=304 (its EPA scratch sits beside
-// the box-box polygons).
-#ifdef MMX_TWO_WAVE
-#define STEP_WG 128
-#else
-#define STEP_WG 64
-#endif
-#ifdef MMX_SUBSTEP_INLINE  // experiment: the substep inlined into the step loop (spills hoisted values)
-#define MMX_SUBSTEP_ATTR always_inline
-#else
-#define MMX_SUBSTEP_ATTR noinline
-#endif
-__device__ __attribute__((MMX_SUBSTEP_ATTR)) void substep(int max_iter, float tol, float* con_dst) {
+// (Measured and removed: splitting one env over two waves, wave 1 running the collision prune and
+// the plane / box-box pairs beside wave 0's dynamics and GJK/EPA: register-bound at 4 workgroups per
+// CU, 1.11 M env steps/s against 1.21 M for one wave at 5 / CU, before the LDS shrink to 8 / CU.)
+__device__ __attribute__((noinline)) void substep(int max_iter, float tol, float* con_dst) {
   EnvSh& E = g_E;
   float* stats = E.stats;
-#ifndef MMX_TWO_WAVE
   CLK_DECL;
   ik_wave(E);  // IK on the kinematics left by the previous position stage
   CLK(stats, STAT_T_IK);
   mj_step_wave(max_iter, tol, E, con_dst);
-#else
-  const int w = WAVE_ID;
-  if (w == 0) {
-    CLK_DECL;
-    ik_wave(E);  // IK on the kinematics left by the previous position stage
-    CLK(stats, STAT_T_IK);
-    kinematics_wave(E);
-    CLK(stats, STAT_T_KIN);
-  }
-  XSYNC();
-  {
-    CLK_DECL;
-    if (w == 0) {
-      dynamics_wave(E);
-      CLK(stats, STAT_T_DYN);
-    } else {
-      collide_prune(E, false);
-    }
-    XSYNC();
-    collide_pairs(E, false, w == 0 ? 2 : 1);  // wave 0: GJK/EPA pairs, wave 1: plane + box-box
-    XSYNC();
-    if (w == 1) CLK(stats, STAT_T_COL);  // wave 1's lane 0 (its own stats slot)
-  }
-  if (w == 0) {
-    CLK_DECL;
-    collide_sort(E);
-    if (con_dst) store_contacts(con_dst, E);  // before the row build reuses contact fields
-    make_constraints_wave(E);
-    CLK(stats, STAT_T_CON);
-    float resid = 0.f;
-    int exit = 0;
-    const int it = newton_wave(E, max_iter, tol, resid, exit);
-    CLK(stats, STAT_T_SOLVE);
-    integrate_wave(E);
-    CLK(stats, STAT_T_INT);
-    if (LANE == 0) {
-      stats[STAT_NEFC] += (float)E.nefc_mj;
-      stats[STAT_NCON] += (float)E.ncon;
-      stats[STAT_SOLVER_ITER] += (float)it;
-      stats[STAT_SUBSTEPS] += 1.f;
-      stats[STAT_RESID] = fmaxf(stats[STAT_RESID], resid);
-      stats[STAT_EXIT_STALL] += exit == 1 ? 1.f : 0.f;
-      stats[STAT_EXIT_CAP] += exit == 2 ? 1.f : 0.f;
-    }
-  }
-  // no trailing barrier: wave 1's next phase (collision) waits at the XSYNC after the next
-  // position stage, which wave 0 reaches only after finishing this substep
-#endif
 }
 
 // The whole PickPlaceGymEnv.step in ONE launch (product path): the 16 substeps loop inside the
@@ -3222,17 +2969,16 @@ extern "C" hipError_t mmx_fsm_profile(double* out, int reset) {
 extern "C" int mmx_fsm_profile_fields() { return FSMP_N; }
 #endif
 
-extern "C" __global__ void __launch_bounds__(STEP_WG) __attribute__((amdgpu_waves_per_eu(2, 2)))
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert, int base, int nsteps) {
   const int i = base + blockIdx.x;
   if (i >= S.N) return;
-  const bool w0 = STEP_WG == 64 || WAVE_ID == 0;
   for (int k = 0; k < nsteps; k++) {
     if (k) {  // the previous step's record stores complete before this step reloads it
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
       XSYNC();
     }
-    if (w0) step_begin(S, i, action, adim, expert);
+    step_begin(S, i, action, adim, expert);
     XSYNC();
 #ifdef MMX_PHASE_CLOCK
     float snap[FSMP_N];
@@ -3257,7 +3003,7 @@ mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert, int b
       atomicAdd(g + FSMP_NCON, (double)(g_E.stats[STAT_NCON] - snap[FSMP_NCON]));
     }
 #endif
-    if (w0) step_finish(S, i);
+    step_finish(S, i);
 #ifdef MMX_PHASE_CLOCK
     if (LANE == 0) {
       double* g = g_fsm_prof + FSMP_N * min(max(fsm, 0), 10);
@@ -3385,7 +3131,7 @@ extern "C" hipError_t mmx_launch_step(const MMXState* S, const float* action, in
                                       int count, int nsteps, hipStream_t st) {
   if (count <= 0 || nsteps <= 0) return hipSuccess;
   if (nsteps > 1 && !expert) return hipErrorInvalidValue;  // host actions: one env step per launch
-  hipLaunchKernelGGL(mmx_env_step_kernel, dim3(count), dim3(STEP_WG), 0, st, *S, action, adim, expert, base, nsteps);
+  hipLaunchKernelGGL(mmx_env_step_kernel, dim3(count), dim3(64), 0, st, *S, action, adim, expert, base, nsteps);
   return hipGetLastError();
 }
 extern "C" hipError_t mmx_launch_expert(const MMXState* S, int n, float* action, hipStream_t st) {

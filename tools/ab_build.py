@@ -1,4 +1,4 @@
-"""Build experiment variants of libmmx.so for A/B runs (tools/lib_ab.sh): each argument is
+"""Build experiment variants of libmmx.so for A/B runs (tools/ab.sh): each argument is
 `name:DEFINE[,DEFINE...]` (sources of the working tree) or `name@REV` (the csrc/ + include/ of a git
 revision, exported to a temp dir).  Output: build/libmmx_<name>.so.  Experiment infrastructure."""
 import os
