@@ -22,7 +22,12 @@ ARCH = os.environ.get("MMX_OFFLOAD_ARCH", "gfx950")
 # v_sqrt_f32, <= 1 ulp) instead of the correctly rounded fdiv / sqrt expansions (~10 VALU each).
 # The env-step kernel is VALU-issue-bound at 8 envs per CU: -11 % VALU instructions in the substep,
 # +3.7 % env steps/s (C3), parity tolerances unchanged.  Host code keeps IEEE semantics.
-DEVICE_MATH = ["-Xarch_device", "-freciprocal-math", "-Xarch_device", "-fapprox-func"]
+# r04: no NaN / Inf / signed-zero semantics either (-ffinite-math-only -fno-signed-zeros): selects
+# and min / max lose their NaN guards, -2.3 % VALU instructions per env step and +1.1 % env steps/s
+# in the interleaved A/B (profiles/r04_ab_finite_math.json), GPU suite unchanged.  The divergence
+# detector (NaN / Inf / |v| >= 1e10 -> counted reset) is an integer bit test, exact under any of these.
+DEVICE_MATH = ["-Xarch_device", "-freciprocal-math", "-Xarch_device", "-fapprox-func",
+               "-Xarch_device", "-ffinite-math-only", "-Xarch_device", "-fno-signed-zeros"]
 # gfx950 machine scheduler: the iterative ILP strategy (schedules for latency within the 256-VGPR
 # budget the 2-waves-per-SIMD occupancy allows) measured +6.4 % env steps/s over the default
 # occupancy-driven scheduler on the C3 bench (max-ilp +2 %, max-memory-clause +0 %).  The option
