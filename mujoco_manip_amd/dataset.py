@@ -372,12 +372,12 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
 
     # local position e <-> global episode ids[e]: slots and rows are indexed locally
     eps = [Episode(g, *task_list[g % len(task_list)], seeds[g] if seeds else None) for g in ids]
-    rows = [dict() for _ in range(E)]  # episode -> "_rows": [(step id, row)], image key -> [PNG bytes]
     slot_ep = np.full(N, -1, np.int64)
     next_ep = 0
     out_eps = [] if sink is None else None
     emitted = 0
     done_eps = {}  # finished, awaiting in-order emission: episode -> True
+    ep_slot = np.full(E, -1, np.int64)  # the slot an episode ran in
 
     def assign(slots):
         nonlocal next_ep
@@ -390,6 +390,7 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
                 continue
             ep = eps[next_ep]
             slot_ep[s] = next_ep
+            ep_slot[next_ep] = s
             next_ep += 1
             mask[s] = 1
             sd[s] = ep.seed
@@ -397,51 +398,73 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
         if mask.any():
             env.sim.reset(seeds=sd if seeds else None, task_override=task, env_mask=mask)
 
-    steps_host = {}  # step id -> [host arrays of the step, episodes still reading it]
-    sid_counter = [0]
+    # Host-side per-slot frame buffers: a slot's running episode gets one row per step, written for
+    # all of the step's slots at once (one fancy-indexed store per feature); an episode's rows are
+    # copied out when it finishes, before its slot's next episode writes there.  PNG files are cut
+    # out of each step's packed buffer into the slot's list.
+    bufs = {}  # host key -> [N, cap, ...]
+    cap = [64]
+    tpos = np.zeros(N, np.int64)  # rows of the slot's current episode so far
+    buf_ep = np.full(N, -1, np.int64)  # the episode whose rows the slot holds
+    png_rows = {f: [[] for _ in range(N)] for _, f in img_feats}
 
-    def absorb(host, payload):
-        """Index one step's host copy by episode (one row per active episode); the PNG files are
-        cut out of the step's packed buffer."""
-        slots, ep_ids, png_offs = payload
+    def absorb(host, slots, ep_ids, png_offs):
         if len(ep_ids) == 0:
             return
-        sid = sid_counter[0]
-        sid_counter[0] += 1
-        for k, offs in png_offs.items():
-            buf = host.pop(k + "/png").tobytes()
-            for j, e in enumerate(ep_ids):
-                rows[e].setdefault(k, []).append(buf[offs[j]:offs[j + 1]])
-        steps_host[sid] = [host, len(ep_ids)]
-        for j, e in enumerate(ep_ids):
-            rows[e].setdefault("_rows", []).append((sid, j))
+        new = buf_ep[slots] != ep_ids
+        if new.any():
+            ns = slots[new]
+            tpos[ns] = 0
+            buf_ep[ns] = ep_ids[new]
+            for rows_f in png_rows.values():
+                for s in ns:
+                    rows_f[s] = []
+        t = tpos[slots]
+        if int(t.max()) >= cap[0]:
+            cap[0] *= 2
+            for k, v in bufs.items():
+                g = np.empty((N, cap[0]) + v.shape[2:], v.dtype)
+                g[:, :v.shape[1]] = v
+                bufs[k] = g
+        for k, v in host.items():
+            if k.endswith("/png"):
+                continue
+            if k not in bufs:
+                bufs[k] = np.empty((N, cap[0]) + v.shape[1:], v.dtype)
+            bufs[k][slots, t] = v
+        for f, offs in png_offs.items():
+            data = host[f + "/png"].tobytes()
+            rows_f = png_rows[f]
+            for j, s in enumerate(slots.tolist()):
+                rows_f[s].append(data[offs[j]:offs[j + 1]])
+        tpos[slots] = t + 1
 
-    def finalize(e):
+    def finish(e):
+        """Copy episode e's rows out of its slot's buffers (it has ended: no row of it is still in
+        flight, and the slot's next episode has not written yet)."""
         ep = eps[e]
-        r = rows[e]
-        refs = r.get("_rows", [])
-        ep.length = len(refs)
+        s = int(ep_slot[e])
+        L = int(tpos[s]) if s >= 0 and buf_ep[s] == e else 0
+        ep.length = L
         ep.image_stats = {}
         for k in feature_keys:
             if k in IMAGE_KEYS:
-                ep.frames[k] = r.get(k, [])
-                fs = np.stack([steps_host[sid][0][k + "/stats"][j] for sid, j in refs]) if refs else None
-                ep.image_stats[k] = _merge_image_stats(fs, npx) if fs is not None else None
+                ep.frames[k] = png_rows[k][s] if L else []
+                if L:
+                    png_rows[k][s] = []
+                ep.image_stats[k] = _merge_image_stats(bufs[k + "/stats"][s, :L], npx) if L else None
             elif k == "observation.phase_description":
-                ep.frames[k] = [phase_description(steps_host[sid][0]["_fsm"][j], ep.obj, ep.bin) for sid, j in refs]
-            elif refs and k in steps_host[refs[0][0]][0]:
-                ep.frames[k] = np.stack([steps_host[sid][0][k][j] for sid, j in refs]).astype(np.float32)
-        for sid, _ in refs:  # release step buffers no episode reads any more
-            steps_host[sid][1] -= 1
-            if steps_host[sid][1] == 0:
-                del steps_host[sid]
-        rows[e] = None
+                ep.frames[k] = [phase_description(int(v), ep.obj, ep.bin) for v in bufs["_fsm"][s, :L]] if L else []
+            elif L and k in bufs:
+                ep.frames[k] = bufs[k][s, :L].astype(np.float32)
+        if L:
+            buf_ep[s] = -1
+        done_eps[e] = True
 
     def emit_ready(block=False):
         nonlocal emitted
         while emitted < E and emitted in done_eps:
             e = emitted
-            finalize(e)
             del done_eps[e]
             if sink is not None:
                 sink(eps[e])
@@ -453,11 +476,14 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
     ring = _PinnedRing(dev)
     step_no = 0
 
+    finished_eps = set()
+
     def process(items):
         for host, payload in items:
-            absorb(host, (payload[0], payload[1], payload[3]))
-            for e in payload[2]:  # episodes whose last frame was in this or an earlier step
-                done_eps[e] = True
+            for e in payload[2]:  # ended before this step: every row of theirs is absorbed
+                finish(e)
+                finished_eps.add(e)
+            absorb(host, payload[0], payload[1], payload[3])
 
     assign(range(N))
     fsm_view = env._epi[:, 4]
@@ -513,8 +539,8 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
         step_no += 1
     process(ring.drain())
     for e in range(E):  # every slot finished: the remaining episodes end here
-        if rows[e] is not None and e not in done_eps and eps[e] is not None:
-            done_eps[e] = True
+        if e not in finished_eps and e >= emitted:
+            finish(e)
     emit_ready(block=True)
     torch.cuda.synchronize(dev)
     env.close()
@@ -541,7 +567,7 @@ class LeRobotWriter:
 
     def __init__(self, root: str, repo_id: str, features: dict, *, fps=CONTROL_FPS, robot_type="franka_panda",
                  chunks_size=1000, data_files_size_in_mb=100, threaded=False, queue_depth=64,
-                 image_compression="SNAPPY", keep_image_sums=False):
+                 image_compression="SNAPPY", keep_image_sums=False, io_threads=None):
         import pyarrow as pa
         import pyarrow.parquet  # noqa: F401  (imported here, not on the first episode)
 
@@ -556,7 +582,7 @@ class LeRobotWriter:
         self.tasks, self.task_idx = [], {}
         self.ep_rows = []
         self.chunk, self.fileno, self.start = 0, 0, 0
-        self.writer, self.cur_bytes = None, 0
+        self.writer, self.cur_bytes = None, 0  # the open data file (its path) and its bytes so far
         self.limit = data_files_size_in_mb * 1024 * 1024
         self.num_acc = {}  # feature -> [min, max, sum, sumsq, count]
         self.img_acc = {}  # feature -> [min, max, sum, sumsq, pixels, frames]
@@ -568,6 +594,19 @@ class LeRobotWriter:
         # threaded: episodes go through a bounded queue to one writer thread (the reference writes
         # with background threads too, generate_dataset.py:260); parquet encoding and the file write
         # release the GIL, so they overlap the collection loop.  Episode order is kept.
+        # parquet encoding + file writes of consecutive data files run on `io_threads` single-thread
+        # lanes (file f on lane f mod io_threads, so one file's row groups stay in episode order and
+        # files are written side by side; the encoding releases the GIL); episodes, statistics and
+        # meta rows stay in order on the collecting thread.  At most 64 tables are in flight.
+        self.io_threads = (4 if threaded else 1) if io_threads is None else max(1, int(io_threads))
+        self._lanes, self._files, self._futs, self._nfile = None, {}, [], 0
+        if self.io_threads > 1:
+            import threading
+            from concurrent.futures import ThreadPoolExecutor
+
+            self._lanes = [ThreadPoolExecutor(max_workers=1, thread_name_prefix=f"lerobot-io{k}")
+                           for k in range(self.io_threads)]
+            self._inflight = threading.BoundedSemaphore(64)
         self._q, self._thread, self._err = None, None, None
         if threaded:
             import queue
@@ -640,9 +679,33 @@ class LeRobotWriter:
         ps = pq.ParquetFile(buf).schema
         return [ps.column(i).path for i in range(len(ps))]
 
+    def _io(self, fn, st):
+        """Run fn(st) on the open file's I/O lane (st: that file's state), or inline without lanes."""
+        if self._lanes is None:
+            fn(st)
+            return
+        self._inflight.acquire()
+        fut = self._lanes[st["lane"]].submit(fn, st)
+        fut.add_done_callback(lambda _f: self._inflight.release())
+        self._futs.append(fut)
+        if len(self._futs) > 256:  # surface I/O errors early, keep the list short
+            for f in [f for f in self._futs if f.done()]:
+                f.result()
+            self._futs = [f for f in self._futs if not f.done()]
+
+    def _io_wait(self):
+        for f in self._futs:
+            f.result()
+        self._futs = []
+
     def _close_file(self):
         if self.writer is not None:
-            self.writer.close()
+            def close(st):
+                if st.get("w") is not None:
+                    st["w"].close()
+                    st["w"] = None
+
+            self._io(close, self.writer)
             self.writer = None
             self.fileno += 1
             if self.fileno >= self.chunks_size:
@@ -671,12 +734,19 @@ class LeRobotWriter:
             # `image_compression` (SNAPPY, parquet's and LeRobot's default, still saves ~17 % on the
             # fixed-Huffman PNGs; NONE writes faster), the other columns keep dictionary + snappy
             plain = [c for c in tab.column_names if c not in self.img_keys]
-            self.writer = pq.ParquetWriter(os.path.join(d, f"file-{self.fileno:03d}.parquet"), tab.schema,
-                                           use_dictionary=plain,
-                                           compression={c: (self.image_compression if c.endswith(".bytes") and c[:-6] in self.img_keys
-                                                            else "SNAPPY")
-                                                        for c in self._leaf_columns(tab.schema)})
-        self.writer.write_table(tab)
+            comp = {c: (self.image_compression if c.endswith(".bytes") and c[:-6] in self.img_keys else "SNAPPY")
+                    for c in self._leaf_columns(tab.schema)}
+            path = os.path.join(d, f"file-{self.fileno:03d}.parquet")
+            self.writer = {"path": path, "lane": self._nfile % self.io_threads, "w": None,
+                           "schema": tab.schema, "kw": dict(use_dictionary=plain, compression=comp)}
+            self._nfile += 1
+
+        def write(st, tab=tab):
+            if st["w"] is None:
+                st["w"] = pq.ParquetWriter(st["path"], st["schema"], **st["kw"])
+            st["w"].write_table(tab)
+
+        self._io(write, self.writer)
         self.cur_bytes += tab.nbytes
         row = {"episode_index": ep.index, "tasks": [make_task_string(ep.obj, ep.bin)], "length": ep.length,
                "data/chunk_index": self.chunk, "data/file_index": self.fileno, "dataset_from_index": self.start,
@@ -721,6 +791,11 @@ class LeRobotWriter:
             self._q, self._thread = None, None
             self._raise_pending()
         self._close_file()
+        if self._lanes is not None:
+            self._io_wait()
+            for lane in self._lanes:
+                lane.shutdown(wait=True)
+            self._lanes = None
         meta = os.path.join(self.root, "meta")
         os.makedirs(os.path.join(meta, "episodes", "chunk-000"), exist_ok=True)
         rows = sorted(self.ep_rows, key=lambda r: r["episode_index"])

@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--out", default=os.path.join(REPO, "gpurun_out", "dataset_bench.json"))
     ap.add_argument("--keep", action="store_true")
     ap.add_argument("--image-compression", default="SNAPPY", choices=("SNAPPY", "NONE"))
+    ap.add_argument("--io-threads", type=int, default=None, help="LeRobotWriter I/O lanes (default 4)")
     a = ap.parse_args()
 
     import torch
@@ -48,7 +49,9 @@ def main():
     feats = D.resolve_features(None, "staged")
     shutil.rmtree(a.root, ignore_errors=True)
     path = os.path.join(a.root, "u", "bench")
-    writer = D.LeRobotWriter(path, "u/bench", feats, threaded=True, image_compression=a.image_compression)
+    feats = D._features_at(feats, a.image_size)
+    writer = D.LeRobotWriter(path, "u/bench", feats, threaded=True, image_compression=a.image_compression,
+                             io_threads=a.io_threads)
     frames = [0]
     png_bytes = [0]
 
@@ -67,7 +70,7 @@ def main():
     size = sum(os.path.getsize(os.path.join(d, f)) for d, _, fs in os.walk(path) for f in fs)
     rec = {"config": {"num_envs": a.num_envs, "episodes": a.episodes, "image_size": a.image_size,
                       "png": "device (mmx_png_encode)", "image_compression": a.image_compression,
-                      "writer": "LeRobotWriter(threaded=True)", "features": "all (2 cameras, numeric, actions, reward, phase)"},
+                      "writer": f"LeRobotWriter(threaded=True, io_threads={writer.io_threads})", "root": a.root, "features": "all (2 cameras, numeric, actions, reward, phase)"},
            "episodes": info["total_episodes"], "frames": info["total_frames"], "seconds": dt,
            "frames_per_s": info["total_frames"] / dt, "images_per_s": 2 * info["total_frames"] / dt,
            "png_mean_bytes": png_bytes[0] / max(2 * frames[0], 1), "dataset_bytes": size,
