@@ -64,15 +64,6 @@ static constexpr int kMaxBig = 512;
 #define MMR_BIG_CACHE 40  // large-triangle setups kept in LDS per band (what fits beside two workgroups per CU)
 #endif
 static constexpr int kBigCache = MMR_BIG_CACHE;  // per band; a full queue sends further large triangles to the small path
-#ifndef MMR_PF
-#define MMR_PF 1  // small raster: vertex ids of the next triangle prefetched
-#endif
-#ifndef MMR_COLS
-#define MMR_COLS 1  // small raster as column walks (0: row-major 16-pixel chunks)
-#endif
-#ifndef MMR_SPAN
-#define MMR_SPAN 1  // column walk restricted to the column's span inside the triangle
-#endif
 #ifndef MMR_BPW
 #define MMR_BPW 2
 #endif
@@ -394,83 +385,79 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
     // queue entry q: the tiny boxes [0, nsf) from the front, then the others from the back
     const unsigned short* sq = smallq + kb * MMR_NTRI;
     auto sq_at = [&](int q) { return (int)sq[q < nsf ? q : MMR_NTRI - 1 - (q - nsf)]; };
-    const int grp = tid / kGroup, gl = tid % kGroup;
-    // one triangle ahead: the next triangle's vertex ids (table loads) are in flight while this
-    // one is scanned
-    int tn = grp < ns ? sq_at(grp) : MMR_FLOOR_TRIS;
-    int an = MMR_tri[3 * tn], bn = MMR_tri[3 * tn + 1], cn = MMR_tri[3 * tn + 2];
-    for (int q = grp; q < ns; q += RWG / kGroup) {
-      int t = tn;
-      const int a = an, b = bn, c = cn;
-      if (MMR_PF && q + RWG / kGroup < ns) {
-        tn = sq_at(q + RWG / kGroup);
-        an = MMR_tri[3 * tn]; bn = MMR_tri[3 * tn + 1]; cn = MMR_tri[3 * tn + 2];
-      }
-      RTri T;
-      if (MMR_PF) rend_setup_abc(vs, a, b, c, Sz, row0, row1, iz_scale, T);
-      else rend_setup(vs, t = sq_at(q), Sz, row0, row1, iz_scale, T);
-      const int w = T.bx1 - T.bx0 + 1;
-      const float rw = 1.f / (float)w;
-      const float qB = fmaf(T.B[0], T.w[0], fmaf(T.B[1], T.w[1], T.B[2] * T.w[2]));  // dq / dy
-#ifdef MMR_CLOCK_STATS  // (global atomics: distorts the MMR_CLOCK times)
-      if (gl == 0) {
-        atomicAdd(&g_rclk[6], 1ull);
-        atomicAdd(&g_rclk[7], (unsigned long long)(w * (T.by1 - T.by0 + 1)));
-      }
-#endif
-#if MMR_COLS
-      // column walk: a box up to 16 wide gives each lane one column and a row phase (16 / w lanes
-      // per column, rows strided by that), a wider one 16 columns per pass, rows one by one; the
-      // edges' x parts are formed once per column, a pixel then costs 3 FMAs and a max
-      const bool narrow = w <= kGroup;
-      const int rstep = narrow ? (int)(((float)kGroup + 0.5f) * rw) : 1;  // kGroup / w (exact)
-      const int rph = narrow ? (int)(((float)gl + 0.5f) * rw) : 0;        // gl / w
-#if MMR_SPAN
-      const float rB[3] = {1.f / T.B[0], 1.f / T.B[1], 1.f / T.B[2]};  // (unused where B_k = 0)
-#endif
-      if (rph < rstep) {
-        for (int col = narrow ? gl - rph * w : gl; col < w; col += kGroup) {
-          const int px = T.bx0 + col;
-          const float x = px + 0.5f;
-          const float ex0 = rend_edge_x(T, 0, x), ex1 = rend_edge_x(T, 1, x), ex2 = rend_edge_x(T, 2, x);
-#if MMR_SPAN
-          // the column's span inside the triangle: edge k bounds the row centres y = py + 0.5 from
-          // above (B_k > 0: y <= -ex_k / B_k) or below (B_k < 0); widened by a row on each side, it
-          // only narrows the walk, every pixel still takes the exact edge test
-          float lo = (float)T.by0, hi = (float)T.by1;
-          {
-            const float ex[3] = {ex0, ex1, ex2};
-            for (int k = 0; k < 3; k++) {
-              const float yb = -ex[k] * rB[k] - 0.5f;  // the boundary in row-index units
-              hi = T.B[k] > 0.f ? fminf(hi, yb + 1.f) : hi;
-              lo = T.B[k] < 0.f ? fmaxf(lo, yb - 1.f) : lo;
+    // Group grp = tid / 8 (wave wv = tid / 64, group g = lane / 8 in it) walks the queue entries
+    // q = grp + 64 k, k = 0, 1, ...  The setups are computed wave-wide, one lane per triangle:
+    // for the 8 steps k = 8 r .. 8 r + 7 of a round, lane 8 j + g sets up group g's triangle of
+    // step 8 r + j, and at step j each group fetches its setup from that lane (ds_bpermute)
+    // instead of its 8 lanes all recomputing it.
+    static_assert(kGroup == 8 && RWG % 64 == 0, "wave-wide setup: 8 groups of 8 lanes per wave");
+    const int lane = tid & 63, wv = tid >> 6, g = lane >> 3, gl = lane & 7;
+    const int per_step = RWG / kGroup;  // groups in the workgroup: queue entries per step
+    for (int r = 0; 8 * r * per_step < ns; r++) {
+      const int qs = (8 * r + (lane >> 3)) * per_step + 8 * wv + (lane & 7);  // this lane's setup
+      RTri Ts;
+      const int ts = qs < ns ? sq_at(qs) : MMR_FLOOR_TRIS;
+      rend_setup(vs, ts, Sz, row0, row1, iz_scale, Ts);
+      for (int j = 0; j < 8; j++) {
+        const int k = 8 * r + j;
+        if (k * per_step + 8 * wv >= ns) break;  // uniform per wave: no group of it has an entry
+        const int q = k * per_step + 8 * wv + g;
+        const int src = 8 * j + g;  // the lane holding this group's setup
+        RTri T;
+#pragma unroll
+        for (int e = 0; e < 3; e++) {
+          T.A[e] = __shfl(Ts.A[e], src);
+          T.B[e] = __shfl(Ts.B[e], src);
+          T.C[e] = __shfl(Ts.C[e], src);
+          T.w[e] = __shfl(Ts.w[e], src);
+        }
+        T.bx0 = __shfl(Ts.bx0, src);
+        T.bx1 = __shfl(Ts.bx1, src);
+        T.by0 = __shfl(Ts.by0, src);
+        T.by1 = __shfl(Ts.by1, src);
+        const int t = __shfl(ts, src);
+        if (q >= ns) continue;
+        const int w = T.bx1 - T.bx0 + 1;
+        const float rw = 1.f / (float)w;
+        const float qB = fmaf(T.B[0], T.w[0], fmaf(T.B[1], T.w[1], T.B[2] * T.w[2]));  // dq / dy
+        // column walk: a box up to 8 wide gives each lane one column and a row phase (8 / w lanes
+        // per column, rows strided by that), a wider one 8 columns per pass, rows one by one; the
+        // edges' x parts are formed once per column, a pixel then costs 3 FMAs and a max
+        const bool narrow = w <= kGroup;
+        const int rstep = narrow ? (int)(((float)kGroup + 0.5f) * rw) : 1;  // kGroup / w (exact)
+        const int rph = narrow ? (int)(((float)gl + 0.5f) * rw) : 0;        // gl / w
+        const float rB[3] = {1.f / T.B[0], 1.f / T.B[1], 1.f / T.B[2]};  // (unused where B_k = 0)
+        if (rph < rstep) {
+          for (int col = narrow ? gl - rph * w : gl; col < w; col += kGroup) {
+            const int px = T.bx0 + col;
+            const float x = px + 0.5f;
+            const float ex0 = rend_edge_x(T, 0, x), ex1 = rend_edge_x(T, 1, x), ex2 = rend_edge_x(T, 2, x);
+            // the column's span inside the triangle: edge k bounds the row centres y = py + 0.5 from
+            // above (B_k > 0: y <= -ex_k / B_k) or below (B_k < 0); widened by a row on each side, it
+            // only narrows the walk, every pixel still takes the exact edge test
+            float lo = (float)T.by0, hi = (float)T.by1;
+            {
+              const float ex[3] = {ex0, ex1, ex2};
+              for (int e = 0; e < 3; e++) {
+                const float yb = -ex[e] * rB[e] - 0.5f;  // the boundary in row-index units
+                hi = T.B[e] > 0.f ? fminf(hi, yb + 1.f) : hi;
+                lo = T.B[e] < 0.f ? fmaxf(lo, yb - 1.f) : lo;
+              }
             }
-          }
-          // (kept inside [by0, by1 + 1] / [by0 - 1, by1] before the integer conversion)
-          const int pylo = (int)ceilf(fminf(lo, (float)(T.by1 + 1))), pyhi = (int)floorf(fmaxf(hi, (float)(T.by0 - 1)));
-#else
-          const int pylo = T.by0, pyhi = T.by1;
-#endif
-          // q is affine in y along the column: q = qB y + qx (one FMA per pixel)
-          const float qx = fmaf(ex0, T.w[0], fmaf(ex1, T.w[1], fmaf(ex2, T.w[2], q0)));
-          uint32_t* zc = zb + (pylo + rph - row0) * Zs + px;
-          const float ystep = (float)rstep;
-          float y = (float)(pylo + rph) + 0.5f;
-          for (int py = pylo + rph; py <= pyhi; py += rstep, zc += rstep * Zs, y += ystep) {
-            const float e0 = fmaf(T.B[0], y, ex0), e1 = fmaf(T.B[1], y, ex1), e2 = fmaf(T.B[2], y, ex2);
-            if (fmaxf(e0, fmaxf(e1, e2)) <= 0.f) atomicMax(zc, rend_key_q(t, fmaf(qB, y, qx)));
+            // (kept inside [by0, by1 + 1] / [by0 - 1, by1] before the integer conversion)
+            const int pylo = (int)ceilf(fminf(lo, (float)(T.by1 + 1))), pyhi = (int)floorf(fmaxf(hi, (float)(T.by0 - 1)));
+            // q is affine in y along the column: q = qB y + qx (one FMA per pixel)
+            const float qx = fmaf(ex0, T.w[0], fmaf(ex1, T.w[1], fmaf(ex2, T.w[2], q0)));
+            uint32_t* zc = zb + (pylo + rph - row0) * Zs + px;
+            const float ystep = (float)rstep;
+            float y = (float)(pylo + rph) + 0.5f;
+            for (int py = pylo + rph; py <= pyhi; py += rstep, zc += rstep * Zs, y += ystep) {
+              const float e0 = fmaf(T.B[0], y, ex0), e1 = fmaf(T.B[1], y, ex1), e2 = fmaf(T.B[2], y, ex2);
+              if (fmaxf(e0, fmaxf(e1, e2)) <= 0.f) atomicMax(zc, rend_key_q(t, fmaf(qB, y, qx)));
+            }
           }
         }
       }
-#else
-      const int area = w * (T.by1 - T.by0 + 1);
-      for (int k = gl; k < area; k += kGroup) {
-        const int r = (int)(((float)k + 0.5f) * rw);  // k / w, exact for these sizes (no integer divide)
-        const int px = T.bx0 + k - r * w, py = T.by0 + r;
-        const uint32_t key = rend_cover(T, t, px, py, q0);
-        if (key) atomicMax(&zb[(py - row0) * Zs + px], key);
-      }
-#endif
     }
   }
   __syncthreads();
