@@ -154,8 +154,8 @@ def test_solver_exit_criteria_consequence():
     """the kernel's Newton exit (30 iterations, relative gradient 1e-6) against
     MuJoCo's defaults (100 iterations, 1e-8; fp32 stops earlier on no progress) on the same 48 C3
     episodes in lockstep: the trajectories agree to well inside the oracle tolerances, so the
-    looser exit changes no episode outcome.  Measured: episode lengths equal, final cubes within
-    0.2 mm, max |qpos| difference over the episodes printed."""
+    looser exit changes no episode outcome.  Measured (r04): episode lengths equal, max |qpos|
+    difference over all 48 episodes 5e-5, Newton iterations per solve 1.79 against 2.74."""
     from mujoco_manip_amd import _lib
 
     N = 48
@@ -186,7 +186,7 @@ def test_solver_exit_criteria_consequence():
     assert (length >= 0).all()
     np.testing.assert_array_equal(length[0], length[1])
     assert np.abs(final[0] - final[1]).max() < 2e-4, np.abs(final[0] - final[1]).max()
-    assert dq < 5e-3, dq
+    assert dq < 5e-4, dq
 
 
 def test_autoreset_continues_rng_stream():
