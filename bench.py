@@ -282,7 +282,7 @@ def main():
         cpu = cpu_baseline(args.cpu_seconds)
     dist = None
     dev_index = 0 if args.share_device else local_rank
-    if world > 1:
+    if world > 1 or "WORLD_SIZE" in os.environ:  # under torchrun: the process group even for 1 rank
         import torch.distributed as dist
 
         import datetime

@@ -389,20 +389,23 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
     // q = grp + 64 k, k = 0, 1, ...  The setups are computed wave-wide, one lane per triangle:
     // for the 8 steps k = 8 r .. 8 r + 7 of a round, lane 8 j + g sets up group g's triangle of
     // step 8 r + j, and at step j each group fetches its setup from that lane (ds_bpermute)
-    // instead of its 8 lanes all recomputing it.
-    static_assert(kGroup == 8 && RWG % 64 == 0, "wave-wide setup: 8 groups of 8 lanes per wave");
-    const int lane = tid & 63, wv = tid >> 6, g = lane >> 3, gl = lane & 7;
+    // instead of its 8 lanes all recomputing it (written for kGroup lanes per group).
+    // (with G = 64 / kGroup groups per wave, a round is kGroup steps: lane j G + g sets up group
+    // g's triangle of step j)
+    constexpr int G = 64 / kGroup;
+    static_assert(64 % kGroup == 0 && RWG % 64 == 0, "wave-wide setup: whole groups per wave");
+    const int lane = tid & 63, wv = tid >> 6, g = lane / kGroup, gl = lane % kGroup;
     const int per_step = RWG / kGroup;  // groups in the workgroup: queue entries per step
-    for (int r = 0; 8 * r * per_step < ns; r++) {
-      const int qs = (8 * r + (lane >> 3)) * per_step + 8 * wv + (lane & 7);  // this lane's setup
+    for (int r = 0; kGroup * r * per_step < ns; r++) {
+      const int qs = (kGroup * r + lane / G) * per_step + G * wv + lane % G;  // this lane's setup
       RTri Ts;
       const int ts = qs < ns ? sq_at(qs) : MMR_FLOOR_TRIS;
       rend_setup(vs, ts, Sz, row0, row1, iz_scale, Ts);
-      for (int j = 0; j < 8; j++) {
-        const int k = 8 * r + j;
-        if (k * per_step + 8 * wv >= ns) break;  // uniform per wave: no group of it has an entry
-        const int q = k * per_step + 8 * wv + g;
-        const int src = 8 * j + g;  // the lane holding this group's setup
+      for (int j = 0; j < kGroup; j++) {
+        const int k = kGroup * r + j;
+        if (k * per_step + G * wv >= ns) break;  // uniform per wave: no group of it has an entry
+        const int q = k * per_step + G * wv + g;
+        const int src = G * j + g;  // the lane holding this group's setup
         RTri T;
 #pragma unroll
         for (int e = 0; e < 3; e++) {

@@ -67,7 +67,7 @@ def gather_env_stats(rec, dist=None, world: int = 1):
     host tensors).  Logging only, outside any timed region."""
     import torch
 
-    if dist is None or world == 1:
+    if dist is None:
         return rec
     out = torch.empty((world * rec.shape[0], rec.shape[1]), dtype=rec.dtype, device=rec.device)
     dist.all_gather_into_tensor(out, rec)

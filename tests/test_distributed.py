@@ -195,3 +195,25 @@ def test_two_rank_hip_rollout_matches_single_process(tmp_path):
     from mujoco_manip_amd.shard import env_stats_record
 
     np.testing.assert_array_equal(stats, env_stats_record(env).cpu().numpy())  # §8(e) gather
+
+
+@pytest.mark.gpu
+def test_rccl_path_single_rank_torchrun():
+    """bench.py under torchrun with one rank: the process group is RCCL (the `nccl` backend) and
+    the line comes out of the RCCL branch (barriers, all_reduce of the window time and counters,
+    all_gather_into_tensor of the per-env records on device tensors); the 8-GPU scaling runs use
+    the same branch.  (Two ranks cannot share one GPU under RCCL, so the 1-GPU box tests N = 1.)"""
+    import json
+
+    if not torch.cuda.is_available():
+        pytest.skip("needs an MI355X")
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+                        os.path.join(repo, "bench.py"), "--gpus", "1", "--steps", "32", "--warmup", "8",
+                        "--repeats", "2", "--no-cpu-baseline", "--dist-backend", "nccl"],
+                       capture_output=True, text=True, timeout=240, cwd=repo)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 1 and line["value"] > 0
+    assert line["rank_envs"][0]["envs"] == 4096 and sum(line["rank_envs"][0]["fsm_phase_hist"]) == 4096
