@@ -198,6 +198,20 @@ int mmx_synchronize(mmx_sim* sim);
 int mmx_get_state(mmx_sim* sim, float* qpos, float* qvel, float* ctrl, float* qacc_warmstart);
 int mmx_set_state(mmx_sim* sim, const float* qpos, const float* qvel, const float* ctrl, const float* qacc_warmstart);
 
+/* Device-side episode queue of dataset generation (scripts/generate_dataset.py:140-198 runs
+ * run_episode per episode with seeds / tasks from :263-277): n_episodes episodes stream through the
+ * N env slots with no host synchronisation per step.  mmx_queue_init uploads every episode's task
+ * (host, n_episodes entries of obj << 4 | bin, -1 = the env's own draw) and, when seeds (host,
+ * n_episodes entries) is non-NULL, its PCG64(SeedSequence(seed)) state; no slot holds an episode
+ * yet (synchronous; replaces a previous queue).  mmx_queue_advance, asynchronous on the sim's
+ * stream: every slot that holds no episode or whose episode's FSM reached DONE takes the next
+ * episode, in ascending slot order, and is reset (PickPlaceGymEnv.reset with the episode's seed
+ * and task, gym_env.py:477-534) and re-rendered; slot_ep_dev (device int32 [N], may be NULL)
+ * receives each slot's episode afterwards (-1: none left) and fin_ep_dev (device int32 [N], may be
+ * NULL) the episode that ended in the slot at this call (-1: none).  MMX_EINVAL without a queue. */
+int mmx_queue_init(mmx_sim* sim, int32_t n_episodes, const uint64_t* seeds, const int32_t* tasks);
+int mmx_queue_advance(mmx_sim* sim, int32_t* slot_ep_dev, int32_t* fin_ep_dev);
+
 /* Host helper: SeedSequence(root).spawn(n)[index].generate_state(1)[0]
  * (scripts/generate_dataset.py:263-268). */
 uint32_t mmx_episode_seed(uint64_t root_seed, int32_t index);

@@ -57,7 +57,8 @@ EXPORTED = ("mmx_config_default", "mmx_create", "mmx_destroy", "mmx_last_error",
             "mmx_expert_plan", "mmx_rollout_expert", "mmx_physics_step", "mmx_forward", "mmx_get_buffers",
             "mmx_synchronize", "mmx_get_state", "mmx_set_state", "mmx_episode_seed", "mmx_rollout_lanes",
             "mmx_rollout_steps_per_launch", "mmx_rollout_launches", "mmx_expert_physics", "mmx_eval_reward", "mmx_kernel_timing",
-            "mmx_kernel_times", "mmx_png_bound", "mmx_png_scratch", "mmx_png_encode", "mmx_png_pack")
+            "mmx_kernel_times", "mmx_png_bound", "mmx_png_scratch", "mmx_png_encode", "mmx_png_pack",
+            "mmx_queue_init", "mmx_queue_advance")
 
 _lib = None
 
@@ -107,12 +108,14 @@ def load(build_if_missing: bool = True):
     L.mmx_synchronize.argtypes = [vp]
     L.mmx_get_state.argtypes = [vp, fp, fp, fp, fp]
     L.mmx_set_state.argtypes = [vp, fp, fp, fp, fp]
+    L.mmx_queue_init.argtypes = [vp, C.c_int32, u64p, i32p]
+    L.mmx_queue_advance.argtypes = [vp, vp, vp]
     L.mmx_episode_seed.restype = C.c_uint32
     L.mmx_episode_seed.argtypes = [C.c_uint64, C.c_int32]
     for name in ("mmx_create", "mmx_reset", "mmx_step", "mmx_expert_plan", "mmx_rollout_expert", "mmx_physics_step",
                  "mmx_forward", "mmx_get_buffers", "mmx_synchronize", "mmx_get_state", "mmx_set_state",
                  "mmx_expert_physics", "mmx_eval_reward", "mmx_kernel_timing", "mmx_kernel_times", "mmx_png_encode",
-                 "mmx_png_pack"):
+                 "mmx_png_pack", "mmx_queue_init", "mmx_queue_advance"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L
@@ -222,6 +225,23 @@ class Sim:
             m = self._mask_arr.ctypes.data_as(u8p)
         self._check(self.L.mmx_reset(self.ptr, s, g, t, m), "mmx_reset")
 
+    def queue_init(self, tasks, seeds=None):
+        """Device-side episode queue (mmx_queue_init): tasks[e] = obj << 4 | bin of episode e and,
+        optionally, its seed (PCG64(SeedSequence(seed)) at its reset)."""
+        t = np.ascontiguousarray(tasks, np.int32)
+        s = None if seeds is None else np.ascontiguousarray([int(v) for v in seeds], np.uint64)
+        if s is not None and len(s) != len(t):
+            raise ValueError("seeds and tasks must have one entry per episode")
+        self._check(self.L.mmx_queue_init(self.ptr, len(t), None if s is None else s.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                          t.ctypes.data_as(C.POINTER(C.c_int32))), "mmx_queue_init")
+
+    def queue_advance(self, slot_ep_ptr: int | None = None, fin_ep_ptr: int | None = None):
+        """Hand the next episodes to the free / finished slots and reset them (mmx_queue_advance;
+        asynchronous).  The pointers: device int32 [N] outputs (slot -> episode after the call,
+        episode that ended in the slot at this call; -1 = none)."""
+        self._check(self.L.mmx_queue_advance(self.ptr, C.c_void_p(slot_ep_ptr) if slot_ep_ptr else None,
+                                             C.c_void_p(fin_ep_ptr) if fin_ep_ptr else None), "mmx_queue_advance")
+
     def step(self, action_ptr: int, action_dim: int):
         self._check(self.L.mmx_step(self.ptr, C.c_void_p(action_ptr), action_dim), "mmx_step")
 
@@ -296,6 +316,44 @@ class Sim:
             offs.extend((ends.cpu().numpy() + offs[-1]).tolist())
         packed = torch.cat(parts) if len(parts) > 1 else parts[0]
         return packed, np.asarray(offs, np.int64)
+
+    def png_encode_device(self, images):
+        """PNG files of RGB8 images [n, H, W, 3] (CUDA uint8, rows contiguous) encoded and packed on
+        the device with NO host synchronisation: returns (packed, ends), both CUDA tensors on the
+        caller's stream: file i is packed[ends[i - 1]:ends[i]] (ends int64 [n]); packed has room for
+        n * mmx_png_bound bytes, of which the first ends[-1] are files.  The dataset loop copies
+        the sizes and the packed bytes to the host asynchronously."""
+        import torch
+
+        n, H, W, c = images.shape
+        assert c == 3 and images.dtype == torch.uint8 and images.is_cuda and n > 0
+        assert images.stride(1) == W * 3 and images.stride(2) == 3 and images.stride(3) == 1, "rows must be contiguous"
+        bound, scr = int(self.L.mmx_png_bound(W, H)), int(self.L.mmx_png_scratch(W, H))
+        if bound < 0:
+            raise ValueError(f"unsupported image size {W} x {H}")
+        cur = torch.cuda.current_stream(images.device)
+        sst = (torch.cuda.ExternalStream(self.cfg.stream, device=images.device) if self.cfg.stream
+               else torch.cuda.default_stream(images.device))
+        sst.wait_stream(cur)
+        dev = images.device
+        with torch.cuda.stream(sst):
+            images.record_stream(sst)
+            out = torch.empty(n * bound, dtype=torch.uint8, device=dev)
+            scratch = torch.empty(n * scr, dtype=torch.uint8, device=dev)
+            sizes = torch.empty(n, dtype=torch.int32, device=dev)
+            self._check(self.L.mmx_png_encode(self.ptr, C.c_void_p(images.data_ptr()), images.stride(0), n, W, H,
+                                              C.c_void_p(out.data_ptr()), bound, C.c_void_p(sizes.data_ptr()),
+                                              C.c_void_p(scratch.data_ptr())), "mmx_png_encode")
+            ends = torch.cumsum(sizes.to(torch.int64), 0)
+            starts = ends - sizes.to(torch.int64)
+            packed = torch.empty(n * bound, dtype=torch.uint8, device=dev)
+            self._check(self.L.mmx_png_pack(self.ptr, C.c_void_p(out.data_ptr()), bound, C.c_void_p(sizes.data_ptr()),
+                                            C.c_void_p(starts.data_ptr()), n, C.c_void_p(packed.data_ptr())),
+                        "mmx_png_pack")
+        cur.wait_stream(sst)
+        packed.record_stream(cur)
+        ends.record_stream(cur)
+        return packed, ends
 
     @property
     def rollout_lanes(self) -> int:

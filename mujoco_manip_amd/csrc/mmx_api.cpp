@@ -23,6 +23,11 @@ extern "C" hipError_t mmx_launch_expert(const MMXState* S, int n, float* action,
 extern "C" hipError_t mmx_launch_physics(const MMXState* S, int n, int with_ik, hipStream_t st);
 extern "C" hipError_t mmx_launch_forward(const MMXState* S, hipStream_t st);
 extern "C" hipError_t mmx_launch_render(const MMXState* S, int base, int count, hipStream_t st);
+extern "C" hipError_t mmx_launch_render_masked(const MMXState* S, int base, int count, const unsigned char* mask,
+                                               hipStream_t st);
+extern "C" hipError_t mmx_launch_queue(const MMXState* S, int* slot, int* next, int n_ep, const unsigned long long* rng,
+                                       const int* qtask, unsigned char* mask, int* task, int* slot_out, int* fin_out,
+                                       hipStream_t st);
 extern "C" hipError_t mmx_launch_png(const uint8_t* rgb, int64_t img_stride, int n, int W, int H, uint8_t* out,
                                      int64_t out_stride, int32_t* sizes, uint32_t* scratch, hipStream_t st);
 extern "C" hipError_t mmx_launch_png_pack(const uint8_t* out, int64_t out_stride, const int32_t* sizes,
@@ -57,6 +62,13 @@ struct mmx_sim {
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   std::vector<std::pair<size_t, size_t>> t_step, t_render;
+  // device-side episode queue (mmx_queue_init / mmx_queue_advance): per-slot episode, next episode,
+  // and the episodes' tasks / PCG64 states; q_n < 0: no queue
+  int* q_slot = nullptr;
+  int* q_next = nullptr;
+  int* q_task = nullptr;
+  unsigned long long* q_rng = nullptr;
+  int q_n = -1;
 };
 
 namespace {
@@ -623,6 +635,58 @@ int mmx_set_state(mmx_sim* sim, const float* qpos, const float* qvel, const floa
   if (e == hipSuccess && ctrl) e = hipMemcpy(sim->S.ctrl, ctrl, MMX_NU_ * n * 4, hipMemcpyHostToDevice);
   if (e == hipSuccess && ws) e = hipMemcpy(sim->S.qacc_ws, ws, MMX_NV_ * n * 4, hipMemcpyHostToDevice);
   return hip_check(sim, e, "mmx_set_state");
+}
+
+int mmx_queue_init(mmx_sim* sim, int32_t n_episodes, const uint64_t* seeds, const int32_t* tasks) {
+  if (!sim || n_episodes < 0 || (n_episodes > 0 && !tasks)) return MMX_EINVAL;
+  DeviceGuard guard(sim);
+  const size_t E = static_cast<size_t>(n_episodes), n = static_cast<size_t>(sim->S.N);
+  for (size_t e = 0; e < E; e++) {
+    const int t = tasks[e];
+    if (t >= 0 && ((t >> 4) > 2 || (t & 15) > 2)) return fail(sim, MMX_EINVAL, "queue task out of range");
+  }
+  if (hipStreamSynchronize(sim->stream) != hipSuccess) return fail(sim, MMX_EDEVICE, "mmx_queue_init sync");
+  for (void* p : {static_cast<void*>(sim->q_slot), static_cast<void*>(sim->q_next), static_cast<void*>(sim->q_task),
+                  static_cast<void*>(sim->q_rng)}) {
+    if (!p) continue;
+    sim->allocs.erase(std::remove(sim->allocs.begin(), sim->allocs.end(), p), sim->allocs.end());
+    (void)hipFree(p);
+  }
+  sim->q_rng = nullptr;
+  sim->q_n = -1;
+  sim->q_slot = dalloc<int>(sim, n);
+  sim->q_next = dalloc<int>(sim, 1);
+  sim->q_task = dalloc<int>(sim, std::max<size_t>(E, 1));
+  if (!sim->q_slot || !sim->q_next || !sim->q_task) return fail(sim, MMX_EDEVICE, "queue allocation");
+  std::vector<int> slot(n, -1);
+  hipError_t e = hipMemcpy(sim->q_slot, slot.data(), n * sizeof(int), hipMemcpyHostToDevice);
+  if (e == hipSuccess && E) e = hipMemcpy(sim->q_task, tasks, E * sizeof(int), hipMemcpyHostToDevice);
+  if (e == hipSuccess && seeds && E) {  // PCG64(SeedSequence(seed_e)) of every episode, once
+    std::vector<unsigned long long> rng(4 * E);
+    for (size_t k = 0; k < E; k++) {
+      uint64_t st[4];
+      pcg64_seed(seeds[k], st);
+      for (int j = 0; j < 4; j++) rng[4 * k + j] = st[j];
+    }
+    sim->q_rng = dalloc<unsigned long long>(sim, 4 * E);
+    if (!sim->q_rng) return fail(sim, MMX_EDEVICE, "queue allocation");
+    e = hipMemcpy(sim->q_rng, rng.data(), rng.size() * sizeof(unsigned long long), hipMemcpyHostToDevice);
+  }
+  if (e != hipSuccess) return hip_check(sim, e, "mmx_queue_init upload");
+  sim->q_n = n_episodes;
+  return MMX_OK;
+}
+
+int mmx_queue_advance(mmx_sim* sim, int32_t* slot_ep_dev, int32_t* fin_ep_dev) {
+  if (!sim) return MMX_EINVAL;
+  if (sim->q_n < 0) return fail(sim, MMX_EINVAL, "mmx_queue_advance without mmx_queue_init");
+  DeviceGuard guard(sim);
+  MMXState& S = sim->S;
+  hipError_t e = mmx_launch_queue(&S, sim->q_slot, sim->q_next, sim->q_n, sim->q_rng, sim->q_task, sim->d_mask,
+                                  sim->d_task, slot_ep_dev, fin_ep_dev, sim->stream);
+  if (e == hipSuccess) e = mmx_launch_reset(&S, sim->d_mask, sim->d_task, sim->stream);
+  if (e == hipSuccess) e = mmx_launch_render_masked(&S, 0, S.N, sim->d_mask, sim->stream);
+  return hip_check(sim, e, "mmx_queue_advance");
 }
 
 uint32_t mmx_episode_seed(uint64_t root, int32_t index) {

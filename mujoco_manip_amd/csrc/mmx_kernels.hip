@@ -64,6 +64,9 @@ static constexpr int kBinBody[3] = {MMX_BODY_BIN_RED, MMX_BODY_BIN_GREEN, MMX_BO
 #define MMX_CAND_MARGIN 0.08f  // m: the list's inflation of the sphere / plane test (A/B: 0.04 +0.2 %, 0.08 +0.8 %, 0.15 -0.6 %)
 #endif
 #define LD 28     // padded row stride for 27-wide rows
+#ifndef MMX_LS_EXACT
+#define MMX_LS_EXACT 1  // line search: accept a Newton root on an unchanged active set without re-evaluating
+#endif
 
 // ============================================================================ per-env LDS
 struct EnvSh {
@@ -2031,8 +2034,26 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid, int& exit) 
     c0 = wave_sum(c0);
     c1 = wave_sum(c1);
     PROBE(10, stats, STAT_T_AUX1);
+    // the lane's edge active bits at step a, laid out like `act` (bit 2q: edge 0 of slice q, with
+    // the equality row always on; bit 2q + 1: edge 1)
+    auto act_at = [&](float a) {
+      int b = 0;
+#pragma unroll
+      for (int q = 0; q < RPL; q++) {
+        if (WG * q >= nefc) break;  // uniform
+        b |= ((EQROW(q) || fmaf(a, j0[q], e0[q]) < 0.f) ? 1 : 0) << (2 * q);
+        b |= (fmaf(a, j1[q], e1[q]) < 0.f ? 2 : 0) << (2 * q);
+      }
+      return b;
+    };
+    // phi' is linear on any interval over which no edge changes state (each edge is linear in a),
+    // so a Newton root of phi' whose active set equals the set of the point it was taken from is
+    // the exact minimiser and needs no confirming evaluation: the full step a = 1 when no edge flips
+    // over it (H and g were built on the set at a = 0), later a Newton update whose set matches.
     float alpha = 1.f, lo = 0.f, hi = 3e38f;
-    for (int ls = 0; ls < 24; ls++) {
+    int bcur = act_at(1.f);
+    bool exact = MMX_LS_EXACT && __ballot(bcur != act) == 0ull;
+    for (int ls = 0; ls < 24 && !exact; ls++) {
       if (MMX_PROBE == 10 && LANE == 0) stats[STAT_T_AUX3] += 1.f;  // line-search steps
       float d1 = 0.f, d2 = 0.f;
 #pragma unroll
@@ -2049,11 +2070,15 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid, int& exit) 
       if (d1 < 0.f) lo = alpha;
       else hi = alpha;
       float na = alpha - d1 / fmaxf(d2, 1e-30f);
-      if (!(na >= lo && na <= hi)) na = hi < 3e38f ? 0.5f * (lo + hi) : 2.f * alpha;
+      const bool newton = na >= lo && na <= hi;
+      if (!newton) na = hi < 3e38f ? 0.5f * (lo + hi) : 2.f * alpha;
       if (fabsf(na - alpha) <= 1e-6f * fabsf(alpha) + 1e-12f) {
         alpha = na;
         break;
       }
+      const int bn = act_at(na);
+      exact = MMX_LS_EXACT && newton && __ballot(bn != bcur) == 0ull;
+      bcur = bn;
       alpha = na;
     }
     PROBE(1, stats, STAT_T_AUX3);
@@ -3121,7 +3146,73 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_expert_kernel(MMXState S, i
     for (int k = 0; k < 4; k++) action[(size_t)i * 4 + k] = a[k];
 }
 
+// ============================================================================ episode queue
+// Device-side slot reassignment of the dataset loop (scripts/generate_dataset.py:140-198 runs one
+// episode per env; here E episodes stream through the N env slots, mmx_queue_advance).  One
+// workgroup scans the slots in order and hands episodes next, next + 1, ... to the slots that need
+// one (no episode yet, or their FSM reached DONE = state 10, pick_and_place.py:167-277), staging the
+// reset: mask, task and the episode's PCG64(SeedSequence(seed_e)) state (generate_dataset.py:263-277).
+// The slot -> episode order is the host loop's (finished slots in ascending order).
+struct MMXQueue {
+  int* slot;                      // [N] episode running in the slot, -1: none
+  int* next;                      // [1] next episode to hand out
+  int n_ep;                       // E
+  const unsigned long long* rng;  // [E][4] initial PCG64 state per episode, or null (no reseed)
+  const int* task;                // [E] obj << 4 | bin, -1: the env's own draw
+};
+#define QWG 1024
+extern "C" __global__ void __launch_bounds__(QWG) mmx_queue_kernel(MMXState S, MMXQueue Q, unsigned char* mask, int* task,
+                                                                  int* slot_out, int* fin_out) {
+  __shared__ int scan[QWG];
+  const int t = threadIdx.x, N = S.N;
+  const int c = (N + QWG - 1) / QWG, s0 = min(N, t * c), s1 = min(N, s0 + c);  // contiguous slots per thread
+  int cnt = 0;
+  for (int s = s0; s < s1; s++) cnt += Q.slot[s] < 0 || S.epi[(size_t)s * EPI_N + EPI_FSM_STATE] == 10;
+  scan[t] = cnt;
+  __syncthreads();
+  for (int off = 1; off < QWG; off <<= 1) {  // inclusive scan of the per-thread counts
+    const int v = t >= off ? scan[t - off] : 0;
+    __syncthreads();
+    scan[t] += v;
+    __syncthreads();
+  }
+  const int base = *Q.next;
+  int e = base + scan[t] - cnt;
+  for (int s = s0; s < s1; s++) {
+    const int cur = Q.slot[s];
+    const bool ended = cur >= 0 && S.epi[(size_t)s * EPI_N + EPI_FSM_STATE] == 10;
+    int now = cur;
+    unsigned char m = 0;
+    if (cur < 0 || ended) {
+      now = e < Q.n_ep ? e : -1;
+      if (now >= 0) {
+        m = 1;
+        task[s] = Q.task[now];
+        if (Q.rng) {
+#pragma unroll
+          for (int k = 0; k < 4; k++) S.rng[4 * (size_t)s + k] = Q.rng[4 * (size_t)now + k];
+          S.epi[(size_t)s * EPI_N + EPI_RNG_HAS32] = 0;
+        }
+      }
+      e++;
+      Q.slot[s] = now;
+    }
+    mask[s] = m;
+    if (slot_out) slot_out[s] = now;
+    if (fin_out) fin_out[s] = ended ? cur : -1;
+  }
+  __syncthreads();
+  if (t == 0) *Q.next = min(Q.n_ep, base + scan[QWG - 1]);
+}
+
 // =========================================================================== host launchers
+extern "C" hipError_t mmx_launch_queue(const MMXState* S, int* slot, int* next, int n_ep, const unsigned long long* rng,
+                                       const int* qtask, unsigned char* mask, int* task, int* slot_out, int* fin_out,
+                                       hipStream_t st) {
+  const MMXQueue Q{slot, next, n_ep, rng, qtask};
+  hipLaunchKernelGGL(mmx_queue_kernel, dim3(1), dim3(QWG), 0, st, *S, Q, mask, task, slot_out, fin_out);
+  return hipGetLastError();
+}
 extern "C" hipError_t mmx_launch_reset(const MMXState* S, const unsigned char* mask, const int* task, hipStream_t st) {
   hipLaunchKernelGGL(mmx_reset_kernel, dim3(S->N), dim3(WG), 0, st, *S, mask, task);
   return hipGetLastError();

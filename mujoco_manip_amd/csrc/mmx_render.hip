@@ -239,7 +239,7 @@ DEV void shade4(const uint32_t* keys, int px0, int py, float half, float f, cons
 }
 
 extern "C" __global__ void __launch_bounds__(RWG) __attribute__((amdgpu_waves_per_eu(2 * RWG / 256, 2 * RWG / 256)))
-mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), registers to match
+mmx_render_kernel(MMXState S, int env_base, const unsigned char* mask) {  // two workgroups per CU (LDS), registers to match
   extern __shared__ __align__(16) unsigned char rsmem[];
   float4* vs = reinterpret_cast<float4*>(rsmem);                                 // [MMR_NVERT] screen
   float* bpose = reinterpret_cast<float*>(vs + MMR_NVERT);                        // [19][12]
@@ -261,7 +261,7 @@ mmx_render_kernel(MMXState S, int env_base) {  // two workgroups per CU (LDS), r
   const int rowA = blockIdx.x * kBPW * rows, rowB = min(Sz, rowA + kBPW * rows);  // the workgroup's bands
   const int ci = blockIdx.y;  // 0 overhead, 1 wrist
   const int i = env_base + blockIdx.z;
-  if (i >= S.N || rowA >= Sz) return;
+  if (i >= S.N || rowA >= Sz || (mask && !mask[i])) return;  // mask: only the envs just reset
   const float* rp = S.rpose + (size_t)i * RNSLOT * 12;
   RCLK_DECL
 
@@ -544,10 +544,16 @@ extern "C" size_t mmx_render_lds_bytes() {
          sizeof(float) * 8 * MMR_NMAT + sizeof(unsigned short) * kBPW * MMR_NTRI + sizeof(RTri) * kBigCache;
 }
 
-extern "C" hipError_t mmx_launch_render(const MMXState* S, int base, int count, hipStream_t st) {
+// envs [base, base + count); with a device mask (N bytes) only the envs whose byte is set
+extern "C" hipError_t mmx_launch_render_masked(const MMXState* S, int base, int count, const unsigned char* mask,
+                                               hipStream_t st) {
   if (count <= 0 || S->image_size <= 0) return hipSuccess;
   const int rows = rend_band_rows((S->image_size + 15) & ~15);
   const int bands = (S->image_size + rows - 1) / rows;
-  hipLaunchKernelGGL(mmx_render_kernel, dim3((bands + kBPW - 1) / kBPW, 2, count), dim3(RWG), mmx_render_lds_bytes(), st, *S, base);
+  hipLaunchKernelGGL(mmx_render_kernel, dim3((bands + kBPW - 1) / kBPW, 2, count), dim3(RWG), mmx_render_lds_bytes(), st, *S,
+                     base, mask);
   return hipGetLastError();
+}
+extern "C" hipError_t mmx_launch_render(const MMXState* S, int base, int count, hipStream_t st) {
+  return mmx_launch_render_masked(S, base, count, nullptr, st);
 }

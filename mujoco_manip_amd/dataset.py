@@ -30,6 +30,7 @@ pinned against the oracle running the reference loop (tests/test_dataset.py).
 from __future__ import annotations
 
 import argparse
+import functools
 import json
 import os
 from dataclasses import dataclass, field
@@ -92,6 +93,7 @@ def make_task_string(obj_name: str, bin_name: str) -> str:
     return f"Pick {obj_name.replace('obj_', '')} object and place in {bin_name.replace('bin_', '')} bin"
 
 
+@functools.lru_cache(maxsize=None)
 def phase_description(state: int, obj_name: str, bin_name: str) -> str:
     """PickAndPlaceTask.phase_description (pick_and_place.py:128-149) for a device FSM code."""
     phase = _STATE_PHASE[int(state)]
@@ -298,14 +300,16 @@ def _raw_image_stats(frames_u8: list) -> dict:
             "_sum": x.sum(0).tolist(), "_sumsq": (x * x).sum(0).tolist(), "_n": int(len(x))}
 
 
-def _frame_image_stats(imgs, chunk=256):
+def _frame_image_stats(imgs, chunk=None):
     """Per-frame channel statistics of uint8 images [k, H, W, 3] on the device: min, max, sum and
     sum of squares of the pixel values scaled to [0, 1] -> float64 [k, 4, 3].  Min / max on the
     uint8 values, sums exact in integers (int32 values, int64 sums) and scaled at the end, in
-    chunks of `chunk` images (no float64 copy of the frames)."""
+    chunks of `chunk` images (default: 256 MB of int32 values; no float64 copy of the frames)."""
     import torch
 
     k = imgs.shape[0]
+    if chunk is None:
+        chunk = max(1, (1 << 26) // max(1, imgs[0].numel()))
     x = imgs.reshape(k, -1, 3)
     out = torch.empty((k, 4, 3), dtype=torch.float64, device=imgs.device)
     out[:, 0] = x.amin(1).to(torch.float64) * (1.0 / 255.0)
@@ -336,15 +340,18 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
     or, with `episode_ids`, only those episodes of the `num_episodes`-episode job (a rank's shard,
     rank_episodes): each keeps its global index, seed and task.
 
-    Streaming: each step's frames (active slots only) are gathered on the device, copied to pinned
-    host memory on a side stream and split into their episodes on the host.  Camera frames are
+    Streaming with no host synchronisation per step: the slot -> episode assignment runs on the
+    device (mmx_queue_advance), each step's frames of every slot (plus the assignment) are copied
+    to pinned host memory on a side stream, and the host splits them into their episodes a few
+    steps later, as the copies complete.  Camera frames are
     encoded to PNG files on the device (mmx_png_encode; LeRobot embeds image features as PNG,
     generate_dataset.py:250-260) with their per-channel statistics, so only the compressed files
     cross PCIe and the host does no image work.  Device memory is O(envs): no frame stays on the
     device after its copy.  A finished episode (FSM DONE) is handed to `sink(episode)` in
     episode-index order, so the host holds only the episodes in flight; without a sink the episodes
     are returned as a list.  on_step(slots, episode_ids, env), when given, sees the env before each
-    batched step.  Returns (episodes or None, seeds).
+    batched step (a diagnostic hook: it costs a host synchronisation per step).  Returns (episodes or
+    None, seeds).
     """
     import torch
 
@@ -370,33 +377,17 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
     img_feats = [(cam, f) for cam, f in enumerate(IMAGE_KEYS) if f in feature_keys]
     npx = image_size * image_size
 
-    # local position e <-> global episode ids[e]: slots and rows are indexed locally
+    # local position e <-> global episode ids[e]: slots and rows are indexed locally.  The slot ->
+    # episode assignment runs on the device (mmx_queue_advance): a slot whose episode's FSM reached
+    # DONE takes the next episode and is reset with its seed and task, in ascending slot order, with
+    # no host synchronisation; the host learns the assignment from the per-step copies.
     eps = [Episode(g, *task_list[g % len(task_list)], seeds[g] if seeds else None) for g in ids]
-    slot_ep = np.full(N, -1, np.int64)
-    next_ep = 0
+    env.sim.queue_init([(OBJECTS.index(ep.obj) << 4) | BINS.index(ep.bin) for ep in eps],
+                       [ep.seed for ep in eps] if seeds else None)
     out_eps = [] if sink is None else None
     emitted = 0
     done_eps = {}  # finished, awaiting in-order emission: episode -> True
     ep_slot = np.full(E, -1, np.int64)  # the slot an episode ran in
-
-    def assign(slots):
-        nonlocal next_ep
-        mask = np.zeros(N, np.uint8)
-        sd = [None] * N
-        task = np.full(N, -1, np.int32)
-        for s in slots:
-            if next_ep >= E:
-                slot_ep[s] = -1
-                continue
-            ep = eps[next_ep]
-            slot_ep[s] = next_ep
-            ep_slot[next_ep] = s
-            next_ep += 1
-            mask[s] = 1
-            sd[s] = ep.seed
-            task[s] = (OBJECTS.index(ep.obj) << 4) | BINS.index(ep.bin)
-        if mask.any():
-            env.sim.reset(seeds=sd if seeds else None, task_override=task, env_mask=mask)
 
     # Host-side per-slot frame buffers: a slot's running episode gets one row per step, written for
     # all of the step's slots at once (one fancy-indexed store per feature); an episode's rows are
@@ -408,9 +399,10 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
     buf_ep = np.full(N, -1, np.int64)  # the episode whose rows the slot holds
     png_rows = {f: [[] for _ in range(N)] for _, f in img_feats}
 
-    def absorb(host, slots, ep_ids, png_offs):
+    def absorb(host, slots, ep_ids, png):
         if len(ep_ids) == 0:
             return
+        ep_slot[ep_ids] = slots
         new = buf_ep[slots] != ep_ids
         if new.any():
             ns = slots[new]
@@ -427,16 +419,16 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
                 g[:, :v.shape[1]] = v
                 bufs[k] = g
         for k, v in host.items():
-            if k.endswith("/png"):
+            if k.endswith("/png") or k.endswith("/ends") or k.startswith("_q"):
                 continue
             if k not in bufs:
                 bufs[k] = np.empty((N, cap[0]) + v.shape[1:], v.dtype)
-            bufs[k][slots, t] = v
-        for f, offs in png_offs.items():
-            data = host[f + "/png"].tobytes()
+            bufs[k][slots, t] = v[slots]
+        for f, data in png.items():
+            ends = host[f + "/ends"]
             rows_f = png_rows[f]
-            for j, s in enumerate(slots.tolist()):
-                rows_f[s].append(data[offs[j]:offs[j + 1]])
+            for s in slots.tolist():
+                rows_f[s].append(data[ends[s - 1] if s else 0:ends[s]])
         tpos[slots] = t + 1
 
     def finish(e):
@@ -461,7 +453,7 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
             buf_ep[s] = -1
         done_eps[e] = True
 
-    def emit_ready(block=False):
+    def emit_ready():
         nonlocal emitted
         while emitted < E and emitted in done_eps:
             e = emitted
@@ -473,87 +465,86 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
                 out_eps.append(eps[e])
             emitted += 1
 
-    ring = _PinnedRing(dev)
-    step_no = 0
+    import torch
 
-    finished_eps = set()
+    ring = _PinnedRing(dev)
+    slot_dev = torch.empty(N, dtype=torch.int32, device=dev)
+    fin_dev = torch.empty(N, dtype=torch.int32, device=dev)
+    png_est = {}  # camera feature -> bytes copied per step: 1.25 x the largest packed size seen + 1 MB
+    png_max = {}
+    state = {"over": False, "started": False}
 
     def process(items):
         for host, payload in items:
-            for e in payload[2]:  # ended before this step: every row of theirs is absorbed
+            fin = host["_q_fin"]
+            for e in fin[fin >= 0].tolist():  # ended before this step: every row of theirs is absorbed
                 finish(e)
-                finished_eps.add(e)
-            absorb(host, payload[0], payload[1], payload[3])
+            slot = host["_q_slot"]
+            act = np.nonzero(slot >= 0)[0]
+            if len(act) == 0:
+                state["over"] = state["over"] or state["started"]
+                continue
+            state["started"] = True
+            png = {}
+            for f, packed in payload.items():  # the step's packed PNG files (copied: a prefix)
+                total = int(host[f + "/ends"][-1])
+                data = host[f + "/png"]
+                if total > len(data):  # more than the estimate: fetch the rest (rare)
+                    data = np.concatenate([data, packed[len(data):total].cpu().numpy()])
+                png_max[f] = max(png_max.get(f, 0), total)
+                png_est[f] = (png_max[f] * 5) // 4 + (1 << 20)
+                png[f] = data.tobytes()
+            absorb(host, act, slot[act].astype(np.int64), png)
 
-    assign(range(N))
-    fsm_view = env._epi[:, 4]
-    while (slot_ep >= 0).any():
+    step_no = 0
+    while not state["over"]:
         if step_no >= max_gym_steps:
-            raise RuntimeError(f"episodes {sorted(set(slot_ep[slot_ep >= 0].tolist()))} did not finish "
-                               f"within {max_gym_steps} gym steps")
-        # the slot reassignment needs the FSM state on the host: one small copy per step (the
-        # frames themselves never wait for it)
-        done_before = (fsm_view == FSM_DONE).cpu().numpy()
-        finished = np.where((slot_ep >= 0) & done_before)[0]
-        fin_eps = [int(slot_ep[s]) for s in finished]
-        if len(finished):
-            for s in finished:
-                slot_ep[s] = -1
-            assign(finished)
-            done_before = (fsm_view == FSM_DONE).cpu().numpy()
-        act_slots = np.where((slot_ep >= 0) & ~done_before)[0]
-        if len(act_slots) == 0:
-            if fin_eps:
-                ring.push({}, (act_slots, np.zeros(0, np.int64), fin_eps, {}))
-            process(ring.ready())
-            emit_ready()
-            continue
-        idx = torch.as_tensor(act_slots, device=dev)
-        obs_pre = env._obs.index_select(0, idx)  # PRE-step obs (from the reset or the previous step)
+            raise RuntimeError(f"episodes did not finish within {max_gym_steps} gym steps")
+        env.sim.queue_advance(slot_dev.data_ptr(), fin_dev.data_ptr())  # resets the slots it assigns
         action = env.expert_plan(ACTION_REPEAT)  # fsm.plan(16) -> (target, gripper) for every slot
-        frame = {}
+        frame = {"_q_slot": slot_dev.clone(), "_q_fin": fin_dev.clone()}
+        obs_pre = env._obs.clone()  # PRE-step obs (from the reset or the previous step)
         for k, f in obs_feats:
             a, b, _ = OBS_SLICES[k]
             frame[f] = obs_pre[:, a:b]
-        png_offs = {}
+        payload = {}
         for cam, f in img_feats:  # PRE-step images (rendered after the reset / previous step)
-            imgs = env._images[:, cam].index_select(0, idx)
-            frame[f + "/png"], png_offs[f] = env.sim.png_encode(imgs)
+            imgs = env._images[:, cam]
+            packed, ends = env.sim.png_encode_device(imgs)
+            if f not in png_est:
+                png_est[f] = packed.numel() // 4
+            frame[f + "/png"] = packed[:min(png_est[f], packed.numel())]
+            frame[f + "/ends"] = ends
             frame[f + "/stats"] = _frame_image_stats(imgs)
-        a_sel = action.index_select(0, idx)
+            payload[f] = packed
         if need_actions:
-            T = env.initial_ee_se3.index_select(0, idx)
-            enc = encode_actions(a_sel[:, :3], a_sel[:, 3], T)
+            enc = encode_actions(action[:, :3], action[:, 3], env.initial_ee_se3)
             for k in ACTION_KEYS:
                 if k in feature_keys:
                     frame[k] = enc[k]
-        frame["_fsm"] = fsm_view.index_select(0, idx)
-        if on_step is not None:
-            on_step(act_slots, np.asarray(ids, np.int64)[slot_ep[act_slots]], env)
-        env.step(action)
+        frame["_fsm"] = env._epi[:, 4].clone()
+        if on_step is not None:  # diagnostic hook: reads the assignment back (a host sync per step)
+            sl = slot_dev.cpu().numpy()
+            act_slots = np.nonzero(sl >= 0)[0]
+            on_step(act_slots, np.asarray(ids, np.int64)[sl[act_slots]], env)
+        env.sim.step(action.data_ptr(), action.shape[1])
         if need_reward:
-            frame["next.reward"] = env._rc.index_select(0, idx)
-        ring.push(frame, (act_slots, slot_ep[act_slots].copy(), fin_eps, png_offs))
+            frame["next.reward"] = env._rc.clone()
+        ring.push(frame, payload)
         process(ring.ready())
         emit_ready()
         step_no += 1
     process(ring.drain())
-    for e in range(E):  # every slot finished: the remaining episodes end here
-        if e not in finished_eps and e >= emitted:
+    for e in range(E):  # episodes still open when the loop ended (none, unless max_gym_steps cut it)
+        if e >= emitted and e not in done_eps:
             finish(e)
-    emit_ready(block=True)
+    emit_ready()
     torch.cuda.synchronize(dev)
     env.close()
     return out_eps, seeds
 
 
 # ----------------------------------------------------------------------------- LeRobot v3.0 writer
-def _feature_stats(x: np.ndarray) -> dict:
-    x = x.reshape(len(x), -1).astype(np.float64)
-    return {"min": x.min(0).tolist(), "max": x.max(0).tolist(), "mean": x.mean(0).tolist(),
-            "std": x.std(0).tolist(), "count": [int(len(x))]}
-
-
 class LeRobotWriter:
     """Streaming LeRobot v3.0 writer (use_videos=False: image features embedded as parquet structs
     {bytes: PNG, path}).  Episodes are added one at a time in episode-index order and appended to
@@ -567,7 +558,8 @@ class LeRobotWriter:
 
     def __init__(self, root: str, repo_id: str, features: dict, *, fps=CONTROL_FPS, robot_type="franka_panda",
                  chunks_size=1000, data_files_size_in_mb=100, threaded=False, queue_depth=64,
-                 image_compression="SNAPPY", keep_image_sums=False, io_threads=None):
+                 image_compression="SNAPPY", keep_image_sums=False, io_threads=None, batch_episodes=64,
+                 batch_mb=64):
         import pyarrow as pa
         import pyarrow.parquet  # noqa: F401  (imported here, not on the first episode)
 
@@ -587,6 +579,10 @@ class LeRobotWriter:
         self.num_acc = {}  # feature -> [min, max, sum, sumsq, count]
         self.img_acc = {}  # feature -> [min, max, sum, sumsq, pixels, frames]
         self.n_episodes = 0
+        # episodes are encoded in batches (one arrow table / parquet row group per run of episodes
+        # that land in the same data file): the per-table arrow overhead is paid once per batch
+        self.batch_episodes, self.batch_bytes = max(1, int(batch_episodes)), float(batch_mb) * 1024 * 1024
+        self.pending, self.pending_bytes = [], 0
         self.image_compression = image_compression
         # shards keep each episode's raw image sums in meta/episodes, so merge_shards rebuilds the
         # dataset statistics bit for bit
@@ -639,31 +635,47 @@ class LeRobotWriter:
             self.tasks.append(t)
         return t
 
-    def _table(self, ep, start):
+    def _table(self, eps, starts):
+        """One arrow table holding the frames of consecutive episodes `eps` (dataset indices from
+        `starts`)."""
         pa = self.pa
-        n = ep.length
+        lens = [ep.length for ep in eps]
         cols, fields = {}, []
         for k in self.num_keys:
             dim = int(np.prod(self.features[k]["shape"]))
-            arr = np.asarray(ep.frames[k], np.float32).reshape(n, dim)
+            arr = np.concatenate([np.asarray(ep.frames[k], np.float32).reshape(ep.length, dim) for ep in eps])
             cols[k] = pa.FixedSizeListArray.from_arrays(pa.array(arr.ravel(), pa.float32()), dim)
             fields.append(pa.field(k, pa.list_(pa.float32(), dim)))
         for k in self.str_keys:
-            cols[k] = pa.array(list(ep.frames[k]), pa.string())
+            cols[k] = pa.array([v for ep in eps for v in ep.frames[k]], pa.string())
             fields.append(pa.field(k, pa.string()))
         for k in self.img_keys:  # LeRobot's embedded image layout (images/<key>/episode_<e>/frame_<i>.png)
-            paths = pa.array([f"images/{k}/episode_{ep.index:06d}/frame_{i:06d}.png" for i in range(n)], pa.string())
-            cols[k] = pa.StructArray.from_arrays([pa.array(ep.frames[k], pa.binary()), paths],
+            paths = pa.array([f"images/{k}/episode_{ep.index:06d}/frame_{i:06d}.png" for ep in eps for i in range(ep.length)],
+                             pa.string())
+            cols[k] = pa.StructArray.from_arrays([pa.array([v for ep in eps for v in ep.frames[k]], pa.binary()), paths],
                                                  fields=list(self.img_type))
             fields.append(pa.field(k, self.img_type))
-        fi = np.arange(n, dtype=np.int64)
+        fi = np.concatenate([np.arange(L, dtype=np.int64) for L in lens])
         extra = {"timestamp": pa.array((fi / self.fps).astype(np.float32)), "frame_index": pa.array(fi),
-                 "episode_index": pa.array(np.full(n, ep.index, np.int64)), "index": pa.array(start + fi),
-                 "task_index": pa.array(np.full(n, self.task_idx[make_task_string(ep.obj, ep.bin)], np.int64))}
+                 "episode_index": pa.array(np.repeat(np.array([ep.index for ep in eps], np.int64), lens)),
+                 "index": pa.array(np.concatenate([st + np.arange(L, dtype=np.int64) for st, L in zip(starts, lens)])),
+                 "task_index": pa.array(np.repeat(np.array([self.task_idx[make_task_string(ep.obj, ep.bin)] for ep in eps],
+                                                           np.int64), lens))}
         for k, v in extra.items():
             cols[k] = v
             fields.append(pa.field(k, v.type))
         return pa.Table.from_arrays([cols[f.name] for f in fields], schema=pa.schema(fields))
+
+    def _episode_bytes(self, ep):
+        """An episode's size in the data file (the roll-over test): its column data."""
+        n = 0
+        for k in self.num_keys:
+            n += 4 * ep.length * int(np.prod(self.features[k]["shape"]))
+        for k in self.str_keys:
+            n += sum(len(v) + 4 for v in ep.frames[k])
+        for k in self.img_keys:
+            n += sum(len(v) + 4 for v in ep.frames[k]) + 50 * ep.length
+        return n + 36 * ep.length
 
     @staticmethod
     def _leaf_columns(schema):
@@ -721,45 +733,30 @@ class LeRobotWriter:
             self._add(ep)
 
     def _add(self, ep):
-        import pyarrow.parquet as pq
-
         self._task(ep)
-        tab = self._table(ep, self.start)
-        if self.writer is not None and self.cur_bytes + tab.nbytes > self.limit:
-            self._close_file()
-        if self.writer is None:
-            d = os.path.join(self.root, "data", f"chunk-{self.chunk:03d}")
-            os.makedirs(d, exist_ok=True)
-            # PNG bytes are unique per frame: no dictionary attempt on them; their compression is
-            # `image_compression` (SNAPPY, parquet's and LeRobot's default, still saves ~17 % on the
-            # fixed-Huffman PNGs; NONE writes faster), the other columns keep dictionary + snappy
-            plain = [c for c in tab.column_names if c not in self.img_keys]
-            comp = {c: (self.image_compression if c.endswith(".bytes") and c[:-6] in self.img_keys else "SNAPPY")
-                    for c in self._leaf_columns(tab.schema)}
-            path = os.path.join(d, f"file-{self.fileno:03d}.parquet")
-            self.writer = {"path": path, "lane": self._nfile % self.io_threads, "w": None,
-                           "schema": tab.schema, "kw": dict(use_dictionary=plain, compression=comp)}
-            self._nfile += 1
-
-        def write(st, tab=tab):
-            if st["w"] is None:
-                st["w"] = pq.ParquetWriter(st["path"], st["schema"], **st["kw"])
-            st["w"].write_table(tab)
-
-        self._io(write, self.writer)
-        self.cur_bytes += tab.nbytes
         row = {"episode_index": ep.index, "tasks": [make_task_string(ep.obj, ep.bin)], "length": ep.length,
-               "data/chunk_index": self.chunk, "data/file_index": self.fileno, "dataset_from_index": self.start,
+               "data/chunk_index": None, "data/file_index": None, "dataset_from_index": self.start,
                "dataset_to_index": self.start + ep.length, "meta/episodes/chunk_index": 0,
                "meta/episodes/file_index": 0}
-        for k in self.num_keys:
-            x = np.asarray(ep.frames[k], np.float64).reshape(ep.length, -1)
-            for st, v in _feature_stats(x).items():
-                row[f"stats/{k}/{st}"] = v
-            acc = self.num_acc.get(k)
-            mn, mx, sm, sq = x.min(0), x.max(0), x.sum(0), (x * x).sum(0)
-            self.num_acc[k] = [mn, mx, sm, sq, len(x)] if acc is None else \
-                [np.minimum(acc[0], mn), np.maximum(acc[1], mx), acc[2] + sm, acc[3] + sq, acc[4] + len(x)]
+        if self.num_keys:  # every numeric feature's statistics from one [length, sum of dims] array
+            xs = [np.asarray(ep.frames[k], np.float64).reshape(ep.length, -1) for k in self.num_keys]
+            X = np.concatenate(xs, axis=1)
+            mn, mx, sm = X.min(0), X.max(0), X.sum(0)
+            mean = sm / ep.length
+            d = X - mean
+            std = np.sqrt((d * d).sum(0) / ep.length)  # np.std's two-pass form
+            sq = (X * X).sum(0)
+            o = 0
+            for k, x in zip(self.num_keys, xs):
+                sl = slice(o, o + x.shape[1])
+                o += x.shape[1]
+                row[f"stats/{k}/min"], row[f"stats/{k}/max"] = mn[sl].tolist(), mx[sl].tolist()
+                row[f"stats/{k}/mean"], row[f"stats/{k}/std"] = mean[sl].tolist(), std[sl].tolist()
+                row[f"stats/{k}/count"] = [int(ep.length)]
+                acc = self.num_acc.get(k)
+                self.num_acc[k] = [mn[sl], mx[sl], sm[sl], sq[sl], ep.length] if acc is None else \
+                    [np.minimum(acc[0], mn[sl]), np.maximum(acc[1], mx[sl]), acc[2] + sm[sl], acc[3] + sq[sl],
+                     acc[4] + ep.length]
         for k in self.img_keys:
             st = (getattr(ep, "image_stats", None) or {}).get(k)
             if st is None:  # episodes built elsewhere: decode a frame sample
@@ -778,8 +775,58 @@ class LeRobotWriter:
             self.img_acc[k] = vals if acc is None else [np.minimum(acc[0], mn), np.maximum(acc[1], mx), acc[2] + vals[2],
                                                         acc[3] + vals[3], acc[4] + vals[4], acc[5] + vals[5]]
         self.ep_rows.append(row)
+        nb = self._episode_bytes(ep)
+        self.pending.append((ep, row, self.start, nb))
+        self.pending_bytes += nb
         self.start += ep.length
         self.n_episodes += 1
+        if len(self.pending) >= self.batch_episodes or self.pending_bytes >= self.batch_bytes:
+            self._flush()
+
+    def _flush(self):
+        """Write the pending episodes: each goes to the open data file unless its bytes would take
+        the file past data_files_size_in_mb (then the file is closed and the next one opened); the
+        episodes of one file are written as one table."""
+        import pyarrow.parquet as pq
+
+        pending, self.pending, self.pending_bytes = self.pending, [], 0
+        run = []
+
+        def emit():
+            if not run:
+                return
+            tab = self._table([r[0] for r in run], [r[2] for r in run])
+            if self.writer is None:
+                d = os.path.join(self.root, "data", f"chunk-{self.chunk:03d}")
+                os.makedirs(d, exist_ok=True)
+                # PNG bytes are unique per frame: no dictionary attempt on them; their compression is
+                # `image_compression` (SNAPPY, parquet's and LeRobot's default, still saves ~17 % on the
+                # fixed-Huffman PNGs; NONE writes faster), the other columns keep dictionary + snappy
+                plain = [c for c in tab.column_names if c not in self.img_keys]
+                comp = {c: (self.image_compression if c.endswith(".bytes") and c[:-6] in self.img_keys else "SNAPPY")
+                        for c in self._leaf_columns(tab.schema)}
+                path = os.path.join(d, f"file-{self.fileno:03d}.parquet")
+                self.writer = {"path": path, "lane": self._nfile % self.io_threads, "w": None,
+                               "schema": tab.schema, "kw": dict(use_dictionary=plain, compression=comp)}
+                self._nfile += 1
+
+            def write(st, tab=tab):
+                if st["w"] is None:
+                    st["w"] = pq.ParquetWriter(st["path"], st["schema"], **st["kw"])
+                st["w"].write_table(tab)
+
+            self._io(write, self.writer)
+            run.clear()
+
+        for item in pending:
+            ep, row, start, nb = item
+            if self.cur_bytes > 0 and self.cur_bytes + nb > self.limit:
+                emit()
+                self._close_file()
+            row["data/chunk_index"], row["data/file_index"] = self.chunk, self.fileno
+            run.append(item)
+            self.cur_bytes += nb
+        emit()
 
     def close(self, extra_info=None):
         import pyarrow as pa
@@ -790,6 +837,7 @@ class LeRobotWriter:
             self._thread.join()
             self._q, self._thread = None, None
             self._raise_pending()
+        self._flush()
         self._close_file()
         if self._lanes is not None:
             self._io_wait()

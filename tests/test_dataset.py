@@ -293,6 +293,67 @@ def test_batched_episodes_match_oracle_run_episode():
 
 
 @pytest.mark.gpu
+def test_device_episode_queue():
+    """mmx_queue_advance, the dataset loop's slot reassignment on the device: episodes go to the
+    free / FSM-DONE slots in ascending slot order, each exactly once, the ended episode is reported
+    per slot, and an assigned slot's state is bit for bit PickPlaceGymEnv.reset with that episode's
+    seed and task (generate_dataset.py:263-277)."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs an MI355X")
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    N, E = 3, 7
+    seeds = D.episode_seeds(5, E)
+    tl = TASK_SETS["all"]
+    codes = [(OBJECTS.index(tl[e % len(tl)][0]) << 4) | BINS.index(tl[e % len(tl)][1]) for e in range(E)]
+    env = PickPlaceVecEnv(N, action_mode="abs_pos", randomize_objects=True, image_size=0)
+    env.sim.queue_init(codes, seeds)
+    slot = torch.empty(N, dtype=torch.int32, device=env.device)
+    fin = torch.empty_like(slot)
+
+    def reset_state(e):
+        ref = PickPlaceVecEnv(1, action_mode="abs_pos", randomize_objects=True, image_size=0)
+        ref.sim.reset(seeds=[seeds[e]], task_override=np.array([codes[e]], np.int32))
+        q, v, _, _ = ref.sim.get_state()
+        o = ref._obs.cpu().numpy()[0]
+        ref.close()
+        return q[0], v[0], o
+
+    def check_slot(s, e):
+        q, v, _, _ = env.sim.get_state()
+        rq, rv, ro = reset_state(e)
+        assert (q[s] == rq).all() and (v[s] == rv).all(), (s, e)
+        assert (env._obs.cpu().numpy()[s] == ro).all(), (s, e)
+
+    env.sim.queue_advance(slot.data_ptr(), fin.data_ptr())
+    assert slot.tolist() == [0, 1, 2] and fin.tolist() == [-1, -1, -1]
+    for s in range(N):
+        check_slot(s, s)
+    ended, nxt, checked = [], N, 0
+    for _ in range(1500):
+        a = env.expert_plan(16)
+        env.sim.step(a.data_ptr(), a.shape[1])
+        prev = slot.tolist()
+        env.sim.queue_advance(slot.data_ptr(), fin.data_ptr())
+        sl, fl = slot.tolist(), fin.tolist()
+        for s in range(N):
+            if fl[s] >= 0:  # the slot's episode ended: it takes the next one (ascending slot order)
+                assert fl[s] == prev[s]
+                ended.append(fl[s])
+                assert sl[s] == (nxt if nxt < E else -1)
+                if nxt < E and checked < 2:
+                    check_slot(s, nxt)
+                    checked += 1
+                nxt += 1
+            else:
+                assert sl[s] == prev[s]
+        if all(x < 0 for x in sl):
+            break
+    assert sorted(ended) == list(range(E)) and checked == 2
+    env.close()
+
+
+@pytest.mark.gpu
 def test_generate_then_replay_reproduces_trajectory(tmp_path):
     if not torch.cuda.is_available():
         pytest.skip("needs an MI355X")

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--keep", action="store_true")
     ap.add_argument("--image-compression", default="SNAPPY", choices=("SNAPPY", "NONE"))
     ap.add_argument("--io-threads", type=int, default=None, help="LeRobotWriter I/O lanes (default 4)")
+    ap.add_argument("--no-write", action="store_true", help="collect only: the sink drops the episodes")
+    ap.add_argument("--cprofile", default=None, help="cProfile the collecting thread into this .txt")
     a = ap.parse_args()
 
     import torch
@@ -58,19 +60,36 @@ def main():
     def sink(ep):
         frames[0] += ep.length
         png_bytes[0] += sum(len(b) for k in D.IMAGE_KEYS for b in ep.frames.get(k, []))
+        if a.no_write:
+            return
         writer.add_episode(ep)
 
+    prof = None
+    if a.cprofile:
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     t0 = time.perf_counter()
     D.collect_episodes(a.episodes, D.TASK_SETS["all"], set(feats), randomize_objects=True, seed=0,
                        num_envs=a.num_envs, sink=sink, image_size=a.image_size,
                        on_step=on_step)
     info = writer.close()
     dt = time.perf_counter() - t0
+    if prof is not None:
+        import io
+        import pstats
+        prof.disable()
+        buf = io.StringIO()
+        pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(40)
+        pstats.Stats(prof, stream=buf).sort_stats("cumulative").print_stats(40)
+        open(a.cprofile, "w").write(buf.getvalue())
+    if a.no_write:
+        info = {"total_episodes": a.episodes, "total_frames": frames[0]}
     rss = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024.0  # MB (Linux: KB)
     size = sum(os.path.getsize(os.path.join(d, f)) for d, _, fs in os.walk(path) for f in fs)
     rec = {"config": {"num_envs": a.num_envs, "episodes": a.episodes, "image_size": a.image_size,
                       "png": "device (mmx_png_encode)", "image_compression": a.image_compression,
-                      "writer": f"LeRobotWriter(threaded=True, io_threads={writer.io_threads})", "root": a.root, "features": "all (2 cameras, numeric, actions, reward, phase)"},
+                      "writer": "none (--no-write)" if a.no_write else f"LeRobotWriter(threaded=True, io_threads={writer.io_threads})", "root": a.root, "features": "all (2 cameras, numeric, actions, reward, phase)"},
            "episodes": info["total_episodes"], "frames": info["total_frames"], "seconds": dt,
            "frames_per_s": info["total_frames"] / dt, "images_per_s": 2 * info["total_frames"] / dt,
            "png_mean_bytes": png_bytes[0] / max(2 * frames[0], 1), "dataset_bytes": size,
