@@ -64,9 +64,6 @@ static constexpr int kBinBody[3] = {MMX_BODY_BIN_RED, MMX_BODY_BIN_GREEN, MMX_BO
 #define MMX_CAND_MARGIN 0.08f  // m: the list's inflation of the sphere / plane test (A/B: 0.04 +0.2 %, 0.08 +0.8 %, 0.15 -0.6 %)
 #endif
 #define LD 28     // padded row stride for 27-wide rows
-#ifndef MMX_LS_EXACT
-#define MMX_LS_EXACT 1  // line search: accept a Newton root on an unchanged active set without re-evaluating
-#endif
 
 // ============================================================================ per-env LDS
 struct EnvSh {
@@ -90,7 +87,13 @@ struct EnvSh {
   // stored: the solver forms them from the basis rows (2/3 of the storage and MFMA steps).
   // Rows past MMX_LDSEFC (a pile of contacts) live in the env's HBM overflow block `ovf` (J rows,
   // then D, then NC): lane-owned row q >= LDSEFC / 64 is always an HBM row.
-  alignas(16) float J[MMX_LDSEFC][16];  // slots past the row's width = 0; slot 15 = the row's aref
+  // Chunk-major (r04): chunk q (slots 4q..4q+3) of row i at J[q][i], a chunk-row stride of
+  // MMX_LDSEFC + 1 chunks.  A row-per-lane read of chunk q is one ds_read_b128 at an immediate
+  // offset with consecutive lanes on consecutive 16-byte bank quads (conflict-free); the Hessian
+  // staging's reads of one row's slot (lane & 15) land on 16 different banks.  Row-major 64-byte
+  // rows put lanes 4 apart on one bank (4-way): LDS bank conflicts 0.71 -> 0.31 cycles per
+  // LDS-active cycle, +0.75 % env steps/s at unchanged VALU (A/B).
+  alignas(16) float J[4][MMX_LDSEFC + 1][4];  // J[k >> 2][i][k & 3] = slot k of row i (past the width 0; 15 = aref)
   unsigned char hdr[MMX_MAXEFC];  // b0 | b1 << 4 (block 15 = none); row 0 is the equality
   // D: the row's 1 / R while the rows are built (doubling as the row -> contact map before) and in
   // the solver's setup; then per Newton iteration the diagonal entry of the group's edge-weight
@@ -147,26 +150,30 @@ static_assert(MMX_NGEOM * GXS <= COL_CAND && MMX_NPAIR <= COL_LIST && MMX_NPAIR 
 static_assert(SCR_BIAS + 9 <= 4096 && SCR_OBS + MMX_NOBS <= SCR_ACT && SCR_ACT + 12 <= MMX_LDSEFC * 16,
               "E.J scratch layout");
 static_assert(27 * 27 <= MMX_MAXCON * CON_F, "Newton Cholesky transpose exceeds E.con");
-DEV float* scr_of(EnvSh& E) { return &E.J[0][0]; }
-DEV float* obs_of(EnvSh& E) { return &E.J[0][0] + SCR_OBS; }
-DEV const float* obs_of(const EnvSh& E) { return &E.J[0][0] + SCR_OBS; }
+DEV float* scr_of(EnvSh& E) { return reinterpret_cast<float*>(&E.J); }
+DEV const float* scr_of(const EnvSh& E) { return reinterpret_cast<const float*>(&E.J); }
+DEV float* obs_of(EnvSh& E) { return scr_of(E) + SCR_OBS; }
+DEV const float* obs_of(const EnvSh& E) { return scr_of(E) + SCR_OBS; }
 DEV float* lrow_of(EnvSh& E) { return &E.con[0][0]; }  // [27][27] Newton factor / staging tile
 // the rows' mu between the row build and the solver setup (E.con is dead once the rows exist)
 DEV float* mu_stage(EnvSh& E) { return &E.con[0][0]; }
 static_assert(MMX_MAXEFC <= MMX_MAXCON * CON_F, "row mu staging exceeds E.con");
-// Constraint row i: J in E.J[i] and D in E.D[i] for i < MMX_LDSEFC, else in the env's HBM
+// Constraint row i: J in E.J[.][i] (chunk-major) and D in E.D[i] for i < MMX_LDSEFC, else in the env's HBM
 // overflow block (J rows [OVFEFC][16], then D [OVFEFC]).  For a lane-owned row i = LANE + 64 q the
 // test folds at compile time (LANE's known bits), so the unrolled loops carry no branch.
 static_assert(MMX_LDSEFC % WG == 0 && MMX_LDSEFC <= MMX_MAXEFC, "LDS rows: whole lane slices");
 DEV float* ovf_j(const EnvSh& E, int i) { return E.ovf + 16 * (i - MMX_LDSEFC); }
 DEV float* ovf_d(const EnvSh& E, int i) { return E.ovf + 16 * MMX_OVFEFC + (i - MMX_LDSEFC); }
 DEV float* ovf_nc(const EnvSh& E, int i) { return E.ovf + 17 * MMX_OVFEFC + (i - MMX_LDSEFC); }
+DEV float& jlds(EnvSh& E, int i, int k) { return E.J[k >> 2][i][k & 3]; }
+DEV const float& jlds(const EnvSh& E, int i, int k) { return E.J[k >> 2][i][k & 3]; }
 DEV float4 jrow4(const EnvSh& E, int i, int q) {
-  return i < MMX_LDSEFC ? reinterpret_cast<const float4*>(E.J[i])[q] : reinterpret_cast<const float4*>(ovf_j(E, i))[q];
+  if (i >= MMX_LDSEFC) return reinterpret_cast<const float4*>(ovf_j(E, i))[q];
+  return *reinterpret_cast<const float4*>(E.J[q][i]);
 }
-DEV float jget(const EnvSh& E, int i, int k) { return i < MMX_LDSEFC ? E.J[i][k] : ovf_j(E, i)[k]; }
+DEV float jget(const EnvSh& E, int i, int k) { return i < MMX_LDSEFC ? jlds(E, i, k) : ovf_j(E, i)[k]; }
 DEV void jset(EnvSh& E, int i, int k, float v) {
-  if (i < MMX_LDSEFC) E.J[i][k] = v;
+  if (i < MMX_LDSEFC) jlds(E, i, k) = v;
   else ovf_j(E, i)[k] = v;
 }
 DEV float dget(const EnvSh& E, int i) { return i < MMX_LDSEFC ? E.D[i] : *ovf_d(E, i); }
@@ -771,7 +778,7 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
     E.ncon = 0;
     E.flags &= ~(SHF_ROBOT_OBST | SHF_CON_OVF);
   }
-  float* scr = &E.J[0][0];
+  float* scr = scr_of(E);
   float* gx = scr + COL_GX;
   int* cand = reinterpret_cast<int*>(scr + COL_CAND);
   // (2) runs over the persistent list when it is still valid: its pairs were within
@@ -944,7 +951,7 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
 DEV void collide_pairs(EnvSh& E, bool only_ro, int which) {
   float* stats = E.stats;
   CLK_DECL;
-  float* scr = &E.J[0][0];
+  float* scr = scr_of(E);
   const float* gx = scr + COL_GX;
   const int* cand = reinterpret_cast<const int*>(scr + COL_CAND);
   const int n0 = E.ncls[0], n1 = E.ncls[1], n2 = E.ncls[2];
@@ -991,7 +998,7 @@ DEV void collide_pairs(EnvSh& E, bool only_ro, int which) {
 DEV void collide_sort(EnvSh& E) {
   float* stats = E.stats;
   CLK_DECL;
-  float* scr = &E.J[0][0];
+  float* scr = scr_of(E);
   const int n = min(E.ncon, MMX_MAXCON);
   float* tmp = scr + COL_WORK;
   int kb = 0, rank = 0;
@@ -1030,10 +1037,18 @@ DEV void row_ref(const float* solref, const float* solimp, float pos, float& imp
 }
 DEV void store_row(EnvSh& E, int row, const float* jv, int hdr, float vel, float imp_ratio, float kid, float B,
                    float diag) {
-  float4* Jr = reinterpret_cast<float4*>(row < MMX_LDSEFC ? E.J[row] : ovf_j(E, row));
+  const float aref = -B * vel - kid;  // slot 15
+  if (row < MMX_LDSEFC) {
 #pragma unroll
-  for (int q = 0; q < 3; q++) Jr[q] = make_float4(jv[4 * q], jv[4 * q + 1], jv[4 * q + 2], jv[4 * q + 3]);
-  Jr[3] = make_float4(jv[12], jv[13], jv[14], -B * vel - kid);  // slot 15: aref
+    for (int q = 0; q < 3; q++)
+      *reinterpret_cast<float4*>(E.J[q][row]) = make_float4(jv[4 * q], jv[4 * q + 1], jv[4 * q + 2], jv[4 * q + 3]);
+    *reinterpret_cast<float4*>(E.J[3][row]) = make_float4(jv[12], jv[13], jv[14], aref);
+  } else {
+    float4* Jr = reinterpret_cast<float4*>(ovf_j(E, row));
+#pragma unroll
+    for (int q = 0; q < 3; q++) Jr[q] = make_float4(jv[4 * q], jv[4 * q + 1], jv[4 * q + 2], jv[4 * q + 3]);
+    Jr[3] = make_float4(jv[12], jv[13], jv[14], aref);
+  }
   E.hdr[row] = (unsigned char)hdr;
   dset(E, row, 1.f / fmaxf(imp_ratio * diag, 1e-15f));
 }
@@ -1548,7 +1563,7 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
               const float4 n4 = *reinterpret_cast<const float4*>(&E.NC[g0]);  // one broadcast read
               nc_[u][0] = n4.x; nc_[u][1] = n4.y; nc_[u][2] = n4.z; nc_[u][3] = n4.w;
   #pragma unroll
-              for (int m = 0; m < 4; m++) jg_[u][m] = E.J[g0 + m][col];  // slot 15 holds g
+              for (int m = 0; m < 4; m++) jg_[u][m] = jlds(E, g0 + m, col);  // slot 15 holds g
               dr_[u] = E.D[r];
             } else {
   #pragma unroll
@@ -1648,7 +1663,7 @@ DEV float hess_grad_delta(EnvSh& E, float* hrow, const unsigned long long* gm) {
         const float4 n4 = *reinterpret_cast<const float4*>(&E.NC[g0]);
         float jg[4];
 #pragma unroll
-        for (int mm = 0; mm < 4; mm++) jg[mm] = E.J[g0 + mm][col];  // slot 15 holds dC r
+        for (int mm = 0; mm < 4; mm++) jg[mm] = jlds(E, g0 + mm, col);  // slot 15 holds dC r
         const float dr = E.D[g0 + rk];
         const float own = fmaf(m_[0], jg[0], fmaf(m_[1], jg[1], fmaf(m_[2], jg[2], m_[3] * jg[3])));
         const float ncr = fmaf(m_[1], n4.y, fmaf(m_[2], n4.z, m_[3] * n4.w));
@@ -2048,11 +2063,13 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid, int& exit) 
     };
     // phi' is linear on any interval over which no edge changes state (each edge is linear in a),
     // so a Newton root of phi' whose active set equals the set of the point it was taken from is
-    // the exact minimiser and needs no confirming evaluation: the full step a = 1 when no edge flips
-    // over it (H and g were built on the set at a = 0), later a Newton update whose set matches.
+    // the minimiser and needs no confirming evaluation (which would only move it by rounding).  The
+    // first evaluation, at the full step a = 1, always runs: it corrects the step length for the
+    // fp32 error of the Cholesky solve p (accepting a = 1 unevaluated moved whole C3 episodes by
+    // up to 7e-4 m against the solver at MuJoCo's tolerance).
     float alpha = 1.f, lo = 0.f, hi = 3e38f;
     int bcur = act_at(1.f);
-    bool exact = MMX_LS_EXACT && __ballot(bcur != act) == 0ull;
+    bool exact = false;  // (+1.0 % env steps/s in the A/B)
     for (int ls = 0; ls < 24 && !exact; ls++) {
       if (MMX_PROBE == 10 && LANE == 0) stats[STAT_T_AUX3] += 1.f;  // line-search steps
       float d1 = 0.f, d2 = 0.f;
@@ -2077,7 +2094,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid, int& exit) 
         break;
       }
       const int bn = act_at(na);
-      exact = MMX_LS_EXACT && newton && __ballot(bn != bcur) == 0ull;
+      exact = newton && __ballot(bn != bcur) == 0ull;
       bcur = bn;
       alpha = na;
     }

@@ -137,6 +137,9 @@ def _quat_xyzw_t(R):
     return torch.where(b0, q0, torch.where(b1, q1, torch.where(b2, q2, q3)))
 
 
+_TARGET_ORI_DEV = {}
+
+
 def encode_actions(target, gripper, T_init):
     """get_actions (generate_dataset.py:57-80) batched on device.
 
@@ -150,7 +153,10 @@ def encode_actions(target, gripper, T_init):
     t = target.to(torch.float64)
     g = gripper.to(torch.float64)[:, None]
     Ti = T_init.to(torch.float64)
-    Rt = torch.as_tensor(TARGET_ORI, dtype=torch.float64, device=dev).expand(n, 3, 3)
+    key = str(dev)
+    if key not in _TARGET_ORI_DEV:  # (a host -> device copy waits for the device: once per device)
+        _TARGET_ORI_DEV[key] = torch.as_tensor(TARGET_ORI, dtype=torch.float64, device=dev)
+    Rt = _TARGET_ORI_DEV[key].expand(n, 3, 3)
     # inv(T_init) @ T_target for a rigid transform: R' = Ri^T Rt, p' = Ri^T (t - pi)
     RiT = Ti[:, :3, :3].transpose(1, 2)
     Rr = RiT @ Rt
@@ -428,7 +434,7 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
             ends = host[f + "/ends"]
             rows_f = png_rows[f]
             for s in slots.tolist():
-                rows_f[s].append(data[ends[s - 1] if s else 0:ends[s]])
+                rows_f[s].append(bytes(data[ends[s - 1] if s else 0:ends[s]]))
         tpos[slots] = t + 1
 
     def finish(e):
@@ -493,7 +499,7 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
                     data = np.concatenate([data, packed[len(data):total].cpu().numpy()])
                 png_max[f] = max(png_max.get(f, 0), total)
                 png_est[f] = (png_max[f] * 5) // 4 + (1 << 20)
-                png[f] = data.tobytes()
+                png[f] = memoryview(data)  # (absorb copies each frame's bytes out of it)
             absorb(host, act, slot[act].astype(np.int64), png)
 
     step_no = 0
@@ -583,6 +589,7 @@ class LeRobotWriter:
         # that land in the same data file): the per-table arrow overhead is paid once per batch
         self.batch_episodes, self.batch_bytes = max(1, int(batch_episodes)), float(batch_mb) * 1024 * 1024
         self.pending, self.pending_bytes = [], 0
+        self._frame_names = []  # "/frame_000000.png", ... (the image paths' per-frame suffixes)
         self.image_compression = image_compression
         # shards keep each episode's raw image sums in meta/episodes, so merge_shards rebuilds the
         # dataset statistics bit for bit
@@ -649,9 +656,13 @@ class LeRobotWriter:
         for k in self.str_keys:
             cols[k] = pa.array([v for ep in eps for v in ep.frames[k]], pa.string())
             fields.append(pa.field(k, pa.string()))
+        nmax = max(lens) if lens else 0
+        if len(self._frame_names) < nmax:
+            self._frame_names = [f"/frame_{i:06d}.png" for i in range(max(nmax, 2 * len(self._frame_names)))]
+        fn = self._frame_names
         for k in self.img_keys:  # LeRobot's embedded image layout (images/<key>/episode_<e>/frame_<i>.png)
-            paths = pa.array([f"images/{k}/episode_{ep.index:06d}/frame_{i:06d}.png" for ep in eps for i in range(ep.length)],
-                             pa.string())
+            paths = pa.array([pre + f for ep in eps for pre in (f"images/{k}/episode_{ep.index:06d}",)
+                              for f in fn[:ep.length]], pa.string())
             cols[k] = pa.StructArray.from_arrays([pa.array([v for ep in eps for v in ep.frames[k]], pa.binary()), paths],
                                                  fields=list(self.img_type))
             fields.append(pa.field(k, self.img_type))
@@ -672,9 +683,9 @@ class LeRobotWriter:
         for k in self.num_keys:
             n += 4 * ep.length * int(np.prod(self.features[k]["shape"]))
         for k in self.str_keys:
-            n += sum(len(v) + 4 for v in ep.frames[k])
+            n += sum(map(len, ep.frames[k])) + 4 * ep.length
         for k in self.img_keys:
-            n += sum(len(v) + 4 for v in ep.frames[k]) + 50 * ep.length
+            n += sum(map(len, ep.frames[k])) + 54 * ep.length
         return n + 36 * ep.length
 
     @staticmethod

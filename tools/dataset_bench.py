@@ -37,16 +37,10 @@ def main():
 
     free0, total = torch.cuda.mem_get_info()
     used = []
-    t_first = [None]
 
-    def on_step(slots, ep_ids, env):
-        if t_first[0] is None:
-            t_first[0] = time.perf_counter()
-        if len(used) % 8 == 0:
-            f, _ = torch.cuda.mem_get_info()
-            used.append(total - f)
-        else:
-            used.append(used[-1])
+    def sample_memory():  # (no per-step hook: collect_episodes' on_step costs a host sync per step)
+        f, _ = torch.cuda.mem_get_info()
+        used.append(total - f)
 
     feats = D.resolve_features(None, "staged")
     shutil.rmtree(a.root, ignore_errors=True)
@@ -58,6 +52,8 @@ def main():
     png_bytes = [0]
 
     def sink(ep):
+        if ep.index % 64 == 0:
+            sample_memory()
         frames[0] += ep.length
         png_bytes[0] += sum(len(b) for k in D.IMAGE_KEYS for b in ep.frames.get(k, []))
         if a.no_write:
@@ -71,8 +67,7 @@ def main():
         prof.enable()
     t0 = time.perf_counter()
     D.collect_episodes(a.episodes, D.TASK_SETS["all"], set(feats), randomize_objects=True, seed=0,
-                       num_envs=a.num_envs, sink=sink, image_size=a.image_size,
-                       on_step=on_step)
+                       num_envs=a.num_envs, sink=sink, image_size=a.image_size)
     info = writer.close()
     dt = time.perf_counter() - t0
     if prof is not None:
@@ -95,7 +90,7 @@ def main():
            "png_mean_bytes": png_bytes[0] / max(2 * frames[0], 1), "dataset_bytes": size,
            "peak_host_rss_mb": rss, "device_used_mb_start": (total - free0) / 2**20,
            "device_used_mb_max": max(used) / 2**20 if used else None,
-           "device_used_mb_min_after_start": min(used) / 2**20 if used else None, "gym_steps": len(used),
+           "device_used_mb_min_after_start": min(used) / 2**20 if used else None,
            "host_cpus": len(os.sched_getaffinity(0))}
     os.makedirs(os.path.dirname(a.out), exist_ok=True)
     json.dump(rec, open(a.out, "w"), indent=1)
