@@ -132,7 +132,9 @@ static __shared__ EnvSh g_E;
 #define COL_CAND 944  // [COL_LIST] candidate pairs after the sphere test, then grouped by class
 #define COL_LIST 784
 #define COL_WORK (COL_CAND + COL_LIST)  // narrowphase work space: box-box polygons and (beside
+#ifndef COL_POLY
 #define COL_POLY 48                     // them) the EPA polytope, then the contact sort
+#endif
 // lanes that clip box-box polygons at a time (their polygons fill the rest of the LDS rows)
 #define COL_PLANES ((MMX_LDSEFC * 16 - COL_WORK) / COL_POLY < 32 ? (MMX_LDSEFC * 16 - COL_WORK) / COL_POLY : 32)
 #define COL_EPA COL_WORK
@@ -1480,6 +1482,11 @@ DEV void cost2_wave(const EnvSh& E, const float* xa, const float* xb, const floa
 // dof lanes into their Hessian row (static columns) and gradient.  Returns, in lane j < 27,
 // row j of H = M + J'WJ in hrow[0..27) and g_j = (M (x - xs) + J'W r)_j.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+// staging tile row stride: 17, so the dof lanes' reads of different tile rows (tile_gather) fall on
+// different banks (a 16-float stride put rows sd and sd + 2 on one bank: up to 5-way)
+#ifndef GST
+#define GST 16
+#endif
 // groups (MFMA steps) per trip, their loads issued together (3 or 4: -1.3 / -0.7 % in the r03 A/B)
 #define MMX_HESS_U 2
 // gather one row type's staged 16 x 16 tile into the dof lanes' Hessian rows: dof lane d reads row
@@ -1490,7 +1497,7 @@ DEV void tile_gather(const float* G, int t, int bd, int od, float* hrow, float& 
   const int n0 = blk_size(b0);
   const int sd = bd == b0 ? od : (bd == b1 ? n0 + od : -1);
   if (sd >= 0) {
-    const float* Gr = G + 16 * sd;
+    const float* Gr = G + GST * sd;
 #pragma unroll
     for (int B = 0; B < 4; B++) {
       const int nb = B == 0 ? 9 : 6, dB = B == 0 ? 0 : 9 + 6 * (B - 1);
@@ -1508,7 +1515,7 @@ DEV void tile_gather(const float* G, int t, int bd, int od, float* hrow, float& 
 // row types staged per barrier round (E.con holds up to three 16 x 16 tiles; 3 measured -1.3 % in the
 // r03 A/B: the unrolled rounds grow the substep's register save area)
 #define HESS_TILES 1
-static_assert(HESS_TILES * 256 <= MMX_MAXCON * CON_F, "Hessian staging tiles exceed E.con");
+static_assert(HESS_TILES * 16 * GST <= MMX_MAXCON * CON_F, "Hessian staging tiles exceed E.con");
 DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
   float* stats = E.stats;
   CLK_DECL;
@@ -1533,7 +1540,7 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
     SYNC();
 #pragma unroll
     for (int j = 0; j < HESS_TILES; j++)
-      if (j < nst) tile_gather(G + 256 * j, (tyslots >> (4 * j)) & 15, bd, od, hrow, gacc);
+      if (j < nst) tile_gather(G + 16 * GST * j, (tyslots >> (4 * j)) & 15, bd, od, hrow, gacc);
     SYNC();
     nst = 0;
     tyslots = 0;
@@ -1607,7 +1614,7 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
       PROBE(6, stats, STAT_T_AUX0);
       // stage: lane l holds G[4 (l >> 4) + q][l & 15]
 #pragma unroll
-      for (int q = 0; q < 4; q++) G[256 * nst + 16 * (4 * rk + q) + col] = acc0[q] + acc1[q];
+      for (int q = 0; q < 4; q++) G[16 * GST * nst + GST * (4 * rk + q) + col] = acc0[q] + acc1[q];
       tyslots |= t << (4 * nst);
       if (++nst == HESS_TILES) flush();
     }
@@ -1641,7 +1648,7 @@ DEV float hess_grad_delta(EnvSh& E, float* hrow, const unsigned long long* gm) {
     SYNC();
 #pragma unroll
     for (int j = 0; j < HESS_TILES; j++)
-      if (j < nst) tile_gather(G + 256 * j, (tyslots >> (4 * j)) & 15, bd, od, hrow, gacc);
+      if (j < nst) tile_gather(G + 16 * GST * j, (tyslots >> (4 * j)) & 15, bd, od, hrow, gacc);
     SYNC();
     nst = 0;
     tyslots = 0;
@@ -1676,7 +1683,7 @@ DEV float hess_grad_delta(EnvSh& E, float* hrow, const unsigned long long* gm) {
     if (!any) continue;
     // stage into the round's next tile; a full round (or the last type) is gathered in type order
 #pragma unroll
-    for (int q = 0; q < 4; q++) G[256 * nst + 16 * (4 * rk + q) + col] = acc[q];
+    for (int q = 0; q < 4; q++) G[16 * GST * nst + GST * (4 * rk + q) + col] = acc[q];
     tyslots |= t << (4 * nst);
     if (++nst == HESS_TILES) flush();
   }
