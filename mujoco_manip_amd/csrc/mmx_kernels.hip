@@ -132,9 +132,8 @@ static __shared__ EnvSh g_E;
 #define COL_CAND 944  // [COL_LIST] candidate pairs after the sphere test, then grouped by class
 #define COL_LIST 784
 #define COL_WORK (COL_CAND + COL_LIST)  // narrowphase work space: box-box polygons and (beside
-#ifndef COL_POLY
-#define COL_POLY 48                     // them) the EPA polytope, then the contact sort
-#endif
+#define COL_POLY 49                     // them) the EPA polytope, then the contact sort (49: the quads'
+                                        // polygons start on different banks; 48 put quads 2 apart on one)
 // lanes that clip box-box polygons at a time (their polygons fill the rest of the LDS rows)
 #define COL_PLANES ((MMX_LDSEFC * 16 - COL_WORK) / COL_POLY < 32 ? (MMX_LDSEFC * 16 - COL_WORK) / COL_POLY : 32)
 #define COL_EPA COL_WORK
@@ -1483,10 +1482,9 @@ DEV void cost2_wave(const EnvSh& E, const float* xa, const float* xb, const floa
 // row j of H = M + J'WJ in hrow[0..27) and g_j = (M (x - xs) + J'W r)_j.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 // staging tile row stride: 17, so the dof lanes' reads of different tile rows (tile_gather) fall on
-// different banks (a 16-float stride put rows sd and sd + 2 on one bank: up to 5-way)
-#ifndef GST
-#define GST 16
-#endif
+// different banks (a 16-float stride put rows sd and sd + 2 on one bank: up to 5-way; with the
+// polygon stride below, LDS bank conflicts 0.31 -> 0.12 per LDS-active cycle, +0.2 % in the A/B)
+#define GST 17
 // groups (MFMA steps) per trip, their loads issued together (3 or 4: -1.3 / -0.7 % in the r03 A/B)
 #define MMX_HESS_U 2
 // gather one row type's staged 16 x 16 tile into the dof lanes' Hessian rows: dof lane d reads row
