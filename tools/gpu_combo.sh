@@ -2,7 +2,7 @@ set -o pipefail
 # one GPU call: interleaved A/B of the product library against $LIBS (tools/ab.sh, PMC=1 adds one SQ
 # counter pass per library), the GPU suite (SUITE=1, no -x: every failure listed; a failing test is
 # re-run with the first A/B library), tests $ALT_K (pytest -k) with each of $LIBS, and the f2
-# host-path profile (DS=1, tools/gpu_ds_profile.sh)
+# host-path profile (DS=1, tools/gpu_ds_profile.sh); RTIME=1: render-only time per library
 cd $GRAFT_REPO_ROOT; mkdir -p gpurun_out
 md5sum mujoco_manip_amd/libmmx.so $LIBS
 if [ -n "$LIBS" ]; then TESTS=0 ROUNDS=${ROUNDS:-3} STEPS=${STEPS:-512} bash tools/ab.sh || exit 1; fi
@@ -12,6 +12,12 @@ if [ -n "$ALT_K" ]; then
     MMX_LIB_PATH=$lib timeout -k 10 600 python -u -m pytest tests -m gpu -k "$ALT_K" -q --timeout 300 \
       --timeout-method thread > gpurun_out/alt_$(basename $lib .so).log 2>&1
     r=$?; echo "$lib [$ALT_K]: $(tail -1 gpurun_out/alt_$(basename $lib .so).log)"; [ $r -gt 1 ] && exit $r
+  done
+fi
+if [ "${RTIME:-0}" = 1 ]; then  # render-only time (tools/render_time.py) per library
+  for lib in mujoco_manip_amd/libmmx.so $LIBS; do
+    MMX_LIB_PATH=$lib timeout -k 10 300 python -u tools/render_time.py > gpurun_out/rtime_$(basename $lib .so).log 2>&1 || exit 1
+    echo "$lib render: $(grep -h '^{' gpurun_out/rtime_$(basename $lib .so).log | cut -c1-220)"
   done
 fi
 if [ "${SUITE:-1}" = 1 ]; then
