@@ -23,6 +23,7 @@ extern "C" hipError_t mmx_launch_expert(const MMXState* S, int n, float* action,
 extern "C" hipError_t mmx_launch_physics(const MMXState* S, int n, int with_ik, hipStream_t st);
 extern "C" hipError_t mmx_launch_forward(const MMXState* S, hipStream_t st);
 extern "C" hipError_t mmx_launch_render(const MMXState* S, int base, int count, hipStream_t st);
+extern "C" hipError_t mmx_launch_render_bg(const MMXState* S, hipStream_t st);
 extern "C" hipError_t mmx_launch_render_masked(const MMXState* S, int base, int count, const unsigned char* mask,
                                                hipStream_t st);
 extern "C" hipError_t mmx_launch_queue(const MMXState* S, int* slot, int* next, int n_ep, const unsigned long long* rng,
@@ -297,6 +298,8 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
     S.rpose = dalloc<float>(sim, 14 * 12 * n);
     S.images = dalloc<unsigned char>(sim, 2 * px * 3 * n);
     S.seg = dalloc<unsigned char>(sim, 2 * px * n);
+    const size_t sg = static_cast<size_t>((cfg->image_size + 15) & ~15);
+    S.bg_overhead = dalloc<unsigned int>(sim, sg * sg);
   }
   for (void* p : sim->allocs)
     if (!p) {
@@ -336,6 +339,10 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
     }
   sim->nlanes = lanes;
   *out = sim;
+  if (S.bg_overhead) {  // the fixed overhead camera's background, once
+    const int rc = hip_check(sim, mmx_launch_render_bg(&S, sim->stream), "mmx_create background");
+    if (rc) return rc;
+  }
   return hip_check(sim, hipDeviceSynchronize(), "mmx_create");
 }
 

@@ -194,33 +194,44 @@ DEV uint32_t rend_pack(float r, float g, float b, uint32_t sid) {
 // floor's normal is world z, so its headlight / directional terms are constants of the camera and
 // the point light's cosine is 1.5 / |(0.5, 0.5, 1.5) - p|), the sky gradient elsewhere; RGB u8
 // (3 dwords) and segment ids (1 dword)
-DEV void shade4(const uint32_t* keys, int px0, int py, float half, float f, const M3& cR, const V3& cx,
-                float floor_light0, const uint32_t* tinfo, const float* mrgb, uint32_t* rgb_out, uint32_t* seg_out,
-                int nvalid) {
-  uint32_t pix[4];
-  // world ray of the first pixel; the next ones step by the camera's x axis / f
+// background of a pixel no triangle covers, from its world ray dw: the floor's checker where the
+// ray meets the floor (the floor's normal is world z, so its headlight / directional terms are
+// constants of the camera and the point light's cosine is 1.5 / |(0.5, 0.5, 1.5) - p|), the sky
+// gradient elsewhere
+DEV uint32_t shade_bg(const V3& dw, const V3& cx, float floor_light0, const float* mrgb) {
+  const float s0 = -cx.z / dw.z;  // ray parameter at the floor plane z = 0
+  const float fx = cx.x + s0 * dw.x, fy = cx.y + s0 * dw.y;
+  if (dw.z < 0.f && fabsf(fx) <= MMR_FLOOR_HALF && fabsf(fy) <= MMR_FLOOR_HALF) {
+    const float* mt = mrgb + 8 * MMR_FLOOR_MAT;  // checker (0.1 m squares) under the face lights
+    const float ddx = 0.5f - fx, ddy = 0.5f - fy;
+    const float light = fminf(floor_light0 + 0.6f * rsqrtf(fmaf(ddx, ddx, fmaf(ddy, ddy, 2.25f))), 3.99f);
+    const bool alt = ((int)floorf(fx / mt[6]) + (int)floorf(fy / mt[6])) & 1;
+    const float* c = alt ? mt + 3 : mt;
+    return rend_pack(fminf(c[0] * light, 1.f), fminf(c[1] * light, 1.f), fminf(c[2] * light, 1.f), (uint32_t)mt[7]);
+  }
+  const float sky = 0.5f * (dw.z * rsqrtf(dot(dw, dw)) + 1.f);  // skybox gradient (rgb1 top -> rgb2 bottom, scene.xml:17-18)
+  return rend_pack(0.3f * sky, 0.5f * sky, 0.7f * sky, 0u);
+}
+// the world rays of 4 horizontally adjacent pixels (px0 .. px0 + 3, py): the first one's, then steps
+// by the camera's x axis / f (one order for every caller: the background table is bit-identical to
+// the per-pixel shading)
+DEV void rays4(int px0, int py, float half, float f, const M3& cR, V3* dw4) {
   const float rf = 1.f / f;
   const V3 dx = col(cR, 0) * rf;
   V3 dw = mul(cR, V3{(px0 + 0.5f - half) * rf, -(py + 0.5f - half) * rf, -1.f});
-  for (int u = 0; u < 4; u++, dw = dw + dx) {
-    const uint32_t key = keys[u];
-    if (key != 0u) {
-      pix[u] = tinfo[key & 4095];
-      continue;
-    }
-    const float s0 = -cx.z / dw.z;  // ray parameter at the floor plane z = 0
-    const float fx = cx.x + s0 * dw.x, fy = cx.y + s0 * dw.y;
-    if (dw.z < 0.f && fabsf(fx) <= MMR_FLOOR_HALF && fabsf(fy) <= MMR_FLOOR_HALF) {
-      const float* mt = mrgb + 8 * MMR_FLOOR_MAT;  // checker (0.1 m squares) under the face lights
-      const float ddx = 0.5f - fx, ddy = 0.5f - fy;
-      const float light = fminf(floor_light0 + 0.6f * rsqrtf(fmaf(ddx, ddx, fmaf(ddy, ddy, 2.25f))), 3.99f);
-      const bool alt = ((int)floorf(fx / mt[6]) + (int)floorf(fy / mt[6])) & 1;
-      const float* c = alt ? mt + 3 : mt;
-      pix[u] = rend_pack(fminf(c[0] * light, 1.f), fminf(c[1] * light, 1.f), fminf(c[2] * light, 1.f), (uint32_t)mt[7]);
-    } else {  // skybox gradient (rgb1 top -> rgb2 bottom, scene.xml:17-18)
-      const float sky = 0.5f * (dw.z * rsqrtf(dot(dw, dw)) + 1.f);
-      pix[u] = rend_pack(0.3f * sky, 0.5f * sky, 0.7f * sky, 0u);
-    }
+  for (int u = 0; u < 4; u++, dw = dw + dx) dw4[u] = dw;
+}
+// bg: the camera's precomputed background row (fixed cameras), or null (computed per pixel)
+DEV void shade4(const uint32_t* keys, int px0, int py, float half, float f, const M3& cR, const V3& cx,
+                float floor_light0, const uint32_t* tinfo, const float* mrgb, const uint32_t* bg, uint32_t* rgb_out,
+                uint32_t* seg_out, int nvalid) {
+  uint32_t pix[4];
+  if (bg) {
+    for (int u = 0; u < 4; u++) pix[u] = keys[u] != 0u ? tinfo[keys[u] & 4095] : bg[px0 + u];
+  } else {
+    V3 dw4[4];
+    rays4(px0, py, half, f, cR, dw4);
+    for (int u = 0; u < 4; u++) pix[u] = keys[u] != 0u ? tinfo[keys[u] & 4095] : shade_bg(dw4[u], cx, floor_light0, mrgb);
   }
   const uint32_t rgbw[3] = {(pix[0] & 0xFFFFFFu) | (pix[1] << 24), ((pix[1] >> 8) & 0xFFFFu) | (pix[2] << 16),
                             ((pix[2] >> 16) & 0xFFu) | (pix[3] << 8)};
@@ -364,6 +375,8 @@ mmx_render_kernel(MMXState S, int env_base, const unsigned char* mask) {  // two
     }
   }
   const int tcols = Sg >> 4;
+  // the overhead camera is fixed: its background (floor / sky per pixel) is one table for every env
+  const uint32_t* bgtab = ci == 0 ? S.bg_overhead : nullptr;
   const int lane = tid & 63, lx = 4 * (lane & 3), ly = lane >> 2;
   unsigned char* img = S.images + ((size_t)i * 2 + ci) * Sz * Sz * 3;
   unsigned char* seg = S.seg + ((size_t)i * 2 + ci) * Sz * Sz;
@@ -514,7 +527,7 @@ mmx_render_kernel(MMXState S, int env_base, const unsigned char* mask) {  // two
       const int nvalid = whole ? 4 : min(4, Sz - (tx[j] + lx));
       if (nvalid <= 0) continue;
       const size_t p0 = (size_t)py * Sz + tx[j] + lx;  // image pixel of the lane's first pixel
-      shade4(best[j], tx[j] + lx, py, half, f, cR, cx, floor_light0, tinfo, mrgb,
+      shade4(best[j], tx[j] + lx, py, half, f, cR, cx, floor_light0, tinfo, mrgb, bgtab ? bgtab + (size_t)py * Sg : nullptr,
              reinterpret_cast<uint32_t*>(img + 3 * p0), reinterpret_cast<uint32_t*>(seg + p0), nvalid);
     }
   }
@@ -532,6 +545,37 @@ extern "C" hipError_t mmx_render_clock(unsigned long long* out, int reset) {
   return e;
 }
 #endif
+
+// The fixed overhead camera's background: for every pixel of the Sg x Sg raster grid, the packed
+// colour + segment id shade4 gives an uncovered pixel (same rays, same arithmetic), computed once per
+// sim; the render kernel then reads it instead of intersecting the floor per pixel and env.
+extern "C" __global__ void __launch_bounds__(256) mmx_render_bg_kernel(MMXState S, uint32_t* bg) {
+  const int Sz = S.image_size, Sg = (Sz + 15) & ~15;
+  const int g = blockIdx.x * 256 + threadIdx.x;  // 4-pixel group
+  if (g >= Sg * Sg / 4) return;
+  const int py = g / (Sg / 4), px0 = 4 * (g % (Sg / 4));
+  const int c = MMX_CAM_OVERHEAD;
+  const M3 cR = qmat(Q4{MMX_cam_quat[4 * c], MMX_cam_quat[4 * c + 1], MMX_cam_quat[4 * c + 2], MMX_cam_quat[4 * c + 3]});
+  const V3 cx = V3{MMX_cam_pos[3 * c], MMX_cam_pos[3 * c + 1], MMX_cam_pos[3 * c + 2]};
+  const float half = 0.5f * Sz;
+  const float f = half / tanf(MMX_cam_fovy[c] * (3.14159265358979f / 360.f));
+  const V3 l_top = mulT(cR, V3{0.f, 0.f, 1.f});
+  const float floor_light0 = 0.3f + 0.6f * fmaxf(l_top.z, 0.f) + 0.8f;
+  float mrgb[8 * MMR_NMAT];
+  for (int k = 0; k < 8 * MMR_NMAT; k++) {
+    const int m = k >> 3, j = k & 7;
+    mrgb[k] = j < 6 ? MMR_mat_rgb[6 * m + j] : (j == 6 ? MMR_mat_checker[m] : (float)MMR_mat_seg[m]);
+  }
+  V3 dw4[4];
+  rays4(px0, py, half, f, cR, dw4);
+  for (int u = 0; u < 4; u++) bg[(size_t)py * Sg + px0 + u] = shade_bg(dw4[u], cx, floor_light0, mrgb);
+}
+extern "C" hipError_t mmx_launch_render_bg(const MMXState* S, hipStream_t st) {
+  if (S->image_size <= 0 || !S->bg_overhead) return hipSuccess;
+  const int Sg = (S->image_size + 15) & ~15;
+  hipLaunchKernelGGL(mmx_render_bg_kernel, dim3((Sg * Sg / 4 + 255) / 256), dim3(256), 0, st, *S, S->bg_overhead);
+  return hipGetLastError();
+}
 
 static_assert(sizeof(float4) * MMR_NVERT + sizeof(float) * 19 * 12 + sizeof(uint32_t) * kZbWords +
                   sizeof(unsigned short) * kBPW * kMaxBig + kNbig * sizeof(int) + 12 * sizeof(float) +

@@ -113,6 +113,7 @@ struct MMXState {
   float* rpose;            // [N][14][12] body poses (R row-major, p) of the last position stage
   unsigned char* images;   // [N][2][S][S][3] overhead, wrist RGB
   unsigned char* seg;      // [N][2][S][S] segment ids (0 sky, 1 floor, 2 table, 3-5 bins, 6-8 cubes, 9 robot)
+  unsigned int* bg_overhead;  // [Sg][Sg] the fixed overhead camera's background (packed RGB | seg << 24)
 };
 
 #endif

@@ -353,7 +353,8 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
     encoded to PNG files on the device (mmx_png_encode; LeRobot embeds image features as PNG,
     generate_dataset.py:250-260) with their per-channel statistics, so only the compressed files
     cross PCIe and the host does no image work.  Device memory is O(envs): no frame stays on the
-    device after its copy.  A finished episode (FSM DONE) is handed to `sink(episode)` in
+    device after its copy; the packed PNG buffers of the steps in flight (ring depth 4 + 1, room for
+    n bounds each) dominate it: 13 GB at 128^2 and 32 GB at 224^2 for 8192 envs.  A finished episode (FSM DONE) is handed to `sink(episode)` in
     episode-index order, so the host holds only the episodes in flight; without a sink the episodes
     are returned as a list.  on_step(slots, episode_ids, env), when given, sees the env before each
     batched step (a diagnostic hook: it costs a host synchronisation per step).  Returns (episodes or
