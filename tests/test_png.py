@@ -137,3 +137,20 @@ def test_png_encode_from_another_stream(sim):
         got = packed.cpu().numpy()  # ordered on the caller's stream
     np.testing.assert_array_equal(offs, woffs)
     np.testing.assert_array_equal(got, want)
+
+
+def test_png_encode_device_matches_host_path(sim):
+    """png_encode_device (the dataset loop's sync-free form: files packed on the device, the end
+    offsets left on the device, room for n bounds) gives the same files as png_encode, also for a
+    strided batch (one camera of [n, 2, H, W, 3] images)."""
+    rng = np.random.default_rng(9)
+    host = rng.integers(0, 256, (5, 2, 40, 56, 3), dtype=np.uint8)
+    host[:, :, 20:] = host[:, :, :20]  # repeated rows: matches at the row-above distance
+    dev = torch.as_tensor(host).cuda()
+    for cam in range(2):
+        want, woffs = sim.png_encode(dev[:, cam].contiguous())
+        packed, ends = sim.png_encode_device(dev[:, cam])
+        ends = ends.cpu().numpy()
+        assert packed.numel() == 5 * sim.L.mmx_png_bound(56, 40)
+        np.testing.assert_array_equal(np.concatenate([[0], ends]), woffs)
+        np.testing.assert_array_equal(packed[:int(ends[-1])].cpu().numpy(), want.cpu().numpy())
