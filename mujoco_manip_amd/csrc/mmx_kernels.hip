@@ -121,6 +121,8 @@ struct EnvSh {
 // The workgroup's env lives in one file-scope LDS object: the non-inlined substep function below
 // reaches it by symbol (LDS address space), not through a generic pointer.
 static __shared__ EnvSh g_E;
+// eight workgroups (envs) per CU share its 160 KiB of LDS: the occupancy the kernel is tuned for
+static_assert(sizeof(EnvSh) <= 160 * 1024 / 8, "EnvSh no longer fits 8 envs per CU");
 
 // E.J is the phases' scratch outside the constraint build + Newton solve (rows are rebuilt every
 // substep): the collision layout below, the position stage's chain scan, the IK system, the RNE /
