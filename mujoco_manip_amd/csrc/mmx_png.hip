@@ -92,6 +92,21 @@ struct BitSink {  // LSB-first bit writer into a row-private word stream
 // row r's scanline byte t (t = 0: filter byte 0, else RGB byte t - 1)
 __device__ inline int scan_byte(const uint8_t* row, int t) { return t == 0 ? 0 : row[t - 1]; }
 
+// length of the common prefix of a[0, lim) and b[0, lim): 4 bytes per step (one compare of two
+// 4-byte loads, independent of each other), so a long match is a quarter of the dependent load
+// round trips of a byte-at-a-time walk; reads stay inside [0, lim)
+__device__ inline int run_len(const uint8_t* a, const uint8_t* b, int lim) {
+  int m = 0;
+  for (; m + 4 <= lim; m += 4) {
+    uint32_t x, y;
+    __builtin_memcpy(&x, a + m, 4);
+    __builtin_memcpy(&y, b + m, 4);
+    if (x != y) return m + (__builtin_ctz(x ^ y) >> 3);
+  }
+  while (m < lim && a[m] == b[m]) m++;
+  return m;
+}
+
 // greedy parse of one scanline; EMIT = false counts bits, true writes them
 template <bool EMIT>
 __device__ int64_t parse_row(const uint8_t* row, const uint8_t* above, int L1, BitSink* bs) {
@@ -102,10 +117,12 @@ __device__ int64_t parse_row(const uint8_t* row, const uint8_t* above, int L1, B
     const int lim = min(kMaxMatch, L1 - t);
     int m2 = 0, m1 = 0;
     if (above) {  // the byte above (filter bytes are both 0)
-      while (m2 < lim && scan_byte(row, t + m2) == scan_byte(above, t + m2)) m2++;
+      m2 = t == 0 ? 1 + run_len(row, above, lim - 1) : run_len(row + t - 1, above + t - 1, lim);
     }
-    if (t >= 3) {  // the same channel one pixel back (inside the row)
-      while (m1 < lim && scan_byte(row, t + m1) == scan_byte(row, t + m1 - 3)) m1++;
+    if (t >= 4) {  // the same channel one pixel back (inside the row)
+      m1 = run_len(row + t - 1, row + t - 4, lim);
+    } else if (t == 3) {  // (its first byte is compared with the filter byte 0)
+      m1 = row[2] == 0 ? 1 + run_len(row + 3, row, lim - 1) : 0;
     }
     const bool near = m1 >= m2;  // ties: the 3-byte distance (no extra bits)
     const int m = near ? m1 : m2;
@@ -149,11 +166,14 @@ __device__ uint32_t crc_table(int k) {  // CRC-32 (IEEE, reflected) table entry,
   return c;
 }
 
-extern "C" __global__ void __launch_bounds__(PNG_WG)
-mmx_png_kernel(const uint8_t* rgb, int64_t img_stride, int W, int H, uint8_t* out, int64_t out_stride,
-               int32_t* sizes, uint32_t* scratch) {
-  __shared__ int64_t s_off[1025];  // bit offset of each row in the block (H <= 1024)
-  __shared__ uint64_t s_a1[PNG_WG], s_a2[PNG_WG];
+// WG lanes per image: one row per lane, so an image of at most 128 rows runs on 128 lanes (no idle
+// waves holding the CU's wave slots during the row parses, which are serial per lane: the encoder's
+// speed is the number of rows in flight per CU)
+template <int WG>
+__device__ void png_encode(const uint8_t* rgb, int64_t img_stride, int W, int H, uint8_t* out, int64_t out_stride,
+                           int32_t* sizes, uint32_t* scratch) {
+  __shared__ int32_t s_off[1025];  // bit offset of each row in the block (H <= 1024, W <= 10922: < 2^29)
+  __shared__ uint64_t s_a1[WG], s_a2[WG];
   __shared__ uint32_t s_crc[256];
   __shared__ int64_t s_tot;
   const int img = blockIdx.x, tid = threadIdx.x;
@@ -162,13 +182,13 @@ mmx_png_kernel(const uint8_t* rgb, int64_t img_stride, int W, int H, uint8_t* ou
   const int64_t rw = png_row_words(W);
   uint32_t* scr = scratch + (int64_t)img * H * rw;
   uint8_t* o = out + (int64_t)img * out_stride;
-  s_crc[tid] = crc_table(tid);  // (PNG_WG = 256 entries)
+  for (int k = tid; k < 256; k += WG) s_crc[k] = crc_table(k);
   // pass 1: row bit counts and Adler-32 partial sums (s1: sum of bytes, s2: sum of (n - i) byte_i)
   const uint64_t n = (uint64_t)H * L1;
   uint64_t a1 = 0, a2 = 0;
-  for (int r = tid; r < H; r += PNG_WG) {
+  for (int r = tid; r < H; r += WG) {
     const uint8_t* row = im + (int64_t)r * L;
-    s_off[r + 1] = parse_row<false>(row, r ? row - L : nullptr, L1, nullptr);
+    s_off[r + 1] = (int32_t)parse_row<false>(row, r ? row - L : nullptr, L1, nullptr);
     const uint64_t i0 = (uint64_t)r * L1 + 1;  // the filter byte (0) adds nothing
     for (int k = 0; k < L; k++) {
       const uint64_t b = row[k];
@@ -183,7 +203,7 @@ mmx_png_kernel(const uint8_t* rgb, int64_t img_stride, int W, int H, uint8_t* ou
     s_off[0] = 3;
     for (int r = 0; r < H; r++) s_off[r + 1] += s_off[r];
     uint64_t A1 = 1, A2 = n;  // s2 = n (the initial 1 of s1 counted at each byte) + sum (n - i) b_i
-    for (int k = 0; k < PNG_WG; k++) {
+    for (int k = 0; k < WG; k++) {
       A1 += s_a1[k];
       A2 += s_a2[k];
     }
@@ -192,7 +212,7 @@ mmx_png_kernel(const uint8_t* rgb, int64_t img_stride, int W, int H, uint8_t* ou
   }
   __syncthreads();
   // pass 2: each row's bits into its private stream
-  for (int r = tid; r < H; r += PNG_WG) {
+  for (int r = tid; r < H; r += WG) {
     const uint8_t* row = im + (int64_t)r * L;
     BitSink bs{scr + (int64_t)r * rw, 0ull, 0, 0};
     parse_row<true>(row, r ? row - L : nullptr, L1, &bs);
@@ -208,7 +228,7 @@ mmx_png_kernel(const uint8_t* rgb, int64_t img_stride, int W, int H, uint8_t* ou
   // deflate block dword w: the header bits and the rows overlapping [32 w, 32 w + 32); written as
   // bytes into the chunked layout (zlib byte j lives at idat + zpos(j))
   const int64_t nw = (nbits + 31) / 32;
-  for (int64_t w = tid; w < nw; w += PNG_WG) {
+  for (int64_t w = tid; w < nw; w += WG) {
     const int64_t b0 = 32 * w, b1 = b0 + 32;
     uint32_t v = w == 0 ? 3u : 0u;  // BFINAL = 1, BTYPE = 01 (fixed Huffman)
     int lo = 0, hi = H;             // first row whose range ends after b0
@@ -266,13 +286,24 @@ mmx_png_kernel(const uint8_t* rgb, int64_t img_stride, int W, int H, uint8_t* ou
   }
   __threadfence();
   __syncthreads();
-  for (int64_t ch = tid; ch < nchunk; ch += PNG_WG) {  // one lane per chunk: CRC of type + data
+  for (int64_t ch = tid; ch < nchunk; ch += WG) {  // one lane per chunk: CRC of type + data
     uint8_t* hp = idat + ch * (kChunk + 12);
     const int64_t len = min((int64_t)kChunk, zlen - ch * kChunk);
     uint32_t c = 0xFFFFFFFFu;
     for (int64_t k = 4; k < 8 + len; k++) c = s_crc[(c ^ hp[k]) & 255] ^ (c >> 8);
     put_be32(hp + 8 + len, ~c);
   }
+}
+
+extern "C" __global__ void __launch_bounds__(PNG_WG)
+mmx_png_kernel(const uint8_t* rgb, int64_t img_stride, int W, int H, uint8_t* out, int64_t out_stride,
+               int32_t* sizes, uint32_t* scratch) {
+  png_encode<PNG_WG>(rgb, img_stride, W, H, out, out_stride, sizes, scratch);
+}
+extern "C" __global__ void __launch_bounds__(128)
+mmx_png_kernel_128(const uint8_t* rgb, int64_t img_stride, int W, int H, uint8_t* out, int64_t out_stride,
+                   int32_t* sizes, uint32_t* scratch) {
+  png_encode<128>(rgb, img_stride, W, H, out, out_stride, sizes, scratch);
 }
 
 // packed[offsets[i] ..] = the first sizes[i] bytes of image i's slot
@@ -291,8 +322,12 @@ extern "C" hipError_t mmx_launch_png(const uint8_t* rgb, int64_t img_stride, int
                                      int64_t out_stride, int32_t* sizes, uint32_t* scratch, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   if (W <= 0 || H <= 0 || H > 1024 || out_stride < png_bound(W, H)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(mmx_png_kernel, dim3(n), dim3(PNG_WG), 0, st, rgb, img_stride, W, H, out, out_stride, sizes,
-                     scratch);
+  if (H <= 128)
+    hipLaunchKernelGGL(mmx_png_kernel_128, dim3(n), dim3(128), 0, st, rgb, img_stride, W, H, out, out_stride, sizes,
+                       scratch);
+  else
+    hipLaunchKernelGGL(mmx_png_kernel, dim3(n), dim3(PNG_WG), 0, st, rgb, img_stride, W, H, out, out_stride, sizes,
+                       scratch);
   return hipGetLastError();
 }
 extern "C" hipError_t mmx_launch_png_pack(const uint8_t* out, int64_t out_stride, const int32_t* sizes,
