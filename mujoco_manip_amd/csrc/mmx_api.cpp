@@ -338,12 +338,16 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
       break;
     }
   sim->nlanes = lanes;
-  *out = sim;
-  if (S.bg_overhead) {  // the fixed overhead camera's background, once
-    const int rc = hip_check(sim, mmx_launch_render_bg(&S, sim->stream), "mmx_create background");
-    if (rc) return rc;
+  // the fixed overhead camera's background, once; the handle is published only when the sim is
+  // complete (on a failure every allocation is released and *out stays null)
+  int rc = S.bg_overhead ? hip_check(sim, mmx_launch_render_bg(&S, sim->stream), "mmx_create background") : 0;
+  if (!rc) rc = hip_check(sim, hipDeviceSynchronize(), "mmx_create");
+  if (rc) {
+    mmx_destroy(sim);
+    return rc;
   }
-  return hip_check(sim, hipDeviceSynchronize(), "mmx_create");
+  *out = sim;
+  return 0;
 }
 
 void mmx_destroy(mmx_sim* sim) {

@@ -328,9 +328,12 @@ DEV unsigned quad_bits(bool b) {
 // Sutherland-Hodgman clip with polygon vertices ql and ql + 4 per lane and plane (quad prefix
 // counts keep the sequential vertex order, and every vertex and intersection is computed with the
 // sequential clip's expression), contacts put with the keys and slots the sequential clip gives
-// them (the same contact list in the same order as the r02 lane-per-pair form, checked on 24,576
-// C3 states in r03: positions and depths bit-identical, normals within 1 ulp; the oracle's box_box
-// is that sequential form).  poly, tmp: 8 V3 each of the quad's LDS scratch.
+// them, i.e. the same contact list in the same order as the oracle's sequential box_box.  (r03
+// checked it bit-identical to the then lane-per-pair form on 24,576 C3 states under strict fp
+// evaluation order; the step kernel has since been compiled with -fassociative-math, so that
+// bit-for-bit claim no longer holds or is re-checked.  What is enforced now: the box-box scenes of
+// tests/test_collision_kat.py against geometry, depth 2e-6 m and the exact contact counts, and the
+// oracle parity tests' qpos / qvel tolerances.)  poly, tmp: 8 V3 each of the quad's LDS scratch.
 template <class Sink>
 DEV void box_box_quad(Sink& cs, const Geom& G1, const Geom& G2, V3 hb1, V3 hb2, V3* poly, V3* tmp) {
   CLK_DECL;

@@ -64,6 +64,11 @@ static constexpr int kBinBody[3] = {MMX_BODY_BIN_RED, MMX_BODY_BIN_GREEN, MMX_BO
 #define MMX_CAND_MARGIN 0.08f  // m: the list's inflation of the sphere / plane test (A/B: 0.04 +0.2 %, 0.08 +0.8 %, 0.15 -0.6 %)
 #endif
 #define LD 28     // padded row stride for 27-wide rows
+// Newton line search: accept a Newton root of phi' on an unchanged active set without a confirming
+// evaluation (1, the product) or always confirm it (0, the parity A/B build: tools/ab_build.py)
+#ifndef MMX_LS_SHORTCUT
+#define MMX_LS_SHORTCUT 1
+#endif
 
 // ============================================================================ per-env LDS
 struct EnvSh {
@@ -2076,7 +2081,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid, int& exit) 
     // up to 7e-4 m against the solver at MuJoCo's tolerance).
     float alpha = 1.f, lo = 0.f, hi = 3e38f;
     int bcur = act_at(1.f);
-    bool exact = false;  // (+1.0 % env steps/s in the A/B)
+    bool exact = false;  // (+1.0 % env steps/s in the A/B; MMX_LS_SHORTCUT=0: always confirm)
     for (int ls = 0; ls < 24 && !exact; ls++) {
       if (MMX_PROBE == 10 && LANE == 0) stats[STAT_T_AUX3] += 1.f;  // line-search steps
       float d1 = 0.f, d2 = 0.f;
@@ -2101,7 +2106,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid, int& exit) 
         break;
       }
       const int bn = act_at(na);
-      exact = newton && __ballot(bn != bcur) == 0ull;
+      exact = MMX_LS_SHORTCUT && newton && __ballot(bn != bcur) == 0ull;
       bcur = bn;
       alpha = na;
     }
@@ -2182,9 +2187,14 @@ DEV void integrate_wave(EnvSh& E) {
     E.ws[LANE] = E.x[LANE];  // warm start keeps the constraint solver's qacc
     const float v = E.qvel[LANE] + kDt * qa;
     E.qvel[LANE] = v;
-    // |v| or |qacc| >= 1e10, Inf or NaN (MuJoCo's mj_checkVel / mj_checkAcc bound mjMAXVAL; a bit
-    // test, exact under any fp-math flags)
-    bad = (__float_as_uint(v) & 0x7fffffffu) >= 0x501502F9u || (__float_as_uint(qa) & 0x7fffffffu) >= 0x501502F9u;
+    // |v| or |qacc| >= 1e10, Inf or NaN (MuJoCo's mj_checkVel / mj_checkAcc bound mjMAXVAL): an
+    // integer test of the bits.  The values pass through an opaque register copy first: the device
+    // code is built without NaN / Inf semantics (-ffinite-math-only), under which the compiler may
+    // treat a NaN or Inf result of the fp ops above as impossible and fold a test it can see through
+    // (ADVICE r04); behind the copy the test reads whatever bits the ALU produced.
+    unsigned vb = __float_as_uint(v), qb = __float_as_uint(qa);
+    asm volatile("" : "+v"(vb), "+v"(qb));
+    bad = (vb & 0x7fffffffu) >= 0x501502F9u || (qb & 0x7fffffffu) >= 0x501502F9u;
     if (LANE < 9) E.qpos[LANE] += kDt * v;
   }
   if (__ballot(bad) != 0ull && LANE == 0) E.flags |= SHF_NAN;

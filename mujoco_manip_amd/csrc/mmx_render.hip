@@ -153,7 +153,13 @@ DEV bool rend_setup_abc(const float4* vs, int a, int b, int c, int S, int row0, 
   if (pa.w == 0.f || pb.w == 0.f || pc.w == 0.f) return false;  // a vertex behind the near plane
   // screen y points down: a counter-clockwise (outward) face has negative signed area
   const float area = (pb.x - pa.x) * (pc.y - pa.y) - (pc.x - pa.x) * (pb.y - pa.y);
-  if (!(area < -1e-12f)) return false;
+  // area < -1e-12 as an integer test of the bits (negative finite values below -1e-12 lie strictly
+  // between the bits of -1e-12 and of -Inf): NaN / Inf areas (a diverged env's poses reach the
+  // renderer when autoreset is off) are culled whatever the fp-math flags let the compiler assume
+  // about fp comparisons; the opaque copy keeps it from reasoning about the bits
+  unsigned ab = __float_as_uint(area);
+  asm volatile("" : "+v"(ab));
+  if (!(ab > 0xAB8CBCCCu && ab < 0xFF800000u)) return false;
   const float mnx = fminf(pa.x, fminf(pb.x, pc.x)), mxx = fmaxf(pa.x, fmaxf(pb.x, pc.x));
   const float mny = fminf(pa.y, fminf(pb.y, pc.y)), mxy = fmaxf(pa.y, fmaxf(pb.y, pc.y));
   // pixel (i, j) has its centre at (i + 0.5, j + 0.5)
@@ -376,7 +382,9 @@ mmx_render_kernel(MMXState S, int env_base, const unsigned char* mask) {  // two
   }
   const int tcols = Sg >> 4;
   // the overhead camera is fixed: its background (floor / sky per pixel) is one table for every env
-  const uint32_t* bgtab = ci == 0 ? S.bg_overhead : nullptr;
+  // the per-sim background table holds a world-fixed camera's view: used only while the overhead
+  // camera is attached to the world (a body-mounted one falls back to per-pixel shading)
+  const uint32_t* bgtab = ci == 0 && MMX_cam_body[MMX_CAM_OVERHEAD] == 0 ? S.bg_overhead : nullptr;
   const int lane = tid & 63, lx = 4 * (lane & 3), ly = lane >> 2;
   unsigned char* img = S.images + ((size_t)i * 2 + ci) * Sz * Sz * 3;
   unsigned char* seg = S.seg + ((size_t)i * 2 + ci) * Sz * Sz;

@@ -702,3 +702,15 @@ int or_get_efc(or_env* e, int* type, double* pos, double* R, double* aref) {
 }
 void or_get_qacc(or_env* e, double* qacc) { memcpy(qacc, e->qacc, sizeof(e->qacc)); }
 void or_get_mass_matrix(or_env* e, double* M) { memcpy(M, e->M, sizeof(e->M)); }
+/* the smooth-force terms of the last forward (tests/test_smooth_dynamics_kat.py pins them against
+ * answers derived from the raw MJCF): qfrc_bias (RNE: Coriolis + gravity), qfrc_actuator, qfrc_passive,
+ * qacc_smooth, qfrc_constraint (NV each) and the clamped actuator forces (NU) */
+void or_get_smooth(or_env* e, double* bias, double* act, double* passive, double* qacc_smooth, double* constraint,
+                   double* act_force) {
+  memcpy(bias, e->qfrc_bias, NV * sizeof(double));
+  memcpy(act, e->qfrc_act, NV * sizeof(double));
+  memcpy(passive, e->qfrc_passive, NV * sizeof(double));
+  memcpy(qacc_smooth, e->qacc_smooth, NV * sizeof(double));
+  memcpy(constraint, e->qfrc_constraint, NV * sizeof(double));
+  memcpy(act_force, e->act_force, NU * sizeof(double));
+}

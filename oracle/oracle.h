@@ -84,6 +84,8 @@ void or_solver_stats(or_env* e, long* calls, long* iters);
 int or_get_efc(or_env* e, int* type, double* pos, double* R, double* aref);
 void or_get_qacc(or_env* e, double* qacc);
 void or_get_mass_matrix(or_env* e, double* M); /* qM (dense NV x NV, CRBA + armature) of the last forward */
+void or_get_smooth(or_env* e, double* bias, double* act, double* passive, double* qacc_smooth, double* constraint,
+                   double* act_force); /* smooth-force terms of the last forward */
 void or_get_obs(or_env* e, float* obs85);
 void or_get_initial_ee(or_env* e, double* T16);
 int or_step_count(or_env* e);

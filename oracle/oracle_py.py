@@ -73,6 +73,7 @@ def lib():
         L.or_get_efc.restype = C.c_int
         L.or_get_efc.argtypes = [C.c_void_p, ip, dp, dp, dp]
         L.or_get_mass_matrix.argtypes = [C.c_void_p, dp]
+        L.or_get_smooth.argtypes = [C.c_void_p, dp, dp, dp, dp, dp, dp]
         L.or_get_obs.argtypes = [C.c_void_p, fp]
         L.or_get_initial_ee.argtypes = [C.c_void_p, dp]
         L.or_step_count.restype = C.c_int
@@ -308,6 +309,13 @@ class OracleEnv:
         M = np.zeros(NV * NV)
         lib().or_get_mass_matrix(self.ptr, _d(M))
         return M.reshape(NV, NV)
+
+    def smooth(self):
+        """Smooth-force terms of the last forward: qfrc_bias, qfrc_actuator, qfrc_passive,
+        qacc_smooth, qfrc_constraint (NV each) and the clamped actuator forces (NU)."""
+        out = [np.zeros(NV) for _ in range(5)] + [np.zeros(NU)]
+        lib().or_get_smooth(self.ptr, *[_d(a) for a in out])
+        return dict(zip(("bias", "actuator", "passive", "qacc_smooth", "constraint", "act_force"), out))
 
     def obs(self):
         o = np.zeros(85, np.float32)

@@ -78,14 +78,18 @@ def _physics_parity(nsub, sts=None, nefc_out=None):
     return np.array(err_q), np.array(err_v)
 
 
-def test_physics_parity_one_substep():  # L1: fp32 GPU vs fp64 oracle, contacts incl. grasps
+def test_physics_parity_one_substep(margin):  # L1: fp32 GPU vs fp64 oracle, contacts incl. grasps
     dq, dv = _physics_parity(1)
+    margin("max_abs_dqpos", float(dq.max()), 1e-5)
+    margin("max_abs_dqvel", float(dv.max()), 5e-3)
     assert dq.max() < 1e-5, dq.max()
     assert dv.max() < 5e-3, dv.max()
 
 
-def test_physics_parity_one_env_step():  # L1: 16 substeps; SURVEY bound qpos <= 1e-4
+def test_physics_parity_one_env_step(margin):  # L1: 16 substeps; SURVEY bound qpos <= 1e-4
     dq, dv = _physics_parity(16)
+    margin("max_abs_dqpos", float(dq.max()), 1e-4)
+    margin("max_abs_dqvel", float(dv.max()), 2e-2)
     assert dq.max() < 1e-4, dq.max()
     assert dv.max() < 2e-2, dv.max()
 
@@ -115,7 +119,7 @@ def _pile_states(n_want=6, min_mean_nefc=215.0):
     return found[:n_want]
 
 
-def test_physics_parity_hbm_overflow_rows():  # L1 on contact piles: rows 192..303 live in HBM
+def test_physics_parity_hbm_overflow_rows(margin):  # L1 on contact piles: rows 192..303 live in HBM
     sts = _pile_states()
     assert len(sts) >= 4, f"only {len(sts)} pile states in 400 C3 steps"
     rows1, rows16 = [], []
@@ -123,9 +127,13 @@ def test_physics_parity_hbm_overflow_rows():  # L1 on contact piles: rows 192..3
     print(f"pile states: rows of the first substep {rows1[0].astype(int).tolist()}, errors qpos {dq.max():.2e} "
           f"qvel {dv.max():.2e}")
     assert (rows1[0] > 192).any(), f"no substep used the overflow rows: {rows1[0]}"
+    margin("substep1_max_abs_dqpos", float(dq.max()), 1e-5)
+    margin("substep1_max_abs_dqvel", float(dv.max()), 5e-3)
     assert dq.max() < 1e-5, dq.max()
     assert dv.max() < 5e-3, dv.max()
     dq, dv = _physics_parity(16, sts, rows16)
+    margin("substep16_max_abs_dqpos", float(dq.max()), 1e-4)
+    margin("substep16_max_abs_dqvel", float(dv.max()), 2e-2)
     assert dq.max() < 1e-4, dq.max()
     assert dv.max() < 2e-2, dv.max()
 
@@ -134,7 +142,7 @@ def _flat(obs, n):  # the 85 numeric observation values (camera images excluded)
     return torch.cat([obs[k].reshape(n, -1) for k in obs if not k.startswith("image_")], 1).cpu().numpy()
 
 
-def test_reset_parity_randomized_seeds():  # L0: PCG64 stream, spawn, task draw, obs codecs
+def test_reset_parity_randomized_seeds(margin):  # L0: PCG64 stream, spawn, task draw, obs codecs
     import oracle_py as O
     from mujoco_manip_amd.vec_env import PickPlaceVecEnv
 
@@ -144,6 +152,7 @@ def test_reset_parity_randomized_seeds():  # L0: PCG64 stream, spawn, task draw,
     obs, _ = env.reset(seed=seeds)
     refs = [O.OracleEnv(action_mode="abs_pos", reward_type="staged", randomize_objects=True) for _ in range(N)]
     robs = np.stack([r.reset(seed=s) for r, s in zip(refs, seeds)])
+    margin("max_abs_dobs", float(np.abs(_flat(obs, N) - robs).max()), 2e-6)
     np.testing.assert_allclose(_flat(obs, N), robs, atol=2e-6)
     assert [tuple(r.task()) for r in refs] == [(o, b) for o, b in env._epi[:, :2].cpu().numpy().tolist()]
     ref_q = np.stack([r.get_state()[0] for r in refs])
@@ -151,7 +160,7 @@ def test_reset_parity_randomized_seeds():  # L0: PCG64 stream, spawn, task draw,
 
 
 @pytest.mark.parametrize("mode", ["abs_pos", "ee_pos_quat_g", "ee_pos_rot6d_g", "ee_pos_quat_g_rel", "ee_pos_rot6d_g_rel"])
-def test_env_step_parity_action_modes(mode):  # L2: decode + 16 x (IK + mj_step) + forward + obs
+def test_env_step_parity_action_modes(mode, margin):  # L2: decode + 16 x (IK + mj_step) + forward + obs
     import oracle_py as O
     from mujoco_manip_amd.vec_env import PickPlaceVecEnv
 
@@ -163,6 +172,7 @@ def test_env_step_parity_action_modes(mode):  # L2: decode + 16 x (IK + mj_step)
     for k, r in enumerate(refs):
         r.reset(seed=k)
     dim = env.action_dim
+    dmax, rmax = 0.0, 0.0
     for t in range(6):
         a = np.zeros((N, dim), np.float32)
         a[:, :3] = rng.uniform(-0.05, 0.05, (N, 3)) + ([0.0, 0.45, 0.42] if "rel" not in mode else 0.0)
@@ -175,11 +185,15 @@ def test_env_step_parity_action_modes(mode):  # L2: decode + 16 x (IK + mj_step)
         got = _flat(obs, N)
         for k, r in enumerate(refs):
             ro, rr, rt, rtr, ri = r.step(a[k])
+            dmax = max(dmax, float(np.abs(got[k, :11] - ro[:11]).max()))
+            rmax = max(rmax, abs(float(rew[k]) - rr))
+            margin("max_abs_dstate", dmax, 1e-4)
+            margin("max_abs_dreward", rmax, 1e-3)
             np.testing.assert_allclose(got[k, :11], ro[:11], atol=1e-4)
             assert abs(float(rew[k]) - rr) < 1e-3
 
 
-def test_expert_rollout_parity_and_completion():  # L2 + L3 (test_pick_and_place.py:274-289)
+def test_expert_rollout_parity_and_completion(margin):  # L2 + L3 (test_pick_and_place.py:274-289)
     import oracle_py as O
     from mujoco_manip_amd.vec_env import PickPlaceVecEnv
 
@@ -206,6 +220,8 @@ def test_expert_rollout_parity_and_completion():  # L2 + L3 (test_pick_and_place
         done_at[(done_at < 0) & (fsm == 10)] = t
         if (done_at >= 0).all():
             break
+    margin("first5_max_abs_dstate", float(max(first_err)), 1e-4)
+    margin("episode_length_max", int(done_at.max()), 2000)
     assert max(first_err) < 1e-4
     assert (done_at >= 0).all(), f"FSM unfinished: {np.where(done_at < 0)[0]}"
     assert done_at.max() < 2000  # reference KAT: <= 2000 gym steps

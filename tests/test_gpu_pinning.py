@@ -105,7 +105,7 @@ def _oracle_run_episode(seed, pool):
     return (o, b), n, succ, obj, placed
 
 
-def test_c3_episodes_match_oracle():
+def test_c3_episodes_match_oracle(margin):
     """SURVEY §8d L2 over 48 C3 episodes (episode seeds SeedSequence(42), all 9 tasks): success
     flag and placement equal, episode length within +-2 env steps, final cube within 1 cm."""
     from mujoco_manip_amd import _lib
@@ -136,7 +136,7 @@ def test_c3_episodes_match_oracle():
     assert (length >= 0).all(), np.where(length < 0)
     assert (env.env_error.cpu().numpy() == 0).all()
     assert len({tuple(t) for t in tasks}) == 9, "the 48 C3 seeds must cover all 9 tasks"
-    bad = []
+    bad, dist, dlen = [], [], []
     for k in range(N):
         task, n, rs, robj, rplaced = _oracle_run_episode(seeds[k], pool)
         assert tuple(tasks[k]) == task
@@ -144,13 +144,18 @@ def test_c3_episodes_match_oracle():
         bp = np.array([(-0.3, 0.55, 0.24), (0.0, 0.65, 0.24), (0.3, 0.55, 0.24)][b])
         placed = np.hypot(*(final[k, :2] - bp[:2])) < 0.05 and final[k, 2] < bp[2] + 0.06
         d = float(np.linalg.norm(final[k] - robj))
+        dist.append(d)
+        dlen.append(int(length[k]) - n)
         if abs(int(length[k]) - n) > 2 or d > 0.01 or bool(succ[k]) != rs or placed != rplaced:
             bad.append((k, task, int(length[k]), n, round(d, 4), bool(succ[k]), rs, placed, rplaced))
     print(f"lengths {length.tolist()}")
+    margin("final_cube_distance_m", max(dist), 0.01, per_episode=[round(x, 6) for x in dist])
+    margin("episode_length_delta", max(abs(x) for x in dlen), 2, per_episode=dlen)
+    margin("outcome_mismatches", len(bad), 0)
     assert not bad, bad
 
 
-def test_solver_exit_criteria_consequence():
+def test_solver_exit_criteria_consequence(margin):
     """the kernel's Newton exit (30 iterations, relative gradient 1e-6) against
     MuJoCo's defaults (100 iterations, 1e-8; fp32 stops earlier on no progress) on the same 48 C3
     episodes in lockstep.  The looser exit changes no episode outcome: equal lengths, success and
@@ -195,6 +200,14 @@ def test_solver_exit_criteria_consequence():
     dfin = np.abs(final[0] - final[1]).max()
     print(f"max |dqpos| {dq:.2e} (first 20 steps {dq_early:.2e}); final cubes {dfin:.2e}; mean Newton "
           f"iterations {its[0]['mean_solver_iter']:.2f} vs {its[1]['mean_solver_iter']:.2f}")
+    tk = envs[0]._epi[:, :2].cpu().numpy()
+    ob = [final[j, np.arange(N)[:, None], 7 * tk[:, 0:1] + np.arange(3)] for j in range(2)]
+    dcar = np.linalg.norm(ob[0] - ob[1], axis=1)  # the carried (target) cube, per episode
+    margin("target_cube_final_distance_m", float(dcar.max()), 1e-2, per_episode=np.round(dcar, 6))
+    margin("max_abs_dqpos_whole", dq)
+    margin("max_abs_dqpos_first20", dq_early, 5e-4)
+    margin("final_qpos_cubes_max_abs", float(dfin), 1e-2)
+    margin("mean_newton_iterations", [its[0]["mean_solver_iter"], its[1]["mean_solver_iter"]])
     assert (length >= 0).all()
     np.testing.assert_array_equal(length[0], length[1])
     np.testing.assert_array_equal(succ[0], succ[1])
@@ -352,18 +365,23 @@ def _ik_parity(states, targets, nsub):
     return np.array(out)
 
 
-def test_physics_parity_with_ik_from_oracle_states():
+def test_physics_parity_with_ik_from_oracle_states(margin):
     """L1 with the IK in the loop (SURVEY A.5 stale kinematics at substeps >= 1): 40 states along an
     oracle expert episode incl. grasps and contacts, toward the FSM's own targets."""
     states, targets = _oracle_states()
     e1 = _ik_parity(states, targets, 1)
+    margin("substep1_ctrl", float(e1[:, 2].max()), 2e-5)
+    margin("substep1_dqpos", float(e1[:, 0].max()), 1e-5)
+    margin("substep1_dqvel", float(e1[:, 1].max()), 5e-3)
     assert e1[:, 2].max() < 2e-5, e1[:, 2].max()  # IK output (ctrl[:7]) after one compute
     assert e1[:, 0].max() < 1e-5 and e1[:, 1].max() < 5e-3, e1.max(0)
     e16 = _ik_parity(states, targets, 16)
+    margin("substep16_dqpos", float(e16[:, 0].max()), 1e-4)
+    margin("substep16_dqvel", float(e16[:, 1].max()), 2e-2)
     assert e16[:, 0].max() < 1e-4 and e16[:, 1].max() < 2e-2, e16.max(0)
 
 
-def test_ik_edge_states():
+def test_ik_edge_states(margin):
     """IKController.compute edge cases (controller.py:21-43, 125-135) on device vs the oracle: the
     ||dq|| > 5 clamp (far targets), the joint-range clip (joints at / past their limits) and a hand
     rotated ~pi about its axis from TARGET_ORI (orientation error near pi)."""
@@ -391,6 +409,8 @@ def test_ik_edge_states():
     e.mj_forward()
     assert np.linalg.norm(e.ik(targets[0]) - q0[:7]) > 1.0
     err = _ik_parity(states, targets, 1)
+    margin("ctrl", float(err[:, 2].max()), 5e-5)
+    margin("dqpos", float(err[:, 0].max()), 1e-5)
     assert err[:, 2].max() < 5e-5, err[:, 2]
     assert err[:, 0].max() < 1e-5, err[:, 0]
 
@@ -461,7 +481,7 @@ def test_observation_goldens_on_device(golden):
 
 
 # --------------------------------------------------------------------------- per-physics-step FSM
-def test_expert_physics_parity_with_oracle():
+def test_expert_physics_parity_with_oracle(margin):
     """main.py:65-91 loop (update() = plan(1) + _actuate(), then mj_step) on device vs the oracle
     over the first 400 physics steps of 4 tasks from the keyframe (approach + grasp descent)."""
     import oracle_py as O
@@ -478,6 +498,7 @@ def test_expert_physics_parity_with_oracle():
         e.mj_forward()
         e.fsm_init([(o, b)])
         refs.append(e)
+    marm, mcube = 0.0, 0.0
     for chunk in range(4):
         sim.expert_physics(100)
         gq = sim.get_state()[0]
@@ -489,6 +510,10 @@ def test_expert_physics_parity_with_oracle():
                 e.mj_step()
             rq = e.get_state()[0]
             assert epi[k, 4] == e.fsm_get()["state"], (chunk, k)
+            marm = max(marm, float(np.abs(gq[k, :9] - rq[:9]).max()))
+            mcube = max(mcube, float(np.abs(gq[k, 9:] - rq[9:]).max()))
+            margin("robot_joints", marm, 2e-4)
+            margin("cubes", mcube, 5e-3)
             # robot joints tight (IK + smooth dynamics); the cubes (touched by the fingers from the
             # grasp descent on) behaviourally, as SURVEY §8d L2 treats contact dynamics
             np.testing.assert_allclose(gq[k, :9], rq[:9], atol=2e-4, err_msg=f"chunk {chunk} env {k}")

@@ -253,3 +253,40 @@ def test_c5_full_batch_properties():
             agree = (seg[i, ci].cpu().numpy() == ref).mean()
             assert agree > 0.98, (i, cam, agree)
     env.close()
+
+
+@pytest.mark.gpu
+def test_render_after_divergence_without_autoreset():
+    """with autoreset off (the dataset loop's setting) a diverged env's NaN / Inf poses
+    reach the renderer.  The step must flag the env (env_error NaN bit), the render must complete
+    without a fault, and every other env's images must equal a run without the injected state bit
+    for bit (the renderer's NaN culling is an integer test, independent of the fp-math flags)."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs an MI355X")
+    from mujoco_manip_amd import _lib
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    outs = []
+    for inject in (False, True):
+        env = PickPlaceVecEnv(4, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
+                              image_size=64, autoreset=False)
+        env.reset(seed=[_lib.episode_seed(13, i) for i in range(4)])
+        if inject:
+            q, v, c, w = env.sim.get_state()
+            v[1, 3] = np.nan
+            v[2, 0] = np.inf
+            env.sim.set_state(q, v, c, w)
+        for _ in range(2):
+            obs, *_ = env.step(env.expert_plan(16))
+        torch.cuda.synchronize()
+        outs.append((obs["image_overhead"].cpu().numpy(), obs["image_wrist"].cpu().numpy(),
+                     env.segmentation.cpu().numpy(), env.env_error.cpu().numpy()))
+        env.close()
+    (o0, w0, s0, e0), (o1, w1, s1, e1) = outs
+    assert (e0 == 0).all()
+    assert e1[1] != 0 and e1[2] != 0 and e1[0] == 0 and e1[3] == 0, e1
+    for k in (0, 3):
+        np.testing.assert_array_equal(o1[k], o0[k])
+        np.testing.assert_array_equal(w1[k], w0[k])
+        np.testing.assert_array_equal(s1[k], s0[k])
+    assert s1.max() <= 9  # valid segment ids everywhere, the diverged envs' images included
