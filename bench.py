@@ -240,6 +240,53 @@ def pmc_evidence(workload: str, envs: int, lanes: int) -> dict | None:
     return rec
 
 
+def binding_roof(pmc: dict | None, workload: str) -> dict | None:
+    """What bounds the step kernel, from counter evidence of this configuration: the SQ pass of
+    pmc_<workload>.json (VALU instructions and issue per wave, active lanes), the extended SQ pass
+    (any-instruction issue per wave) and the VALU issue calibration (what a wave / SIMD can issue).
+    HBM is not the roof: the constraint working set MuJoCo streams (SURVEY §8d's algorithmic bytes)
+    stays in LDS here, so the HBM frac cannot pass ~0.2 by design."""
+    if pmc is None or not pmc.get("valu"):
+        return None
+    v = pmc["valu"]
+    out = {"valu_insts_per_env_step": v.get("valu_insts_per_env_step"),
+           "valu_issue_per_wave": v.get("active_inst_valu_per_wave_cycle"),
+           "waves_per_simd": v.get("waves_per_simd"),
+           "valu_issue_per_simd": v.get("frac"),
+           "active_lane_fraction": v.get("active_lane_fraction"),
+           "lane_weighted_valu_issue_per_simd": (v["frac"] * v["active_lane_fraction"]
+                                                 if v.get("frac") and v.get("active_lane_fraction") else None),
+           "hbm_frac_note": "HBM frac <= ~0.2 by design while the efc working set stays in LDS (DESIGN §4)",
+           "units": "SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (quad-cycles): instructions per quad-cycle"}
+    cal_f = os.path.join(REPO, "profiles", "r05_valu_issue_calibration.json")
+    ext_f = os.path.join(REPO, "profiles", f"r05_{workload}_sq_extended.json")
+    try:
+        cal = json.load(open(cal_f))
+        two = [r for r in cal["scalar_v_fma_f32"] if r["chains"] == 8 and r["waves_per_simd"] == 2][0]
+        ceil_w = 4.0 / two["cycles_per_fma_inst_per_wave"]  # VALU per quad-cycle one wave can issue
+        out["valu_issue_ceiling_per_wave"] = ceil_w
+        out["valu_issue_ceiling_per_simd"] = ceil_w * (v.get("waves_per_simd") or 2)
+        out["valu_issue_frac_of_ceiling"] = v["active_inst_valu_per_wave_cycle"] / ceil_w
+        out["calibration"] = "profiles/r05_valu_issue_calibration.json"
+    except (OSError, ValueError, KeyError, IndexError, TypeError, ZeroDivisionError):
+        pass
+    try:
+        ext = json.load(open(ext_f))["per_wave_quad_cycle"]
+        out["any_inst_issue_per_wave"] = ext["SQ_ACTIVE_INST_ANY"]
+        out["salu_issue_per_wave"] = ext["SQ_INSTS_SALU"]
+        out["extended_sq"] = os.path.relpath(ext_f, REPO)
+    except (OSError, ValueError, KeyError):
+        pass
+    frac = out.get("valu_issue_frac_of_ceiling")
+    out["bound"] = ("latency" if frac is not None and frac < 0.6 else "valu-issue")
+    out["note"] = ("a wave issues one instruction per quad-cycle at most and VALU at ~0.94 per quad-cycle "
+                   "(calibration); the step kernel's waves issue VALU at the fraction above of that and any "
+                   "instruction in ~56 % of their quad-cycles: latency / dependency-bound, so env steps/s follow "
+                   "the resident envs per CU (profiles/r05_occupancy_probe.json) and the instructions on each "
+                   "env's critical path, not the VALU rate")
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -448,6 +495,8 @@ def main():
                          "min_hbm_bytes_per_launch": min_bytes,
                          "min_hbm_GBs": lanes * min_bytes / (kern_ms * 1e-3) / 1e9},
             "valu": None if pmc is None else pmc.get("valu"),
+            # the binding roof of the step kernel (what the HBM roofline object above is not)
+            "bound": binding_roof(pmc, args.workload),
             "render": render,
             "cpu_baseline": cpu,
             "solver": solver,
