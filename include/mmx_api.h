@@ -170,6 +170,13 @@ int mmx_png_encode(mmx_sim* sim, const uint8_t* rgb_dev, int64_t img_stride, int
 int mmx_png_pack(mmx_sim* sim, const uint8_t* out_dev, int64_t out_stride, const int32_t* sizes_dev,
                  const int64_t* offsets_dev, int32_t n, uint8_t* packed_dev);
 
+/* Per-image channel statistics of n RGB8 images (device, image i at rgb_dev + i * img_stride, rows
+ * of 3 * width bytes, width and height <= 4096): out_dev[i] = int64 [min R G B, max R G B, sum R G B,
+ * sum of squares R G B] over every pixel (LeRobot's image feature statistics, which the dataset
+ * writer scales to [0, 1]; generate_dataset.py:250-260).  Asynchronous on the sim's stream. */
+int mmx_image_stats(mmx_sim* sim, const uint8_t* rgb_dev, int64_t img_stride, int32_t n, int32_t width,
+                    int32_t height, int64_t* out_dev);
+
 /* Physics-level entry points (parity harnesses): n x mujoco.mj_step with the current ctrl
  * (env.py:119-121), optionally preceded by IKController.compute toward the decoded target
  * each substep; and the mj_forward position stage (kinematics + IK cache). */

@@ -57,7 +57,7 @@ EXPORTED = ("mmx_config_default", "mmx_create", "mmx_destroy", "mmx_last_error",
             "mmx_expert_plan", "mmx_rollout_expert", "mmx_physics_step", "mmx_forward", "mmx_get_buffers",
             "mmx_synchronize", "mmx_get_state", "mmx_set_state", "mmx_episode_seed", "mmx_rollout_lanes",
             "mmx_rollout_steps_per_launch", "mmx_rollout_launches", "mmx_expert_physics", "mmx_eval_reward", "mmx_kernel_timing",
-            "mmx_kernel_times", "mmx_png_bound", "mmx_png_scratch", "mmx_png_encode", "mmx_png_pack",
+            "mmx_kernel_times", "mmx_png_bound", "mmx_png_scratch", "mmx_png_encode", "mmx_png_pack", "mmx_image_stats",
             "mmx_queue_init", "mmx_queue_advance")
 
 _lib = None
@@ -103,6 +103,7 @@ def load(build_if_missing: bool = True):
     L.mmx_png_scratch.restype = C.c_int64
     L.mmx_png_encode.argtypes = [vp, vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, vp, C.c_int64, vp, vp]
     L.mmx_png_pack.argtypes = [vp, vp, C.c_int64, vp, vp, C.c_int32, vp]
+    L.mmx_image_stats.argtypes = [vp, vp, C.c_int64, C.c_int32, C.c_int32, C.c_int32, vp]
     L.mmx_kernel_times.argtypes = [vp, fp, i32p, fp, i32p]
     L.mmx_get_buffers.argtypes = [vp, C.POINTER(MMXBuffers)]
     L.mmx_synchronize.argtypes = [vp]
@@ -115,7 +116,7 @@ def load(build_if_missing: bool = True):
     for name in ("mmx_create", "mmx_reset", "mmx_step", "mmx_expert_plan", "mmx_rollout_expert", "mmx_physics_step",
                  "mmx_forward", "mmx_get_buffers", "mmx_synchronize", "mmx_get_state", "mmx_set_state",
                  "mmx_expert_physics", "mmx_eval_reward", "mmx_kernel_timing", "mmx_kernel_times", "mmx_png_encode",
-                 "mmx_png_pack", "mmx_queue_init", "mmx_queue_advance"):
+                 "mmx_png_pack", "mmx_image_stats", "mmx_queue_init", "mmx_queue_advance"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L
@@ -354,6 +355,30 @@ class Sim:
         packed.record_stream(cur)
         ends.record_stream(cur)
         return packed, ends
+
+    def image_stats(self, images):
+        """Per-image channel statistics of RGB8 images [n, H, W, 3] (CUDA uint8, rows contiguous, any
+        stride between images) on the device, asynchronously on the caller's stream: int64 [n, 4, 3]
+        = (min, max, sum, sum of squares) x (R, G, B) over every pixel (mmx_image_stats)."""
+        import torch
+
+        n, H, W, c = images.shape
+        assert c == 3 and images.dtype == torch.uint8 and images.is_cuda
+        assert images.stride(1) == W * 3 and images.stride(2) == 3 and images.stride(3) == 1, "rows must be contiguous"
+        out = torch.empty((n, 4, 3), dtype=torch.int64, device=images.device)
+        if n == 0:
+            return out
+        cur = torch.cuda.current_stream(images.device)
+        sst = (torch.cuda.ExternalStream(self.cfg.stream, device=images.device) if self.cfg.stream
+               else torch.cuda.default_stream(images.device))
+        sst.wait_stream(cur)
+        with torch.cuda.stream(sst):
+            images.record_stream(sst)
+            out.record_stream(sst)
+            self._check(self.L.mmx_image_stats(self.ptr, C.c_void_p(images.data_ptr()), images.stride(0), n, W, H,
+                                               C.c_void_p(out.data_ptr())), "mmx_image_stats")
+        cur.wait_stream(sst)
+        return out
 
     @property
     def rollout_lanes(self) -> int:

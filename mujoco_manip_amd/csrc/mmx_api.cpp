@@ -33,6 +33,8 @@ extern "C" hipError_t mmx_launch_png(const uint8_t* rgb, int64_t img_stride, int
                                      int64_t out_stride, int32_t* sizes, uint32_t* scratch, hipStream_t st);
 extern "C" hipError_t mmx_launch_png_pack(const uint8_t* out, int64_t out_stride, const int32_t* sizes,
                                           const int64_t* offsets, int n, uint8_t* packed, hipStream_t st);
+extern "C" hipError_t mmx_launch_image_stats(const uint8_t* rgb, int64_t img_stride, int n, int64_t npx, int64_t* out,
+                                             hipStream_t st);
 extern "C" int64_t mmx_png_bound_bytes(int width, int height);
 extern "C" int64_t mmx_png_scratch_bytes(int width, int height);
 extern "C" hipError_t mmx_launch_expert_physics(const MMXState* S, int n, hipStream_t st);
@@ -559,6 +561,16 @@ int mmx_png_pack(mmx_sim* sim, const uint8_t* out_dev, int64_t out_stride, const
   DeviceGuard guard(sim);
   return hip_check(sim, mmx_launch_png_pack(out_dev, out_stride, sizes_dev, offsets_dev, n, packed_dev, sim->stream),
                    "mmx_png_pack");
+}
+
+int mmx_image_stats(mmx_sim* sim, const uint8_t* rgb_dev, int64_t img_stride, int32_t n, int32_t width, int32_t height,
+                    int64_t* out_dev) {
+  if (!sim || n < 0 || (n > 0 && (!rgb_dev || !out_dev)) || width <= 0 || height <= 0 || width > 4096 ||
+      height > 4096 || img_stride < 3LL * width * height)
+    return sim ? fail(sim, MMX_EINVAL, "mmx_image_stats: bad arguments") : MMX_EINVAL;
+  DeviceGuard guard(sim);
+  return hip_check(sim, mmx_launch_image_stats(rgb_dev, img_stride, n, (int64_t)width * height, out_dev, sim->stream),
+                   "mmx_image_stats");
 }
 
 int mmx_rollout_steps_per_launch(const mmx_sim* sim) {

@@ -18,6 +18,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include <type_traits>
 
 #define MMX_MODEL_QUAL static __constant__
@@ -3028,7 +3031,12 @@ extern "C" hipError_t mmx_fsm_profile(double* out, int reset) {
 extern "C" int mmx_fsm_profile_fields() { return FSMP_N; }
 #endif
 
-extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
+// waves per SIMD the step kernel's register allocation is made for (2: <= 256 VGPRs; the A/B build
+// MMX_STEP_WAVES=3 caps it at 168)
+#ifndef MMX_STEP_WAVES
+#define MMX_STEP_WAVES 2
+#endif
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MMX_STEP_WAVES, MMX_STEP_WAVES)))
 mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert, int base, int nsteps) {
   const int i = base + blockIdx.x;
   if (i >= S.N) return;
@@ -3251,12 +3259,22 @@ extern "C" hipError_t mmx_launch_reset(const MMXState* S, const unsigned char* m
   hipLaunchKernelGGL(mmx_reset_kernel, dim3(S->N), dim3(WG), 0, st, *S, mask, task);
   return hipGetLastError();
 }
+// Occupancy probe (diagnostics only, never set by the product): MMX_LDS_PAD bytes of dynamic LDS
+// per step-kernel workgroup lower the envs per CU (tools/occupancy_probe.sh).
+static size_t step_lds_pad() {
+  static const size_t pad = [] {
+    const char* v = std::getenv("MMX_LDS_PAD");
+    return v ? (size_t)std::max(0, std::atoi(v)) : (size_t)0;
+  }();
+  return pad;
+}
 // envs [base, base+count): independent env ranges may run on separate streams
 extern "C" hipError_t mmx_launch_step(const MMXState* S, const float* action, int adim, int expert, int base,
                                       int count, int nsteps, hipStream_t st) {
   if (count <= 0 || nsteps <= 0) return hipSuccess;
   if (nsteps > 1 && !expert) return hipErrorInvalidValue;  // host actions: one env step per launch
-  hipLaunchKernelGGL(mmx_env_step_kernel, dim3(count), dim3(64), 0, st, *S, action, adim, expert, base, nsteps);
+  hipLaunchKernelGGL(mmx_env_step_kernel, dim3(count), dim3(64), step_lds_pad(), st, *S, action, adim, expert, base,
+                     nsteps);
   return hipGetLastError();
 }
 extern "C" hipError_t mmx_launch_expert(const MMXState* S, int n, float* action, hipStream_t st) {

@@ -3,14 +3,13 @@
 // raw: each RGB8 image becomes a complete PNG file in one workgroup, so the host receives
 // compressed bytes (flat-shaded renders compress ~8x) and does no image work.
 //
-// One 256-lane workgroup per image:
+// One 256-lane workgroup per image (128 lanes for images of at most 128 rows):
 //   1. rows in parallel (one row per lane): the PNG scanline (filter byte 0 + RGB bytes) is parsed
 //      greedily into deflate symbols with two match candidates, the same pixel 3 bytes back and
 //      the byte one scanline above (distance 3 S + 1); matches stay inside their row, so every
-//      row parses independently.  Pass 1 counts each row's bits (fixed Huffman codes, RFC 1951
-//      §3.2.6) and its Adler-32 partial sums; a workgroup scan gives every row its bit offset in
-//      the single final block; pass 2 re-parses and writes the row's bits to a row-private
-//      scratch stream;
+//      row parses independently.  One pass writes each row's bits (fixed Huffman codes, RFC 1951
+//      §3.2.6) to a row-private scratch stream and counts them, with the row's Adler-32 partial
+//      sums; a workgroup scan then gives every row its bit offset in the single final block;
 //   2. every lane assembles whole dwords of the block from the rows that overlap them (no atomics),
 //      then the zlib stream (header 78 01, block, Adler-32) is cut into IDAT chunks of kChunk
 //      bytes written after the signature and IHDR; one lane per chunk computes its CRC-32; IEND
@@ -183,12 +182,15 @@ __device__ void png_encode(const uint8_t* rgb, int64_t img_stride, int W, int H,
   uint32_t* scr = scratch + (int64_t)img * H * rw;
   uint8_t* o = out + (int64_t)img * out_stride;
   for (int k = tid; k < 256; k += WG) s_crc[k] = crc_table(k);
-  // pass 1: row bit counts and Adler-32 partial sums (s1: sum of bytes, s2: sum of (n - i) byte_i)
+  // one pass: each row's bits into its private stream, its bit count, and the Adler-32 partial sums
+  // (s1: sum of bytes, s2: sum of (n - i) byte_i)
   const uint64_t n = (uint64_t)H * L1;
   uint64_t a1 = 0, a2 = 0;
   for (int r = tid; r < H; r += WG) {
     const uint8_t* row = im + (int64_t)r * L;
-    s_off[r + 1] = (int32_t)parse_row<false>(row, r ? row - L : nullptr, L1, nullptr);
+    BitSink bs{scr + (int64_t)r * rw, 0ull, 0, 0};  // (the row's stream is private: no offset needed yet)
+    s_off[r + 1] = (int32_t)parse_row<true>(row, r ? row - L : nullptr, L1, &bs);
+    bs.flush();
     const uint64_t i0 = (uint64_t)r * L1 + 1;  // the filter byte (0) adds nothing
     for (int k = 0; k < L; k++) {
       const uint64_t b = row[k];
@@ -211,13 +213,6 @@ __device__ void png_encode(const uint8_t* rgb, int64_t img_stride, int W, int H,
     s_tot = s_off[H] + 7;  // + end of block (code 256: seven 0 bits)
   }
   __syncthreads();
-  // pass 2: each row's bits into its private stream
-  for (int r = tid; r < H; r += WG) {
-    const uint8_t* row = im + (int64_t)r * L;
-    BitSink bs{scr + (int64_t)r * rw, 0ull, 0, 0};
-    parse_row<true>(row, r ? row - L : nullptr, L1, &bs);
-    bs.flush();
-  }
   __threadfence();  // the streams are read by other lanes of the workgroup
   __syncthreads();
   const uint32_t adler = (uint32_t)s_a1[0];
@@ -334,5 +329,112 @@ extern "C" hipError_t mmx_launch_png_pack(const uint8_t* out, int64_t out_stride
                                           const int64_t* offsets, int n, uint8_t* packed, hipStream_t st) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(mmx_png_pack_kernel, dim3(n), dim3(PNG_WG), 0, st, out, out_stride, sizes, offsets, packed);
+  return hipGetLastError();
+}
+
+// ============================================================================ image statistics
+// Per-image, per-channel min / max / sum / sum of squares of RGB8 images (LeRobot's image feature
+// statistics, generate_dataset.py:250-260; the dataset scales them to [0, 1]): out[i] = int64
+// [min R G B, max R G B, sum R G B, sumsq R G B], exact integers.  One 256-lane workgroup per image,
+// a single pass over its bytes (HBM-bound: one read of the frames the PNG encoder reads anyway),
+// replacing the dataset's torch reductions (4-6 passes with int32 / int64 widening copies).
+// Fast path (image base 4-byte aligned, pixel count a multiple of 4): a lane reads 3 dwords = 4
+// pixels; the channels' bytes of the 3 dwords fall on disjoint byte lanes, so each channel's 4
+// bytes are gathered into one dword with AND / OR, then v_dot4_u32_u8 against 0x01010101 (sum)
+// and against itself (sum of squares).  Otherwise one pixel per step.
+#define IST_WG 256
+__device__ __forceinline__ void ist_minmax4(uint32_t x, uint32_t& mn, uint32_t& mx) {
+#pragma unroll
+  for (int k = 0; k < 4; k++) {
+    const uint32_t b = (x >> (8 * k)) & 255u;
+    mn = min(mn, b);
+    mx = max(mx, b);
+  }
+}
+__device__ __forceinline__ uint64_t ist_wave_sum(uint64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ uint32_t ist_wave_min(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+__device__ __forceinline__ uint32_t ist_wave_max(uint32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o, 64));
+  return v;
+}
+extern "C" __global__ void __launch_bounds__(IST_WG)
+mmx_image_stats_kernel(const uint8_t* rgb, int64_t img_stride, int64_t npx, int64_t* out) {
+  const int img = blockIdx.x, tid = threadIdx.x;
+  const uint8_t* im = rgb + (int64_t)img * img_stride;
+  uint32_t mn[3] = {255u, 255u, 255u}, mx[3] = {0u, 0u, 0u};
+  uint64_t sm[3] = {0, 0, 0}, sq[3] = {0, 0, 0};
+  if ((reinterpret_cast<uintptr_t>(im) & 3) == 0 && (npx & 3) == 0) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(im);
+    const int64_t ng = npx >> 2;  // groups of 4 pixels = 3 dwords
+    // (per-lane 32-bit partial sums: at most 4 x 255^2 per group and npx / 4 / 256 groups per lane
+    // before the 64-bit fold below, i.e. safe for images up to 4096 x 4096)
+    uint32_t s32[3] = {0u, 0u, 0u}, q32[3] = {0u, 0u, 0u};
+    for (int64_t g = tid; g < ng; g += IST_WG) {
+      const uint32_t w0 = w[3 * g], w1 = w[3 * g + 1], w2 = w[3 * g + 2];
+      // bytes: w0 = R0 G0 B0 R1, w1 = G1 B1 R2 G2, w2 = B2 R3 G3 B3 (little-endian byte order)
+      const uint32_t xr = (w0 & 0xFF0000FFu) | (w1 & 0x00FF0000u) | (w2 & 0x0000FF00u);
+      const uint32_t xg = (w0 & 0x0000FF00u) | (w1 & 0xFF0000FFu) | (w2 & 0x00FF0000u);
+      const uint32_t xb = (w0 & 0x00FF0000u) | (w1 & 0x0000FF00u) | (w2 & 0xFF0000FFu);
+      const uint32_t xc[3] = {xr, xg, xb};
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        s32[c] = __builtin_amdgcn_udot4(xc[c], 0x01010101u, s32[c], false);
+        q32[c] = __builtin_amdgcn_udot4(xc[c], xc[c], q32[c], false);
+        ist_minmax4(xc[c], mn[c], mx[c]);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      sm[c] = s32[c];
+      sq[c] = q32[c];
+    }
+  } else {
+    for (int64_t p = tid; p < npx; p += IST_WG) {
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        const uint32_t b = im[3 * p + c];
+        mn[c] = min(mn[c], b);
+        mx[c] = max(mx[c], b);
+        sm[c] += b;
+        sq[c] += b * b;
+      }
+    }
+  }
+  __shared__ uint64_t red[IST_WG / 64][12];
+  const int wv = tid >> 6;
+#pragma unroll
+  for (int c = 0; c < 3; c++) {
+    const uint32_t a = ist_wave_min(mn[c]), b = ist_wave_max(mx[c]);
+    const uint64_t s1 = ist_wave_sum(sm[c]), s2 = ist_wave_sum(sq[c]);
+    if ((tid & 63) == 0) {
+      red[wv][c] = a;
+      red[wv][3 + c] = b;
+      red[wv][6 + c] = s1;
+      red[wv][9 + c] = s2;
+    }
+  }
+  __syncthreads();
+  if (tid < 12) {
+    uint64_t v = red[0][tid];
+    for (int k = 1; k < IST_WG / 64; k++) {
+      const uint64_t u = red[k][tid];
+      v = tid < 3 ? min(v, u) : (tid < 6 ? max(v, u) : v + u);
+    }
+    out[(int64_t)img * 12 + tid] = (int64_t)v;
+  }
+}
+extern "C" hipError_t mmx_launch_image_stats(const uint8_t* rgb, int64_t img_stride, int n, int64_t npx, int64_t* out,
+                                             hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mmx_image_stats_kernel, dim3(n), dim3(IST_WG), 0, st, rgb, img_stride, npx, out);
   return hipGetLastError();
 }

@@ -306,11 +306,29 @@ def _raw_image_stats(frames_u8: list) -> dict:
             "_sum": x.sum(0).tolist(), "_sumsq": (x * x).sum(0).tolist(), "_n": int(len(x))}
 
 
+# [min, max, sum, sum of squares] of the uint8 values -> the same of the values scaled to [0, 1]
+_STAT_SCALE = (1.0 / 255.0, 1.0 / 255.0, 1.0 / 255.0, 1.0 / (255.0 * 255.0))
+_STAT_SCALE_DEV = {}
+
+
+def _frame_image_stats_device(sim, imgs):
+    """Per-frame channel statistics of uint8 images [k, H, W, 3] by the HIP kernel mmx_image_stats
+    (one pass over the frames, exact integers) -> float64 [k, 4, 3], the values of
+    _frame_image_stats bit for bit (the same integers scaled by the same constants)."""
+    import torch
+
+    st = sim.image_stats(imgs).to(torch.float64)
+    scale = _STAT_SCALE_DEV.get(st.device)
+    if scale is None:  # cached per device: a host-to-device copy per step would wait for the queue
+        scale = _STAT_SCALE_DEV[st.device] = torch.tensor(_STAT_SCALE, dtype=torch.float64, device=st.device)[None, :, None]
+    return st * scale
+
+
 def _frame_image_stats(imgs, chunk=None):
-    """Per-frame channel statistics of uint8 images [k, H, W, 3] on the device: min, max, sum and
-    sum of squares of the pixel values scaled to [0, 1] -> float64 [k, 4, 3].  Min / max on the
-    uint8 values, sums exact in integers (int32 values, int64 sums) and scaled at the end, in
-    chunks of `chunk` images (default: 256 MB of int32 values; no float64 copy of the frames)."""
+    """Torch form of _frame_image_stats_device (the reference for its test; the dataset loop uses
+    the kernel): min, max, sum and sum of squares of the pixel values scaled to [0, 1] -> float64
+    [k, 4, 3].  Min / max on the uint8 values, sums exact in integers (int32 values, int64 sums) and
+    scaled at the end, in chunks of `chunk` images (default: 256 MB of int32 values)."""
     import torch
 
     k = imgs.shape[0]
@@ -529,7 +547,7 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
                 png_est[f] = packed.numel() // 4
             frame[f + "/png"] = packed[:min(png_est[f], packed.numel())]
             frame[f + "/ends"] = ends
-            frame[f + "/stats"] = _frame_image_stats(imgs)
+            frame[f + "/stats"] = _frame_image_stats_device(env.sim, imgs)
             payload[f] = packed
         if need_actions:
             enc = encode_actions(action[:, :3], action[:, 3], env.initial_ee_se3)

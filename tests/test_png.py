@@ -154,3 +154,31 @@ def test_png_encode_device_matches_host_path(sim):
         assert packed.numel() == 5 * sim.L.mmx_png_bound(56, 40)
         np.testing.assert_array_equal(np.concatenate([[0], ends]), woffs)
         np.testing.assert_array_equal(packed[:int(ends[-1])].cpu().numpy(), want.cpu().numpy())
+
+
+def test_image_stats_kernel_equals_torch_definition(sim):
+    """mmx_image_stats (one HIP pass, dword-gathered channel bytes + v_dot4) equals the torch
+    definition of the dataset's per-frame statistics bit for bit: aligned 4-pixel groups (128^2,
+    224^2), sizes whose pixel count is not a multiple of 4 (byte path), a camera batch with a stride
+    between images (the dataset's [N, 2, S, S, 3] images, one camera) and extreme values."""
+    from mujoco_manip_amd import dataset as D
+
+    rng = np.random.default_rng(21)
+    cases = [rng.integers(0, 256, (7, 128, 128, 3), dtype=np.uint8),
+             rng.integers(0, 256, (3, 224, 224, 3), dtype=np.uint8),
+             rng.integers(0, 256, (4, 17, 23, 3), dtype=np.uint8),
+             np.zeros((2, 16, 16, 3), np.uint8), np.full((2, 16, 16, 3), 255, np.uint8)]
+    for imgs in cases:
+        t = torch.as_tensor(imgs).cuda()
+        got = sim.image_stats(t).cpu().numpy()
+        x = imgs.reshape(len(imgs), -1, 3).astype(np.int64)
+        want = np.stack([x.min(1), x.max(1), x.sum(1), (x * x).sum(1)], 1)
+        np.testing.assert_array_equal(got, want)
+        np.testing.assert_array_equal(D._frame_image_stats_device(sim, t).cpu().numpy(),
+                                      D._frame_image_stats(t).cpu().numpy())
+    both = torch.as_tensor(rng.integers(0, 256, (5, 2, 64, 64, 3), dtype=np.uint8)).cuda()
+    for cam in (0, 1):
+        v = both[:, cam]
+        assert v.stride(0) == 2 * 64 * 64 * 3
+        np.testing.assert_array_equal(sim.image_stats(v).cpu().numpy(),
+                                      sim.image_stats(v.contiguous()).cpu().numpy())
