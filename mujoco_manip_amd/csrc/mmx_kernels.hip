@@ -544,12 +544,42 @@ DEV void rne_wave(EnvSh& E) {
   SYNC();
 }
 
-// (A^{-1} v)_j in lane j for a small SPD A given by rows (lane j holds row j in arow[0..N)).
-// Right-looking Cholesky with v_readlane broadcasts; lane k keeps column k of L (selects) for
-// the transposed solve.  eps: pivot floor.
+// DPP row_newbcast:K, the value of lane K of each 16-lane row in every lane of that row
+template <int K>
+DEV float row_bcast_t(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + K, 0xF, 0xF, true));
+}
+// k is a constant of a fully unrolled loop at every call: the switch folds to one DPP move
+DEV float row_bcast(float v, int k) {
+  switch (k) {
+    case 0: return row_bcast_t<0>(v);
+    case 1: return row_bcast_t<1>(v);
+    case 2: return row_bcast_t<2>(v);
+    case 3: return row_bcast_t<3>(v);
+    case 4: return row_bcast_t<4>(v);
+    case 5: return row_bcast_t<5>(v);
+    case 6: return row_bcast_t<6>(v);
+    case 7: return row_bcast_t<7>(v);
+    default: return row_bcast_t<8>(v);
+  }
+}
+// broadcast of lane k's value (k < 16) to the lanes of DPP row 0 that hold the small system: one
+// row_newbcast (a VGPR result, no SGPR round trip and its hazard nops) or, the A/B form, v_readlane
+#ifndef MMX_CHOL_SMALL_DPP
+#define MMX_CHOL_SMALL_DPP 1
+#endif
+DEV float small_bcast(float v, int k) {
+  return MMX_CHOL_SMALL_DPP ? row_bcast(v, k) : __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
+}
+
+// (A^{-1} v)_j in lane j for a small SPD A given by rows (lane j holds row j in arow[0..N), N <= 9:
+// the rows sit in DPP row 0; lanes of rows 1..3 compute values nobody reads).  Right-looking
+// Cholesky with lane broadcasts; lane k keeps column k of L (selects) for the transposed solve.
+// eps: pivot floor.  The arithmetic is the same in either broadcast form (bit-identical results).
 template <int N>
 DEV float chol_solve_small(const float* arow, float v, float eps) {
-  const int j = LANE;
+  static_assert(N <= 9, "row_bcast covers lanes 0..8");
+  const int j = LANE & 15;
   float h[N], c[N], dinv[N];
 #pragma unroll
   for (int i = 0; i < N; i++) {
@@ -558,7 +588,7 @@ DEV float chol_solve_small(const float* arow, float v, float eps) {
   }
 #pragma unroll
   for (int k = 0; k < N; k++) {
-    const float d = fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(h[k]), k)), eps);
+    const float d = fmaxf(small_bcast(h[k], k), eps);
     const float inv = __builtin_amdgcn_rsqf(d), sd = d * inv;
     dinv[k] = inv;
     const float l = j == k ? sd : h[k] * inv;
@@ -566,7 +596,7 @@ DEV float chol_solve_small(const float* arow, float v, float eps) {
     c[k] = j == k ? sd : c[k];
 #pragma unroll
     for (int i = k + 1; i < N; i++) {
-      const float li = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(l), i));
+      const float li = small_bcast(l, i);
       h[i] = fmaf(-li, l, h[i]);
       c[i] = j == k ? li : c[i];
     }
@@ -574,12 +604,12 @@ DEV float chol_solve_small(const float* arow, float v, float eps) {
   float y = j < N ? v : 0.f;
 #pragma unroll
   for (int k = 0; k < N; k++) {
-    const float yk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(y), k)) * dinv[k];
+    const float yk = small_bcast(y, k) * dinv[k];
     y = j == k ? yk : (j > k ? fmaf(-h[k], yk, y) : y);
   }
 #pragma unroll
   for (int k = N - 1; k >= 0; k--) {
-    const float zk = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(y), k)) * dinv[k];
+    const float zk = small_bcast(y, k) * dinv[k];
     y = j == k ? zk : (j < k ? fmaf(-c[k], zk, y) : y);
   }
   return y;
@@ -1336,25 +1366,6 @@ DEV int newton_dof(int L) {
   return r == 0 ? (k < 9 ? k : -1) : (k < 6 ? 9 + 6 * (r - 1) + k : -1);
 }
 __host__ __device__ constexpr int newton_lane(int d) { return d < 9 ? d : 16 * (1 + (d - 9) / 6) + (d - 9) % 6; }
-// DPP row_newbcast:K, the value of lane K of each 16-lane row in every lane of that row
-template <int K>
-DEV float row_bcast_t(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x150 + K, 0xF, 0xF, true));
-}
-// k is a constant of a fully unrolled loop at every call: the switch folds to one DPP move
-DEV float row_bcast(float v, int k) {
-  switch (k) {
-    case 0: return row_bcast_t<0>(v);
-    case 1: return row_bcast_t<1>(v);
-    case 2: return row_bcast_t<2>(v);
-    case 3: return row_bcast_t<3>(v);
-    case 4: return row_bcast_t<4>(v);
-    case 5: return row_bcast_t<5>(v);
-    case 6: return row_bcast_t<6>(v);
-    case 7: return row_bcast_t<7>(v);
-    default: return row_bcast_t<8>(v);
-  }
-}
 
 // J_i . x for a block-format row (slots past the row's width hold zeros)
 DEV float row_dot16(const EnvSh& E, int i, const float* x) {
