@@ -19,6 +19,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <cstdlib>
 
 #include <type_traits>
@@ -129,37 +130,52 @@ struct EnvSh {
 // The workgroup's env lives in one file-scope LDS object: the non-inlined substep function below
 // reaches it by symbol (LDS address space), not through a generic pointer.
 static __shared__ EnvSh g_E;
-// eight workgroups (envs) per CU share its 160 KiB of LDS: the occupancy the kernel is tuned for
+// ten workgroups (envs) per CU share its 160 KiB of LDS: the occupancy the kernel is tuned for (r05; with
+// 192 LDS rows, MMX_LDSEFC=192, eight)
+static_assert(MMX_LDSEFC != 128 || sizeof(EnvSh) <= 160 * 1024 / 10, "EnvSh no longer fits 10 envs per CU");
 static_assert(sizeof(EnvSh) <= 160 * 1024 / 8, "EnvSh no longer fits 8 envs per CU");
 
-// E.J is the phases' scratch outside the constraint build + Newton solve (rows are rebuilt every
-// substep): the collision layout below, the position stage's chain scan, the IK system, the RNE /
-// composite-inertia / actuator scratch of the dynamics (at COL_WORK) and the observation of the
-// step end.  The Newton Hessian staging tile and Cholesky transpose live in E.con instead
-// (contacts are dead once the rows exist; the last substep stores them to HBM first).
-#define COL_GX 0      // [NGEOM][GXS] world pose (x3, R9), rbound, type, -, -, box half extents (3), -
-#define GXS 20
-#define COL_CAND 944  // [COL_LIST] candidate pairs after the sphere test, then grouped by class
-#define COL_LIST 784
-#define COL_WORK (COL_CAND + COL_LIST)  // narrowphase work space: box-box polygons and (beside
-#define COL_POLY 49                     // them) the EPA polytope, then the contact sort (49: the quads'
-                                        // polygons start on different banks; 48 put quads 2 apart on one)
-// lanes that clip box-box polygons at a time (their polygons fill the rest of the LDS rows)
-#define COL_PLANES ((MMX_LDSEFC * 16 - COL_WORK) / COL_POLY < 32 ? (MMX_LDSEFC * 16 - COL_WORK) / COL_POLY : 32)
+// The scratch region: E.J, E.hdr, E.D and E.NC (contiguous in EnvSh) hold the phases' scratch outside
+// the constraint build + Newton solve (rows are rebuilt every substep): the collision layout below,
+// the position stage's chain scan, the IK system, the RNE / composite-inertia / actuator scratch of the
+// dynamics (at COL_WORK) and the observation of the step end.  The Newton Hessian staging tile and
+// Cholesky transpose live in E.con instead (contacts are dead once the rows exist; the last substep
+// stores them to HBM first).
+// r05: 128 LDS rows (MMX_LDSEFC) and this 2,400-float layout bring the env to 15,824 B of LDS, ten
+// per CU (was 20,432 B with 192 rows: eight); rows past 128 go to the HBM overflow block.
+#define GXS 17        // geom record: world pose (x 3, R 9), rbound, type, box half extents (3)
+#define GX_RB 12
+#define GX_TYPE 13
+#define GX_HALF 14
+#define COL_GX 0      // [NGEOM][GXS]
+#define COL_CAND ((MMX_NGEOM * GXS + 15) & ~15)  // [COL_LIST] candidate pairs after the sphere test, then by class
+#ifndef MMX_COL_LIST
+#define MMX_COL_LIST 320  // more survivors of the sphere test than this: the rest are dropped, SHF_CON_OVF
+#endif
+#define COL_LIST MMX_COL_LIST
+#define COL_WORK (COL_CAND + COL_LIST)  // narrowphase work space: box-box polygons, the EPA polytope
+#define COL_POLY 49                     // (GJK pass), then the contact sort (49: the quads' polygons
+                                        // start on different banks; 48 put quads 2 apart on one)
+#define COL_PLANES 16                   // box-box lane quads per pass: one polygon each
 #define COL_EPA COL_WORK
-static_assert(COL_EPA + EPA_SCRATCH_FLOATS <= MMX_LDSEFC * 16, "box-box polygons + EPA scratch exceed E.J");
-static_assert(COL_WORK + MMX_MAXCON * CON_F <= MMX_LDSEFC * 16, "contact sort exceeds E.J");
-static_assert(COL_PLANES >= 16 && COL_WORK + COL_PLANES * COL_POLY <= MMX_LDSEFC * 16, "box-box polygons exceed E.J");
-static_assert(MMX_NGEOM * GXS <= COL_CAND && MMX_NPAIR <= COL_LIST && MMX_NPAIR < 4096, "collision scratch layout");
+static_assert(offsetof(EnvSh, hdr) == offsetof(EnvSh, J) + sizeof(EnvSh::J) &&
+                  offsetof(EnvSh, D) == offsetof(EnvSh, hdr) + sizeof(EnvSh::hdr) &&
+                  offsetof(EnvSh, NC) == offsetof(EnvSh, D) + sizeof(EnvSh::D),
+              "the scratch region must be contiguous");
+#define SCR_FLOATS ((int)((offsetof(EnvSh, NC) + sizeof(EnvSh::NC) - offsetof(EnvSh, J)) / 4))
+static_assert(COL_EPA + EPA_SCRATCH_FLOATS <= SCR_FLOATS, "EPA scratch exceeds the scratch region");
+static_assert(COL_WORK + MMX_MAXCON * CON_F <= SCR_FLOATS, "contact sort exceeds the scratch region");
+static_assert(COL_WORK + COL_PLANES * COL_POLY <= SCR_FLOATS, "box-box polygons exceed the scratch region");
+static_assert(MMX_CAND_CAP <= COL_LIST && MMX_NPAIR < 4096, "collision scratch layout");
 
 #define SCR_DYN COL_WORK           // RNE frc + inertia [12][16], subtree force [12][6] (264), then:
 #define SCR_IC (SCR_DYN + 272)     // composite inertias [12][10]
 #define SCR_AF (SCR_IC + 120)      // actuator forces [8]
 #define SCR_BIAS (SCR_AF + 8)      // RNE bias force of the arm dofs [9]
-#define SCR_OBS 2816               // observation (step end, reset, forward)
-#define SCR_ACT 2912               // raw action of the step (lane 0, before the substeps)
-static_assert(SCR_BIAS + 9 <= 4096 && SCR_OBS + MMX_NOBS <= SCR_ACT && SCR_ACT + 12 <= MMX_LDSEFC * 16,
-              "E.J scratch layout");
+#define SCR_OBS COL_WORK           // observation (step end after its contact scan, reset, forward)
+#define SCR_ACT (COL_WORK + 96)    // raw action of the step (lane 0, before the substeps)
+static_assert(SCR_BIAS + 9 <= SCR_FLOATS && SCR_OBS + MMX_NOBS <= SCR_ACT && SCR_ACT + 12 <= SCR_FLOATS,
+              "scratch layout");
 static_assert(27 * 27 <= MMX_MAXCON * CON_F, "Newton Cholesky transpose exceeds E.con");
 DEV float* scr_of(EnvSh& E) { return reinterpret_cast<float*>(&E.J); }
 DEV const float* scr_of(const EnvSh& E) { return reinterpret_cast<const float*>(&E.J); }
@@ -771,13 +787,13 @@ struct WaveSink {
 
 DEV V3 geom_half(const float* gx, int g) {
   const float* o = gx + GXS * g;
-  return V3{o[16], o[17], o[18]};
+  return V3{o[GX_HALF], o[GX_HALF + 1], o[GX_HALF + 2]};
 }
 DEV Geom geom_lds(const float* gx, int g) {
   const float* o = gx + GXS * g;
   Geom G;
   G.g = g;
-  G.type = __float_as_int(o[13]);
+  G.type = __float_as_int(o[GX_TYPE]);
   G.x = V3{o[0], o[1], o[2]};
 #pragma unroll
   for (int k = 0; k < 9; k++) G.R.m[k] = o[3 + k];
@@ -849,11 +865,11 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
     o[0] = G.x.x; o[1] = G.x.y; o[2] = G.x.z;
 #pragma unroll
     for (int k = 0; k < 9; k++) o[3 + k] = G.R.m[k];
-    o[12] = MMX_geom_rbound[LANE];
-    o[13] = __int_as_float(G.type);
-    o[16] = MMX_geom_aabb[3 * LANE];  // bounding-box half extents in the geom frame (= size for boxes)
-    o[17] = MMX_geom_aabb[3 * LANE + 1];
-    o[18] = MMX_geom_aabb[3 * LANE + 2];
+    o[GX_RB] = MMX_geom_rbound[LANE];
+    o[GX_TYPE] = __int_as_float(G.type);
+    o[GX_HALF] = MMX_geom_aabb[3 * LANE];  // bounding-box half extents in the geom frame (= size for boxes)
+    o[GX_HALF + 1] = MMX_geom_aabb[3 * LANE + 1];
+    o[GX_HALF + 2] = MMX_geom_aabb[3 * LANE + 2];
   }
   if (rebuild) {  // uniform: the moving geoms' extent about their body origins (rigid: any pose)
     float ext = 0.f;
@@ -874,8 +890,8 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
     const float* o1 = gx + GXS * g1;
     const float* o2 = gx + GXS * g2;
     const V3 d = V3{o2[0] - o1[0], o2[1] - o1[1], o2[2] - o1[2]};
-    if (__float_as_int(o1[13]) == GT_PLANE) return d.x * o1[5] + d.y * o1[8] + d.z * o1[11] <= o2[12] + infl;
-    const float rb = o1[12] + o2[12] + infl;
+    if (__float_as_int(o1[GX_TYPE]) == GT_PLANE) return d.x * o1[5] + d.y * o1[8] + d.z * o1[11] <= o2[GX_RB] + infl;
+    const float rb = o1[GX_RB] + o2[GX_RB] + infl;
     return dot(d, d) <= rb * rb;
   };
   int nc = 0;
@@ -920,7 +936,7 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
     const unsigned long long m = km[q];
     if ((m >> LANE) & 1ull) {
       const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-      cand[nc + pos] = cand_pack(q * WG + LANE, pg[q]);
+      if (nc + pos < COL_LIST) cand[nc + pos] = cand_pack(q * WG + LANE, pg[q]);
     }
     nc += __popcll(m);
     if (rebuild) {  // the inflated set -> the persistent list (pair order)
@@ -933,6 +949,10 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
   if (rebuild && LANE == 0) {
     E.ncand = ni <= MMX_CAND_CAP ? ni : -1;
     E.cdisp = 0.f;
+  }
+  if (nc > COL_LIST) {  // uniform: more sphere-test survivors than the list holds (flagged; none in C3)
+    if (LANE == 0) E.flags |= SHF_CON_OVF;
+    nc = COL_LIST;
   }
   }
   SYNC();
@@ -1650,9 +1670,15 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
 // (g = M (x - xs) + sum B' C r; B' C_old r_new = B' C_old r_old + a B' C_old B p).  E.D / E.NC /
 // slot 15 hold dC_kk, dC_nk and dC r_new (newton_wave's weight pass in delta mode); gm[q] bit 4m
 // marks group m of row slice q as changed (wave-uniform).  Only the changed groups' MFMA steps run,
-// and only the row types holding one are staged and gathered.  LDS rows only (the caller runs the
-// full pass when rows spill to HBM).  Adds into hrow; returns sum B' dC r in lane j < 27.
+// and only the row types holding one are staged and gathered, LDS and (MMX_DELTA_OVF) HBM overflow rows
+// alike.  Adds into hrow; returns sum B' dC r in lane j < 27.
 #define HESS_LQ (MMX_LDSEFC / WG)  // row slices held in LDS
+// incremental Hessian also over the HBM overflow rows (r05: with 128 LDS rows the grasp phases' rows
+// spill; 0 = the full pass whenever rows spill, as with 192 rows in r02-r04)
+#ifndef MMX_DELTA_OVF
+#define MMX_DELTA_OVF 1
+#endif
+#define HESS_NQ (MMX_DELTA_OVF ? RPL : HESS_LQ)  // row slices the delta pass covers
 DEV float hess_grad_delta(EnvSh& E, float* hrow, const unsigned long long* gm) {
   float* G = lrow_of(E);
   const int col = LANE & 15, rk = LANE >> 4;
@@ -1678,19 +1704,28 @@ DEV float hess_grad_delta(EnvSh& E, float* hrow, const unsigned long long* gm) {
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     bool any = false;
 #pragma unroll
-    for (int q = 0; q < HESS_LQ; q++) {
+    for (int q = 0; q < HESS_NQ; q++) {
       if (64 * q >= r1 || 64 * (q + 1) <= r0) continue;  // uniform
       const int lo = max(r0 - 64 * q, 0), hi = min(r1 - 64 * q, 64);
       unsigned long long m = gm[q] & (hi >= 64 ? ~0ull : ((1ull << hi) - 1ull)) & (~0ull << lo);
+      if (q >= HESS_LQ && m) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the HBM rows' stores
       while (m) {  // uniform: the type's changed groups, one MFMA step each
         const int g0 = 64 * q + __builtin_ctzll(m);
         m &= m - 1ull;
         any = true;
-        const float4 n4 = *reinterpret_cast<const float4*>(&E.NC[g0]);
-        float jg[4];
+        float4 n4;
+        float jg[4], dr;
+        if (q < HESS_LQ) {  // (static per unrolled slice: LDS or HBM rows)
+          n4 = *reinterpret_cast<const float4*>(&E.NC[g0]);
 #pragma unroll
-        for (int mm = 0; mm < 4; mm++) jg[mm] = jlds(E, g0 + mm, col);  // slot 15 holds dC r
-        const float dr = E.D[g0 + rk];
+          for (int mm = 0; mm < 4; mm++) jg[mm] = jlds(E, g0 + mm, col);  // slot 15 holds dC r
+          dr = E.D[g0 + rk];
+        } else {
+          n4 = make_float4(*ovf_nc(E, g0), *ovf_nc(E, g0 + 1), *ovf_nc(E, g0 + 2), *ovf_nc(E, g0 + 3));
+#pragma unroll
+          for (int mm = 0; mm < 4; mm++) jg[mm] = ovf_j(E, g0 + mm)[col];
+          dr = *ovf_d(E, g0 + rk);
+        }
         const float own = fmaf(m_[0], jg[0], fmaf(m_[1], jg[1], fmaf(m_[2], jg[2], m_[3] * jg[3])));
         const float ncr = fmaf(m_[1], n4.y, fmaf(m_[2], n4.z, m_[3] * n4.w));
         const float s123 = fmaf(n4.y, jg[1], fmaf(n4.z, jg[2], n4.w * jg[3]));
@@ -1991,10 +2026,10 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid, int& exit) 
     // collects its edges' normal parts over the DPP quad.  Delta mode: the same with the change
     // of each edge's weight (+-D where its active state flipped, else 0), and a mask of the
     // groups holding a flipped edge.
-    const bool delta = it > 0 && nefc <= MMX_LDSEFC;  // uniform
-    unsigned long long gm[HESS_LQ];
+    const bool delta = it > 0 && (MMX_DELTA_OVF || nefc <= MMX_LDSEFC);  // uniform
+    unsigned long long gm[HESS_NQ];
 #pragma unroll
-    for (int q = 0; q < HESS_LQ; q++) gm[q] = 0ull;
+    for (int q = 0; q < HESS_NQ; q++) gm[q] = 0ull;
 #pragma unroll
     for (int q = 0; q < RPL; q++) {
       if (WG * q >= nefc) break;  // uniform: no rows past this slice
@@ -2009,9 +2044,9 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid, int& exit) 
       if (delta) {
         w0 = on0 == was0 ? 0.f : (on0 ? dd[q] : -dd[q]);
         w1 = on1 == was1 ? 0.f : (on1 ? dd[q] : -dd[q]);
-        if (q < HESS_LQ) {
+        if (q < HESS_NQ) {
           const unsigned long long bm = __ballot(w0 != 0.f || w1 != 0.f);
-          gm[q < HESS_LQ ? q : 0] = (bm | (bm >> 1) | (bm >> 2) | (bm >> 3)) & 0x1111111111111111ull;
+          gm[q < HESS_NQ ? q : 0] = (bm | (bm >> 1) | (bm >> 2) | (bm >> 3)) & 0x1111111111111111ull;
         }
       }
       const float ckk = fmaf(w0 * ec.b0, ec.b0, w1 * ec.b1 * ec.b1);
@@ -3045,7 +3080,7 @@ extern "C" int mmx_fsm_profile_fields() { return FSMP_N; }
 // waves per SIMD the step kernel's register allocation is made for (2: <= 256 VGPRs; the A/B build
 // MMX_STEP_WAVES=3 caps it at 168)
 #ifndef MMX_STEP_WAVES
-#define MMX_STEP_WAVES 2
+#define MMX_STEP_WAVES (MMX_LDSEFC == 128 ? 3 : 2)
 #endif
 extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MMX_STEP_WAVES, MMX_STEP_WAVES)))
 mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert, int base, int nsteps) {

@@ -17,9 +17,10 @@
 // constraint rows (basis rows: 4 per contact + equality / limits padded to 4; <= 64 x 4 + 20)
 #define MMX_MAXEFC 320
 // constraint rows [0, MMX_LDSEFC) live in the workgroup's LDS, rows [MMX_LDSEFC, MMX_MAXEFC) in the
-// env's HBM overflow block (efc_ovf); 192 rows keep the env's LDS under 20 KB (8 envs per CU)
+// env's HBM overflow block (efc_ovf); 128 rows keep the env's LDS under 16 KB (10 envs per CU; r01-r04:
+// 192 rows, 20 KB, 8 per CU)
 #ifndef MMX_LDSEFC
-#define MMX_LDSEFC 192
+#define MMX_LDSEFC 128
 #endif
 #define MMX_OVFEFC (MMX_MAXEFC - MMX_LDSEFC)
 #define MMX_OVF_F (MMX_OVFEFC * 18)  // floats per env: J rows [OVFEFC][16], then D, NC [OVFEFC]

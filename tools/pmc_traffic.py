@@ -83,7 +83,9 @@ def main():
     if os.path.isdir(lanes_dir):
         ln = timed_mean(per_dispatch(lanes_dir, ["SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU"]), n_timed)
         lane_util = ln["SQ_THREAD_CYCLES_VALU"] / max(64.0 * ln["SQ_ACTIVE_INST_VALU"], 1.0)
-    waves_per_simd = 2  # 8 one-wave workgroups per CU (LDS- and VGPR-bound), 4 SIMDs
+    # resident one-wave workgroups per CU / 4 SIMDs: 10 per CU since r05 (15,824 B of LDS per env,
+    # 168 VGPRs: 3 waves on two SIMDs, 2 on the others), 8 per CU before (MMX_LDSEFC=192)
+    waves_per_simd = float(os.environ.get("MMX_ENVS_PER_CU", "10")) / 4.0
     per_wave = sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_WAVE_CYCLES"]
     hbm = 2.0 * fetch * 1024.0 + write * 1024.0
     rec = {
