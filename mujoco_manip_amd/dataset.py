@@ -628,7 +628,11 @@ class LeRobotWriter:
         self.chunk, self.fileno, self.start = 0, 0, 0
         self.writer, self.cur_bytes = None, 0  # the open data file (its path) and its bytes so far
         self.limit = data_files_size_in_mb * 1024 * 1024
-        self.num_acc = {}  # feature -> [min, max, sum, sumsq, count]
+        # numeric features' running [min, max, sum, sumsq, count] over the concatenation of their
+        # dims (num_keys order, _num_dims each): one set of vector ops per episode, split per feature
+        # at close (elementwise, so bit-identical to per-feature accumulators)
+        self._num_dims = [int(np.prod(features[k]["shape"])) for k in self.num_keys]
+        self.num_acc = None
         self.img_acc = {}  # feature -> [min, max, sum, sumsq, pixels, frames]
         self.n_episodes = 0
         # seconds spent per part of the writer (diagnostics, tools/dataset_bench.py): episode
@@ -733,9 +737,7 @@ class LeRobotWriter:
 
     def _episode_bytes(self, ep):
         """An episode's size in the data file (the roll-over test): its column data."""
-        n = 0
-        for k in self.num_keys:
-            n += 4 * ep.length * int(np.prod(self.features[k]["shape"]))
+        n = 4 * ep.length * sum(self._num_dims)
         for k in self.str_keys:
             n += sum(map(len, ep.frames[k])) + 4 * ep.length
         for k in self.img_keys:
@@ -807,24 +809,24 @@ class LeRobotWriter:
                "dataset_to_index": self.start + ep.length, "meta/episodes/chunk_index": 0,
                "meta/episodes/file_index": 0}
         if self.num_keys:  # every numeric feature's statistics from one [length, sum of dims] array
-            xs = [np.asarray(ep.frames[k], np.float64).reshape(ep.length, -1) for k in self.num_keys]
-            X = np.concatenate(xs, axis=1)
+            L = ep.length
+            X = np.concatenate([np.asarray(ep.frames[k], np.float64).reshape(L, -1) for k in self.num_keys], axis=1)
             mn, mx, sm = X.min(0), X.max(0), X.sum(0)
-            mean = sm / ep.length
+            mean = sm / L
             d = X - mean
-            std = np.sqrt((d * d).sum(0) / ep.length)  # np.std's two-pass form
+            std = np.sqrt((d * d).sum(0) / L)  # np.std's two-pass form
             sq = (X * X).sum(0)
+            # one list conversion per statistic, then python slices per feature
+            lmn, lmx, lmean, lstd = mn.tolist(), mx.tolist(), mean.tolist(), std.tolist()
             o = 0
-            for k, x in zip(self.num_keys, xs):
-                sl = slice(o, o + x.shape[1])
-                o += x.shape[1]
-                row[f"stats/{k}/min"], row[f"stats/{k}/max"] = mn[sl].tolist(), mx[sl].tolist()
-                row[f"stats/{k}/mean"], row[f"stats/{k}/std"] = mean[sl].tolist(), std[sl].tolist()
-                row[f"stats/{k}/count"] = [int(ep.length)]
-                acc = self.num_acc.get(k)
-                self.num_acc[k] = [mn[sl], mx[sl], sm[sl], sq[sl], ep.length] if acc is None else \
-                    [np.minimum(acc[0], mn[sl]), np.maximum(acc[1], mx[sl]), acc[2] + sm[sl], acc[3] + sq[sl],
-                     acc[4] + ep.length]
+            for k, n in zip(self.num_keys, self._num_dims):
+                row[f"stats/{k}/min"], row[f"stats/{k}/max"] = lmn[o:o + n], lmx[o:o + n]
+                row[f"stats/{k}/mean"], row[f"stats/{k}/std"] = lmean[o:o + n], lstd[o:o + n]
+                row[f"stats/{k}/count"] = [int(L)]
+                o += n
+            acc = self.num_acc
+            self.num_acc = [mn, mx, sm, sq, L] if acc is None else \
+                [np.minimum(acc[0], mn), np.maximum(acc[1], mx), acc[2] + sm, acc[3] + sq, acc[4] + L]
         for k in self.img_keys:
             st = (getattr(ep, "image_stats", None) or {}).get(k)
             if st is None:  # episodes built elsewhere: decode a frame sample
@@ -925,7 +927,10 @@ class LeRobotWriter:
         pq.write_table(pa.table({"task_index": pa.array(np.arange(len(self.tasks), dtype=np.int64)),
                                  "task": pa.array(self.tasks, pa.string())}), os.path.join(meta, "tasks.parquet"))
         stats = {}
-        for k, (mn, mx, sm, sq, n) in self.num_acc.items():
+        o = 0
+        for k, nd in zip(self.num_keys, self._num_dims) if self.num_acc is not None else ():
+            mn, mx, sm, sq, n = [a[o:o + nd] for a in self.num_acc[:4]] + [self.num_acc[4]]
+            o += nd
             mean = sm / n
             stats[k] = {"min": mn.tolist(), "max": mx.tolist(), "mean": mean.tolist(),
                         "std": np.sqrt(np.maximum(sq / n - mean * mean, 0.0)).tolist(), "count": [int(n)]}

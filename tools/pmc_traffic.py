@@ -48,6 +48,32 @@ def timed_mean(rows: list[dict], n_last: int) -> dict:
     return {k: sum(r.get(k, 0.0) for r in rows) / len(rows) for k in rows[0]}
 
 
+EXT_A = ["SQ_WAVE_CYCLES", "SQ_WAVES", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_SMEM", "SQ_INSTS_BRANCH",
+         "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"]
+EXT_B = ["SQ_WAVE_CYCLES", "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_MISC", "SQ_INST_CYCLES_SALU", "SQ_WAIT_INST_LDS",
+         "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_ACTIVE_INST_VALU"]
+
+
+def extended_sq(prof: str, n_timed: int, config: dict, rnd: str) -> dict | None:
+    """The two extended SQ passes (profile.sh sqx_a / sqx_b) per dispatch and per wave quad-cycle
+    (each counter over its own pass's SQ_WAVE_CYCLES); None when the passes are missing."""
+    da, db = os.path.join(prof, "sqx_a"), os.path.join(prof, "sqx_b")
+    if not (os.path.isdir(da) and os.path.isdir(db)):
+        return None
+    a = timed_mean(per_dispatch(da, EXT_A), n_timed)
+    b = timed_mean(per_dispatch(db, EXT_B), n_timed)
+    per = dict(a)
+    per.update({k: v for k, v in b.items() if k != "SQ_WAVE_CYCLES"})
+    norm = {k: round(v / a["SQ_WAVE_CYCLES"], 4) for k, v in a.items()}
+    norm.update({k: round(v / b["SQ_WAVE_CYCLES"], 4) for k, v in b.items() if k != "SQ_WAVE_CYCLES"})
+    return {"kernel": KERNEL, "round": rnd, "config": config, "timed_dispatches": n_timed,
+            "per_dispatch": per, "per_wave_quad_cycle": norm,
+            "reading": (f"per wave and quad-cycle: any instruction issued {norm['SQ_ACTIVE_INST_ANY']:.2f} (VALU "
+                        f"{norm['SQ_ACTIVE_INST_VALU']:.2f}, SALU {norm['SQ_INSTS_SALU']:.2f}, LDS "
+                        f"{norm['SQ_INSTS_LDS']:.3f}, branch {norm['SQ_INSTS_BRANCH']:.3f}); a wave can issue ~0.94 VALU "
+                        "per quad-cycle (profiles/r05_valu_issue_calibration.json)")}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--round", default="r03")
@@ -83,9 +109,11 @@ def main():
     if os.path.isdir(lanes_dir):
         ln = timed_mean(per_dispatch(lanes_dir, ["SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU"]), n_timed)
         lane_util = ln["SQ_THREAD_CYCLES_VALU"] / max(64.0 * ln["SQ_ACTIVE_INST_VALU"], 1.0)
-    # resident one-wave workgroups per CU / 4 SIMDs: 10 per CU since r05 (15,824 B of LDS per env,
-    # 168 VGPRs: 3 waves on two SIMDs, 2 on the others), 8 per CU before (MMX_LDSEFC=192)
-    waves_per_simd = float(os.environ.get("MMX_ENVS_PER_CU", "10")) / 4.0
+    # resident one-wave workgroups (envs) per SIMD: at most 10 per CU since r05 (15,824 B of LDS per
+    # env, 168 VGPRs), 8 per CU before (MMX_LDSEFC=192); fewer when the configuration has fewer envs
+    # than the 256 CUs hold (C2: 1024)
+    per_cu = float(os.environ.get("MMX_ENVS_PER_CU", "10"))
+    waves_per_simd = min(per_cu * 256.0, float(line["config"]["envs_per_gpu"])) / 1024.0
     per_wave = sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_WAVE_CYCLES"]
     hbm = 2.0 * fetch * 1024.0 + write * 1024.0
     rec = {
@@ -112,6 +140,9 @@ def main():
     }
     if rec["config"]["workload"] not in ("c2", "c3", "c5"):
         rec["config"]["workload"] = a.workload
+    ext = extended_sq(a.prof, n_timed, rec["config"], a.round)
+    if ext:
+        json.dump(ext, open(os.path.join(dst, f"{tag}_sq_extended.json"), "w"), indent=1)
     json.dump(rec, open(os.path.join(dst, f"pmc_{a.workload}.json"), "w"), indent=1)
     json.dump(rec, open(os.path.join(dst, f"{tag}_pmc.json"), "w"), indent=1)
     print(json.dumps({k: rec[k] for k in ("hbm_bytes_per_env_step", "valu")}))

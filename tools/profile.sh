@@ -27,5 +27,12 @@ timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAVES SQ_BUSY_CYCLES SQ_AC
 # lane utilisation: thread-cycles of VALU work / (VALU instruction cycles x 64 lanes)
 timeout -s KILL 300 rocprofv3 --pmc SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU --output-format csv -d $OUT/lanes -o run -- \
   python3 $ROOT/bench.py $ARGS > $OUT/bench_lanes.log 2>&1
+# extended SQ passes: any-instruction issue, SALU / LDS / branch / memory instruction mix per wave
+timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAVES SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH \
+  SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY --output-format csv -d $OUT/sqx_a -o run -- \
+  python3 $ROOT/bench.py $ARGS > $OUT/bench_sqx_a.log 2>&1
+timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_SALU \
+  SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU --output-format csv -d $OUT/sqx_b -o run -- \
+  python3 $ROOT/bench.py $ARGS > $OUT/bench_sqx_b.log 2>&1
 cd $ROOT
 python3 tools/pmc_traffic.py --round $ROUND --workload $WL --prof $OUT --timed-steps $STEPS
