@@ -119,6 +119,22 @@ int mmx_reset(mmx_sim* sim, const uint64_t* seeds, const uint8_t* seed_given, co
  * fp32 (row-major, env-major).  Runs decode -> 16 x (IK + mj_step) -> mj_forward -> reward -> obs. */
 int mmx_step(mmx_sim* sim, const float* action_dev, int32_t action_dim);
 
+/* Host helper of the dataset path (dataset.py collect_episodes, generate_dataset.py:250-260's
+ * per-frame PNG files): copies n byte ranges (src[k] = host address, len[k] bytes) back to back into
+ * dst; returns the bytes copied, -1 on bad arguments.  One call per episode and camera assembles the
+ * episode's PNG files from the per-step packed buffers without a Python object per frame (ctypes
+ * releases the GIL for the call). */
+int64_t mmx_gather_bytes(int64_t n, const uint64_t* src, const int64_t* len, uint8_t* dst);
+
+/* Constraint rows the env-step kernel (mmx_step, mmx_rollout_expert) keeps in LDS: 128 (ten envs
+ * per CU: the fastest layout when the step kernel alone fills the GPU, C3) or 192 (eight per CU:
+ * faster with cameras, C5, and with fewer envs than the GPU's workgroup slots, C2).  Default 192
+ * with cameras, 128 without; env MMX_STEP_ROWS overrides at create.  The rows past the LDS ones live
+ * in the env's HBM overflow block; results agree within fp32 rounding (the parity tests run both).
+ * MMX_EINVAL for any other value.  (No reference counterpart: a layout choice of this port.) */
+int mmx_set_step_rows(mmx_sim* sim, int32_t rows);
+int mmx_step_rows(const mmx_sim* sim);
+
 /* PickAndPlaceTask.plan(n_steps) (pick_and_place.py:167-277) for every env; writes the
  * abs_pos action [N][4] = (target_xyz, gripper_val) to action_dev_out (may be NULL). */
 int mmx_expert_plan(mmx_sim* sim, int32_t n_steps, float* action_dev_out);

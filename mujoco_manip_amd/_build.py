@@ -14,8 +14,8 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libmmx.so")
 LIB_PROF = os.path.join(PKG, "libmmx_prof.so")
-SOURCES = ["mmx_kernels.hip", "mmx_render.hip", "mmx_png.hip", "mmx_api.cpp"]
-HEADERS = ["mmx_model_gen.h", "mmx_render_gen.h", "mmx_state.h", "mmx_device.h", "mmx_geom.h", "mmx_clock.h",
+SOURCES = ["mmx_kernels.hip", "mmx_step_l192.hip", "mmx_render.hip", "mmx_png.hip", "mmx_api.cpp"]
+HEADERS = ["mmx_kernels.hip", "mmx_model_gen.h", "mmx_render_gen.h", "mmx_state.h", "mmx_device.h", "mmx_geom.h", "mmx_clock.h",
            os.path.join("..", "..", "include", "mmx_api.h")]
 ARCH = os.environ.get("MMX_OFFLOAD_ARCH", "gfx950")
 # device-code math: x / y as x * rcp(y) and sqrt without the denormal-scaling wrapper (v_rcp_f32 /
@@ -46,7 +46,8 @@ FLAGS = DEVICE_MATH + DEVICE_SCHED + DEVICE_NOSLP + os.environ.get("MMX_EXTRA_FL
 # (-fassociative-math; explicit fmaf / DPP / readlane reductions keep their written order), -2 %
 # VALU instructions per env step, C3 +0.9 % in the interleaved A/B (profiles/r04_ab_assoc.json),
 # GPU suite unchanged.  Not the renderer, whose shared-edge functions rely on one evaluation order.
-SOURCE_FLAGS = {"mmx_kernels.hip": ["-Xarch_device", "-fassociative-math"]}
+SOURCE_FLAGS = {"mmx_kernels.hip": ["-Xarch_device", "-fassociative-math"],
+                "mmx_step_l192.hip": ["-Xarch_device", "-fassociative-math"]}
 
 
 def lib_path(profile: bool = False) -> str:

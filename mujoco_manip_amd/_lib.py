@@ -58,7 +58,7 @@ EXPORTED = ("mmx_config_default", "mmx_create", "mmx_destroy", "mmx_last_error",
             "mmx_synchronize", "mmx_get_state", "mmx_set_state", "mmx_episode_seed", "mmx_rollout_lanes",
             "mmx_rollout_steps_per_launch", "mmx_rollout_launches", "mmx_expert_physics", "mmx_eval_reward", "mmx_kernel_timing",
             "mmx_kernel_times", "mmx_png_bound", "mmx_png_scratch", "mmx_png_encode", "mmx_png_pack", "mmx_image_stats",
-            "mmx_queue_init", "mmx_queue_advance")
+            "mmx_queue_init", "mmx_queue_advance", "mmx_set_step_rows", "mmx_step_rows", "mmx_gather_bytes")
 
 _lib = None
 
@@ -89,6 +89,11 @@ def load(build_if_missing: bool = True):
     L.mmx_physics_step.argtypes = [vp, C.c_int32, C.c_int32]
     L.mmx_rollout_lanes.argtypes = [vp]
     L.mmx_rollout_lanes.restype = C.c_int
+    L.mmx_gather_bytes.argtypes = [C.c_int64, vp, vp, vp]
+    L.mmx_gather_bytes.restype = C.c_int64
+    L.mmx_set_step_rows.argtypes = [vp, C.c_int32]
+    L.mmx_step_rows.argtypes = [vp]
+    L.mmx_step_rows.restype = C.c_int
     L.mmx_rollout_steps_per_launch.argtypes = [vp]
     L.mmx_rollout_steps_per_launch.restype = C.c_int
     L.mmx_rollout_launches.argtypes = [vp, C.c_int32]
@@ -116,7 +121,7 @@ def load(build_if_missing: bool = True):
     for name in ("mmx_create", "mmx_reset", "mmx_step", "mmx_expert_plan", "mmx_rollout_expert", "mmx_physics_step",
                  "mmx_forward", "mmx_get_buffers", "mmx_synchronize", "mmx_get_state", "mmx_set_state",
                  "mmx_expert_physics", "mmx_eval_reward", "mmx_kernel_timing", "mmx_kernel_times", "mmx_png_encode",
-                 "mmx_png_pack", "mmx_image_stats", "mmx_queue_init", "mmx_queue_advance"):
+                 "mmx_png_pack", "mmx_image_stats", "mmx_queue_init", "mmx_queue_advance", "mmx_set_step_rows"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L
@@ -383,6 +388,15 @@ class Sim:
     @property
     def rollout_lanes(self) -> int:
         return int(self.L.mmx_rollout_lanes(self.ptr))
+
+    @property
+    def step_rows(self) -> int:
+        """Constraint rows the env-step kernel keeps in LDS (128: ten envs per CU; 192: eight)."""
+        return int(self.L.mmx_step_rows(self.ptr))
+
+    @step_rows.setter
+    def step_rows(self, rows: int):
+        self._check(self.L.mmx_set_step_rows(self.ptr, int(rows)), "mmx_set_step_rows")
 
     @property
     def rollout_steps_per_launch(self) -> int:

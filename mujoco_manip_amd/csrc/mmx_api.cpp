@@ -19,6 +19,8 @@
 extern "C" hipError_t mmx_launch_reset(const MMXState* S, const unsigned char* mask, const int* task, hipStream_t st);
 extern "C" hipError_t mmx_launch_step(const MMXState* S, const float* action, int adim, int expert_autoreset,
                                       int base, int count, int nsteps, hipStream_t st);
+extern "C" hipError_t mmx_launch_step_l192(const MMXState* S, const float* action, int adim, int expert_autoreset,
+                                           int base, int count, int nsteps, hipStream_t st);
 extern "C" hipError_t mmx_launch_expert(const MMXState* S, int n, float* action, hipStream_t st);
 extern "C" hipError_t mmx_launch_physics(const MMXState* S, int n, int with_ik, hipStream_t st);
 extern "C" hipError_t mmx_launch_forward(const MMXState* S, hipStream_t st);
@@ -57,6 +59,9 @@ struct mmx_sim {
   int nlanes = 1;
   // env steps per mmx_env_step_kernel launch in expert rollouts without cameras (MMX_FUSE overrides)
   int fuse = 16;
+  // constraint rows the env-step kernel keeps in LDS: 128 (ten envs per CU) or 192 (eight per CU,
+  // mmx_step_l192.hip); by default 192 with cameras, 128 without (mmx_set_step_rows, MMX_STEP_ROWS)
+  int step_rows = 128;
   hipStream_t lane[kMaxLanes] = {};
   hipEvent_t ev_fork = nullptr, ev_join[kMaxLanes] = {};
   // per-launch kernel timing (mmx_kernel_timing): an event pair around every step / render launch
@@ -330,6 +335,11 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
   int lanes = std::min(N / 1024, 4);
   if (const char* v = std::getenv("MMX_STREAMS")) lanes = std::atoi(v);
   if (const char* v = std::getenv("MMX_FUSE")) sim->fuse = std::max(1, std::atoi(v));
+  sim->step_rows = cfg->image_size > 0 ? 192 : 128;
+  if (const char* v = std::getenv("MMX_STEP_ROWS")) {
+    const int r = std::atoi(v);
+    if (r == 128 || r == 192) sim->step_rows = r;
+  }
   lanes = std::max(1, std::min(lanes, std::min(N, int(mmx_sim::kMaxLanes))));
   if (hipEventCreateWithFlags(&sim->ev_fork, hipEventDisableTiming) != hipSuccess) lanes = 1;
   for (int l = 1; l < lanes; l++)
@@ -419,12 +429,27 @@ int mmx_reset(mmx_sim* sim, const uint64_t* seeds, const uint8_t* seed_given, co
   return hip_check(sim, hipStreamSynchronize(sim->stream), "mmx_reset sync");
 }
 
+namespace {
+static hipError_t launch_step(const mmx_sim* sim, const float* action, int adim, int expert, int base, int count, int nsteps,
+                       hipStream_t st) {
+  return sim->step_rows == 192 ? mmx_launch_step_l192(&sim->S, action, adim, expert, base, count, nsteps, st)
+                               : mmx_launch_step(&sim->S, action, adim, expert, base, count, nsteps, st);
+}
+}  // namespace
+
+int mmx_set_step_rows(mmx_sim* sim, int32_t rows) {
+  if (!sim || (rows != 128 && rows != 192)) return MMX_EINVAL;
+  sim->step_rows = rows;
+  return MMX_OK;
+}
+int mmx_step_rows(const mmx_sim* sim) { return sim ? sim->step_rows : 0; }
+
 int mmx_step(mmx_sim* sim, const float* action_dev, int32_t action_dim) {
   if (!sim || !action_dev) return MMX_EINVAL;
   DeviceGuard guard(sim);
   static const int kDim[5] = {4, 8, 10, 8, 10};
   if (action_dim < kDim[sim->S.action_mode]) return fail(sim, MMX_EINVAL, "action_dim too small for action_mode");
-  hipError_t e = mmx_launch_step(&sim->S, action_dev, action_dim, 0, 0, sim->S.N, 1, sim->stream);
+  hipError_t e = launch_step(sim, action_dev, action_dim, 0, 0, sim->S.N, 1, sim->stream);
   if (e == hipSuccess) e = mmx_launch_render(&sim->S, 0, sim->S.N, sim->stream);
   return hip_check(sim, e, "mmx_step");
 }
@@ -517,7 +542,7 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
       const int b0 = (int)((long)N * l / L), b1 = (int)((long)N * (l + 1) / L);
       hipStream_t st = l ? sim->lane[l] : sim->stream;
       e = timed(sim, st, sim->t_step,
-                [&] { return mmx_launch_step(&sim->S, sim->expert_action, 4, 1, b0, b1 - b0, ns, st); });
+                [&] { return launch_step(sim, sim->expert_action, 4, 1, b0, b1 - b0, ns, st); });
       if (e == hipSuccess && sim->S.image_size > 0)
         e = timed(sim, st, sim->t_render, [&] { return mmx_launch_render(&sim->S, b0, b1 - b0, st); });
     }
@@ -571,6 +596,17 @@ int mmx_image_stats(mmx_sim* sim, const uint8_t* rgb_dev, int64_t img_stride, in
   DeviceGuard guard(sim);
   return hip_check(sim, mmx_launch_image_stats(rgb_dev, img_stride, n, (int64_t)width * height, out_dev, sim->stream),
                    "mmx_image_stats");
+}
+
+int64_t mmx_gather_bytes(int64_t n, const uint64_t* src, const int64_t* len, uint8_t* dst) {
+  if (n < 0 || (n > 0 && (!src || !len || !dst))) return -1;
+  int64_t o = 0;
+  for (int64_t k = 0; k < n; k++) {
+    if (len[k] < 0) return -1;
+    if (len[k]) std::memcpy(dst + o, reinterpret_cast<const void*>(static_cast<uintptr_t>(src[k])), (size_t)len[k]);
+    o += len[k];
+  }
+  return o;
 }
 
 int mmx_rollout_steps_per_launch(const mmx_sim* sim) {

@@ -2980,6 +2980,10 @@ DEV void step_end(const MMXState& S, int i, EnvSh& E) {
   store_obs(S, i, E);
 }
 
+// The env-step kernel is built twice (mmx_step_l192.hip): MMX_STEP_ONLY compiles only it and its
+// launcher, under names with the MMX_STEP_SUFFIX suffix; every other kernel comes from this file's
+// own build.
+#ifndef MMX_STEP_ONLY
 extern "C" __global__ void __launch_bounds__(WG) mmx_substep_kernel(MMXState S, const float* action, int adim, int mode) {
   EnvSh& E = g_E;
   float* act = scr_of(E) + SCR_ACT;  // lane 0's decoded action (E.J is free before the substeps)
@@ -3014,6 +3018,8 @@ extern "C" __global__ void __launch_bounds__(WG) mmx_substep_kernel(MMXState S, 
   }
   store_env(S, i, E);
 }
+
+#endif  // MMX_STEP_ONLY
 
 // One substep = IK + mj_step, kept out of line: nothing is hoisted across the 16 iterations of
 // the env-step loop (hoisted invariants would pin registers for the whole kernel and serialise
@@ -3065,6 +3071,9 @@ __device__ __attribute__((noinline)) void step_finish(const MMXState& S, int i) 
 // (tools/gpu_probe.py fsm_profile).  Lane 0 of each env adds with global atomics.
 enum { FSMP_PHASES = STAT_T_AUX3 - STAT_T_IK + 1, FSMP_STEP = FSMP_PHASES, FSMP_ITER, FSMP_NEFC, FSMP_NCON,
        FSMP_COUNT, FSMP_N };
+#ifdef MMX_STEP_ONLY
+static __device__ double g_fsm_prof[11 * FSMP_N];  // (this build's copy is not read out)
+#else
 __device__ double g_fsm_prof[11 * FSMP_N];
 extern "C" hipError_t mmx_fsm_profile(double* out, int reset) {
   hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_fsm_prof), sizeof(g_fsm_prof));
@@ -3075,6 +3084,7 @@ extern "C" hipError_t mmx_fsm_profile(double* out, int reset) {
   return e;
 }
 extern "C" int mmx_fsm_profile_fields() { return FSMP_N; }
+#endif  // MMX_STEP_ONLY
 #endif
 
 // waves per SIMD the step kernel's register allocation is made for (2: <= 256 VGPRs; the A/B build
@@ -3082,8 +3092,14 @@ extern "C" int mmx_fsm_profile_fields() { return FSMP_N; }
 #ifndef MMX_STEP_WAVES
 #define MMX_STEP_WAVES (MMX_LDSEFC == 128 ? 3 : 2)
 #endif
+#ifndef MMX_STEP_SUFFIX
+#define MMX_STEP_SUFFIX
+#endif
+#define MMX_CAT2_(a, b) a##b
+#define MMX_CAT_(a, b) MMX_CAT2_(a, b)
+#define MMX_STEP_SYM(name) MMX_CAT_(name, MMX_STEP_SUFFIX)
 extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MMX_STEP_WAVES, MMX_STEP_WAVES)))
-mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert, int base, int nsteps) {
+MMX_STEP_SYM(mmx_env_step_kernel)(MMXState S, const float* action, int adim, int expert, int base, int nsteps) {
   const int i = base + blockIdx.x;
   if (i >= S.N) return;
   for (int k = 0; k < nsteps; k++) {
@@ -3128,6 +3144,7 @@ mmx_env_step_kernel(MMXState S, const float* action, int adim, int expert, int b
   }
 }
 
+#ifndef MMX_STEP_ONLY
 // mj_forward position stage only (kinematics -> IK cache) + observation refresh
 extern "C" __global__ void __launch_bounds__(WG) mmx_forward_kernel(MMXState S) {
   EnvSh& E = g_E;
@@ -3305,6 +3322,7 @@ extern "C" hipError_t mmx_launch_reset(const MMXState* S, const unsigned char* m
   hipLaunchKernelGGL(mmx_reset_kernel, dim3(S->N), dim3(WG), 0, st, *S, mask, task);
   return hipGetLastError();
 }
+#endif  // MMX_STEP_ONLY
 // Occupancy probe (diagnostics only, never set by the product): MMX_LDS_PAD bytes of dynamic LDS
 // per step-kernel workgroup lower the envs per CU (tools/occupancy_probe.sh).
 static size_t step_lds_pad() {
@@ -3315,14 +3333,15 @@ static size_t step_lds_pad() {
   return pad;
 }
 // envs [base, base+count): independent env ranges may run on separate streams
-extern "C" hipError_t mmx_launch_step(const MMXState* S, const float* action, int adim, int expert, int base,
-                                      int count, int nsteps, hipStream_t st) {
+extern "C" hipError_t MMX_STEP_SYM(mmx_launch_step)(const MMXState* S, const float* action, int adim, int expert, int base,
+                                                    int count, int nsteps, hipStream_t st) {
   if (count <= 0 || nsteps <= 0) return hipSuccess;
   if (nsteps > 1 && !expert) return hipErrorInvalidValue;  // host actions: one env step per launch
-  hipLaunchKernelGGL(mmx_env_step_kernel, dim3(count), dim3(64), step_lds_pad(), st, *S, action, adim, expert, base,
+  hipLaunchKernelGGL(MMX_STEP_SYM(mmx_env_step_kernel), dim3(count), dim3(64), step_lds_pad(), st, *S, action, adim, expert, base,
                      nsteps);
   return hipGetLastError();
 }
+#ifndef MMX_STEP_ONLY
 extern "C" hipError_t mmx_launch_expert(const MMXState* S, int n, float* action, hipStream_t st) {
   hipLaunchKernelGGL(mmx_expert_kernel, dim3((S->N + WG - 1) / WG), dim3(WG), 0, st, *S, n, action);
   return hipGetLastError();
@@ -3347,3 +3366,4 @@ extern "C" hipError_t mmx_launch_forward(const MMXState* S, hipStream_t st) {
   hipLaunchKernelGGL(mmx_forward_kernel, dim3(S->N), dim3(WG), 0, st, *S);
   return hipGetLastError();
 }
+#endif  // MMX_STEP_ONLY

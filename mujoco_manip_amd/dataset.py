@@ -196,6 +196,40 @@ class Episode:
     image_stats: dict = field(default_factory=dict)  # image feature -> stats of a raw frame sample
 
 
+class PngFrames:
+    """An episode's PNG files back to back in one uint8 buffer (file i = data[offsets[i]:offsets[i+1]]).
+    Reads as a sequence of `bytes` (len, indexing, iteration) wherever a list of PNG files is expected;
+    the LeRobot writer hands the buffer to arrow as is (no Python object per frame)."""
+    __slots__ = ("data", "offsets")
+
+    def __init__(self, data: np.ndarray, offsets: np.ndarray):
+        self.data, self.offsets = data, offsets
+
+    def __len__(self):
+        return len(self.offsets) - 1
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        n = len(self)
+        if i < 0:
+            i += n
+        if not 0 <= i < n:
+            raise IndexError(i)
+        return self.data[int(self.offsets[i]):int(self.offsets[i + 1])].tobytes()
+
+    def __iter__(self):
+        return (self[i] for i in range(len(self)))
+
+    @property
+    def nbytes(self) -> int:
+        return int(self.offsets[-1])
+
+
+def _png_nbytes(frames) -> int:
+    return frames.nbytes if isinstance(frames, PngFrames) else sum(map(len, frames))
+
+
 def resolve_tasks(task=None, tasks="all"):
     """generate_dataset.py:205-216 (same ValueErrors)."""
     if task is not None:
@@ -434,9 +468,17 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
     cap = [64]
     tpos = np.zeros(N, np.int64)  # rows of the slot's current episode so far
     buf_ep = np.full(N, -1, np.int64)  # the episode whose rows the slot holds
-    png_rows = {f: [[] for _ in range(N)] for _, f in img_feats}
+    # PNG files: each step's packed buffer of a camera is copied once out of the pinned ring (one
+    # large numpy copy, which releases the GIL) and kept while an open episode has a frame in it; a
+    # frame is (step, start, length) in the per-slot buffers, and a finished episode's files are
+    # gathered back to back by one C call per camera (mmx_gather_bytes) into PngFrames
+    png_store = {f: {} for _, f in img_feats}  # camera -> {step: uint8 buffer}
+    png_addr = {f: np.zeros(1024, np.uint64) for _, f in img_feats}  # camera -> step -> buffer address
+    slot_first = np.zeros(N, np.int64)  # the step the slot's current episode's first frame came from
+    step_ctr = [0]  # steps absorbed so far
+    gather = env.sim.L.mmx_gather_bytes
 
-    def absorb(host, slots, ep_ids, png):
+    def absorb(host, slots, ep_ids, step):
         if len(ep_ids) == 0:
             return
         ep_slot[ep_ids] = slots
@@ -445,9 +487,7 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
             ns = slots[new]
             tpos[ns] = 0
             buf_ep[ns] = ep_ids[new]
-            for rows_f in png_rows.values():
-                for s in ns:
-                    rows_f[s] = []
+            slot_first[ns] = step
         t = tpos[slots]
         if int(t.max()) >= cap[0]:
             cap[0] *= 2
@@ -463,15 +503,6 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
                 bufs[k] = np.empty((N, cap[0]) + v.shape[1:], v.dtype)
             b = bufs[k]
             b.reshape((N * cap[0],) + b.shape[2:])[flat] = v[slots]
-        for f, data in png.items():
-            ends = host[f + "/ends"]
-            starts = np.empty_like(ends)
-            starts[0] = 0
-            starts[1:] = ends[:-1]
-            rows_f = png_rows[f]
-            # (python ints from tolist, not numpy scalar indexing per frame: 3x less host time)
-            for s, a, z in zip(slots.tolist(), starts[slots].tolist(), ends[slots].tolist()):
-                rows_f[s].append(bytes(data[a:z]))
         tpos[slots] = t + 1
 
     def finish(e):
@@ -484,9 +515,17 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
         ep.image_stats = {}
         for k in feature_keys:
             if k in IMAGE_KEYS:
-                ep.frames[k] = png_rows[k][s] if L else []
                 if L:
-                    png_rows[k][s] = []
+                    lens = np.ascontiguousarray(bufs[k + "/plen"][s, :L], np.int64)
+                    src = png_addr[k][bufs[k + "/pstep"][s, :L]] + bufs[k + "/pstart"][s, :L].astype(np.uint64)
+                    offs = np.zeros(L + 1, np.int64)
+                    np.cumsum(lens, out=offs[1:])
+                    data = np.empty(int(offs[-1]), np.uint8)
+                    if gather(L, src.ctypes.data, lens.ctypes.data, data.ctypes.data) != offs[-1]:
+                        raise RuntimeError("mmx_gather_bytes failed")
+                    ep.frames[k] = PngFrames(data, offs)
+                else:
+                    ep.frames[k] = []
                 ep.image_stats[k] = _merge_image_stats(bufs[k + "/stats"][s, :L], npx) if L else None
             elif k == "observation.phase_description":
                 lut = _phase_lut(ep.obj, ep.bin)
@@ -529,16 +568,36 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
                 state["over"] = state["over"] or state["started"]
                 continue
             state["started"] = True
-            png = {}
+            step = step_ctr[0]
+            step_ctr[0] += 1
             for f, packed in payload.items():  # the step's packed PNG files (copied: a prefix)
-                total = int(host[f + "/ends"][-1])
+                ends = host[f + "/ends"]
+                total = int(ends[-1])
                 data = host[f + "/png"]
                 if total > len(data):  # more than the estimate: fetch the rest (rare)
                     data = np.concatenate([data, packed[len(data):total].cpu().numpy()])
                 png_max[f] = max(png_max.get(f, 0), total)
                 png_est[f] = (png_max[f] * 5) // 4 + (1 << 20)
-                png[f] = memoryview(data)  # (absorb copies each frame's bytes out of it)
-            absorb(host, act, slot[act].astype(np.int64), png)
+                keep = np.empty(total, np.uint8)
+                np.copyto(keep, data[:total])  # out of the pinned ring slot before it is reused
+                png_store[f][step] = keep
+                if step >= len(png_addr[f]):
+                    png_addr[f] = np.concatenate([png_addr[f], np.zeros(len(png_addr[f]), np.uint64)])
+                png_addr[f][step] = keep.ctypes.data
+                starts = np.zeros_like(ends)
+                starts[1:] = ends[:-1]
+                host[f + "/pstart"] = starts
+                host[f + "/plen"] = (ends - starts).astype(np.int64)
+                host[f + "/pstep"] = np.full(len(ends), step, np.int64)
+            absorb(host, act, slot[act].astype(np.int64), step)
+
+    def release_png():
+        # step buffers no open episode has a frame in any more
+        live = slot_first[buf_ep >= 0]
+        oldest = int(live.min()) if len(live) else step_ctr[0]
+        for store in png_store.values():
+            for st in [st for st in store if st < oldest]:
+                del store[st]
 
     step_no = 0
     while not state["over"]:
@@ -584,6 +643,7 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
         ring.push(frame, payload)
         process(ring.ready())
         emit_ready()
+        release_png()
         step_no += 1
     process(ring.drain())
     for e in range(E):  # episodes still open when the loop ended (none, unless max_gym_steps cut it)
@@ -722,8 +782,21 @@ class LeRobotWriter:
         for k in self.img_keys:  # LeRobot's embedded image layout (images/<key>/episode_<e>/frame_<i>.png)
             pre = pa.array([f"images/{k}/episode_{ep.index:06d}" for ep in eps], pa.string()).take(pa.array(ei))
             paths = pa.compute.binary_join_element_wise(pre, names, "")  # joined in arrow, not per frame in Python
-            cols[k] = pa.StructArray.from_arrays([pa.array([v for ep in eps for v in ep.frames[k]], pa.binary()), paths],
-                                                 fields=list(self.img_type))
+            if all(isinstance(ep.frames[k], PngFrames) for ep in eps):
+                # one chunk per episode straight over its PngFrames buffer (zero-copy)
+                chunks, o = [], 0
+                for ep in eps:
+                    fr = ep.frames[k]
+                    if fr.nbytes >= 1 << 31:
+                        raise ValueError("an episode's PNG files exceed arrow's 32-bit binary offsets")
+                    b = pa.Array.from_buffers(pa.binary(), len(fr), [None, pa.py_buffer(fr.offsets.astype(np.int32)),
+                                                                     pa.py_buffer(fr.data)])
+                    chunks.append(pa.StructArray.from_arrays([b, paths.slice(o, len(fr))], fields=list(self.img_type)))
+                    o += len(fr)
+                cols[k] = pa.chunked_array(chunks, type=self.img_type)
+            else:
+                cols[k] = pa.StructArray.from_arrays([pa.array([v for ep in eps for v in ep.frames[k]], pa.binary()),
+                                                      paths], fields=list(self.img_type))
             fields.append(pa.field(k, self.img_type))
         extra = {"timestamp": pa.array((fi / self.fps).astype(np.float32)), "frame_index": pa.array(fi),
                  "episode_index": pa.array(np.repeat(np.array([ep.index for ep in eps], np.int64), lens)),
@@ -741,7 +814,7 @@ class LeRobotWriter:
         for k in self.str_keys:
             n += sum(map(len, ep.frames[k])) + 4 * ep.length
         for k in self.img_keys:
-            n += sum(map(len, ep.frames[k])) + 54 * ep.length
+            n += _png_nbytes(ep.frames[k]) + 54 * ep.length
         return n + 36 * ep.length
 
     @staticmethod

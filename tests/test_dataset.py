@@ -223,6 +223,72 @@ def test_threaded_writer_matches_inline_and_keeps_png_uncompressed(tmp_path):
     assert comp["observation.state.list.element"] == "SNAPPY"
 
 
+def _as_png_frames(frames):
+    lens = np.array([len(b) for b in frames], np.int64)
+    offs = np.zeros(len(frames) + 1, np.int64)
+    np.cumsum(lens, out=offs[1:])
+    return D.PngFrames(np.frombuffer(b"".join(frames), np.uint8).copy(), offs)
+
+
+def test_png_frames_sequence_and_writer(tmp_path):
+    """PngFrames (an episode's PNG files in one buffer, as collect_episodes builds them with
+    mmx_gather_bytes) reads like the list of files, and the writer's zero-copy per-episode chunks
+    give the same dataset (frames, meta/stats.json, info, episode metadata) as list frames."""
+    import pyarrow.parquet as pq
+
+    rng = np.random.default_rng(5)
+    feats = {k: v for k, v in D.FEATURES.items() if k in ("observation.state", "action.joint_pos")}
+    feats.update({k: dict(D.FEATURES[k], shape=(8, 8, 3)) for k in D.IMAGE_KEYS})
+    eps = _synthetic_episodes(rng, feats, n_eps=6)
+    pf = _as_png_frames(eps[0].frames[D.IMAGE_KEYS[0]])
+    want = eps[0].frames[D.IMAGE_KEYS[0]]
+    assert len(pf) == len(want) and list(pf) == want and pf[-1] == want[-1] and pf[1:3] == want[1:3]
+    assert pf.nbytes == sum(map(len, want)) == D._png_nbytes(want)
+    with pytest.raises(IndexError):
+        pf[len(want)]
+    out = {}
+    for mode in ("list", "buffer"):
+        root = str(tmp_path / mode)
+        w = D.LeRobotWriter(root, "u/ds", feats, threaded=False, batch_episodes=4)
+        for ep in eps:
+            if mode == "buffer":
+                ep = D.Episode(ep.index, ep.obj, ep.bin, ep.seed, length=ep.length,
+                               frames={k: (_as_png_frames(v) if k in D.IMAGE_KEYS else v) for k, v in ep.frames.items()})
+            w.add_episode(ep)
+        info = w.close()
+        out[mode] = (info, D.read_lerobot_v3(root)[2], root)
+    assert out["list"][0] == out["buffer"][0]
+    for ep in eps:
+        a, b = out["list"][1][ep.index], out["buffer"][1][ep.index]
+        for k in a:
+            if isinstance(a[k], np.ndarray):
+                np.testing.assert_array_equal(a[k], b[k])
+            else:
+                assert a[k] == b[k], k
+    for name in ("stats.json", "info.json"):
+        assert open(os.path.join(out["list"][2], "meta", name)).read() == \
+            open(os.path.join(out["buffer"][2], "meta", name)).read()
+    meta = [pq.read_table(os.path.join(out[m][2], "meta", "episodes", "chunk-000", "file-000.parquet")).to_pylist()
+            for m in ("list", "buffer")]
+    assert meta[0] == meta[1]
+
+
+def test_gather_bytes_host_helper():
+    """mmx_gather_bytes (host code of the C-ABI library, no GPU): byte ranges back to back."""
+    from mujoco_manip_amd import _lib
+
+    L = _lib.load(build_if_missing=False)
+    a = np.frombuffer(b"0123456789abcdefghij", np.uint8).copy()
+    src = np.array([a.ctypes.data + 10, a.ctypes.data, a.ctypes.data + 5, a.ctypes.data], np.uint64)
+    ln = np.array([3, 2, 0, 4], np.int64)
+    out = np.zeros(9, np.uint8)
+    assert L.mmx_gather_bytes(4, src.ctypes.data, ln.ctypes.data, out.ctypes.data) == 9
+    assert out.tobytes() == b"abc010123"
+    bad = np.array([-1], np.int64)
+    assert L.mmx_gather_bytes(1, src.ctypes.data, bad.ctypes.data, out.ctypes.data) == -1
+    assert L.mmx_gather_bytes(0, None, None, None) == 0
+
+
 def test_threaded_writer_reports_errors(tmp_path):
     rng = np.random.default_rng(4)
     feats = {"observation.state": D.FEATURES["observation.state"]}

@@ -86,6 +86,64 @@ def test_physics_parity_one_substep(margin):  # L1: fp32 GPU vs fp64 oracle, con
     assert dv.max() < 5e-3, dv.max()
 
 
+def test_step_layout_api():
+    """mmx_set_step_rows / mmx_step_rows: 128 rows (ten envs per CU) without cameras, 192 (eight)
+    with them, settable to either, anything else rejected."""
+    from mujoco_manip_amd import _lib
+
+    a = _lib.Sim(8, action_mode="abs_pos", image_size=0)
+    b = _lib.Sim(8, action_mode="abs_pos", image_size=32)
+    try:
+        assert a.step_rows == 128 and b.step_rows == 192
+        a.step_rows = 192
+        assert a.step_rows == 192
+        with pytest.raises(RuntimeError):
+            a.step_rows = 100
+        assert a.step_rows == 192
+    finally:
+        a.close()
+        b.close()
+
+
+def test_step_layouts_agree(margin):
+    """The two env-step kernel layouts (128 LDS rows + HBM overflow at ten envs per CU; 192 LDS rows
+    at eight) run the same arithmetic: 1024 C3 envs in lockstep through their approach and grasp
+    phases, where the contact piles put rows past 128 into the overflow block of the first layout
+    only.  Over the first 20 env steps (approach, resting contacts) the states agree to 5e-4; over
+    60 (into the grasps) every env's FSM phase is the same."""
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    import oracle_py as O
+
+    envs = []
+    for rows in (128, 192):
+        e = PickPlaceVecEnv(1024, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
+                            autoreset=False, image_size=0)
+        e.sim.step_rows = rows
+        e.reset(seed=[O.episode_seed(42, i) for i in range(1024)])
+        envs.append(e)
+    d20, fsm_diff, deep = 0.0, 0, 0.0
+    for t in range(60):
+        before = envs[0].stats[:, 0].clone()
+        for e in envs:
+            e.step(e.expert_plan(16))
+        deep = max(deep, float(((envs[0].stats[:, 0] - before) / 16).max()))
+        if t < 20:
+            d20 = max(d20, float((envs[0].qpos - envs[1].qpos).abs().max()))
+    fsm_diff = int((envs[0].fsm_state != envs[1].fsm_state).sum())
+    for e in envs:
+        e.close()
+    print(f"first 20 steps max |dqpos| {d20:.2e}; FSM phases differing after 60 steps: {fsm_diff}; "
+          f"largest mean rows per substep {deep:.0f}")
+    margin("max_abs_dqpos_first20", d20, 5e-4)
+    margin("fsm_phase_mismatches_after60", fsm_diff, 0)
+    # (stats count MuJoCo's rows: 6 pyramid edges per contact where the kernel stores 4 basis rows,
+    # so > 200 MuJoCo rows is > ~135 stored ones)
+    assert deep > 200, "no env step used the overflow rows of the 128-row layout"
+    assert d20 < 5e-4, d20
+    assert fsm_diff == 0, fsm_diff
+
+
 def test_physics_parity_one_env_step(margin):  # L1: 16 substeps; SURVEY bound qpos <= 1e-4
     dq, dv = _physics_parity(16)
     margin("max_abs_dqpos", float(dq.max()), 1e-4)

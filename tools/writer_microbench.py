@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from mujoco_manip_amd import dataset as D  # noqa: E402
 
 
-def make_episodes(n, image_size, seed=0):
+def make_episodes(n, image_size, seed=0, png_frames=False):
     rng = np.random.default_rng(seed)
     feats = D._features_at(D.resolve_features(None), image_size)
     eps = []
@@ -27,7 +27,12 @@ def make_episodes(n, image_size, seed=0):
         ep.length = L
         for k, f in feats.items():
             if k in D.IMAGE_KEYS:
-                ep.frames[k] = [rng.bytes(int(rng.integers(5000, 8000))) for _ in range(L)]
+                files = [rng.bytes(int(rng.integers(5000, 8000))) for _ in range(L)]
+                if png_frames:  # as collect_episodes hands them over (one buffer per episode)
+                    offs = np.zeros(L + 1, np.int64)
+                    np.cumsum([len(b) for b in files], out=offs[1:])
+                    files = D.PngFrames(np.frombuffer(b"".join(files), np.uint8).copy(), offs)
+                ep.frames[k] = files
                 fs = np.zeros((L, 4, 3))
                 fs[:, 0] = rng.integers(0, 40, (L, 3)) / 255.0
                 fs[:, 1] = rng.integers(200, 256, (L, 3)) / 255.0
@@ -46,8 +51,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--episodes", type=int, default=1024)
     ap.add_argument("--image-size", type=int, default=128)
+    ap.add_argument("--list-frames", action="store_true", help="PNG files as lists of bytes (default: PngFrames)")
     a = ap.parse_args()
-    feats, eps = make_episodes(a.episodes, a.image_size)
+    feats, eps = make_episodes(a.episodes, a.image_size, png_frames=not a.list_frames)
     with tempfile.TemporaryDirectory() as root:
         w = D.LeRobotWriter(os.path.join(root, "ds"), "u/bench", feats, threaded=False, io_threads=0)
         t0 = time.perf_counter()
