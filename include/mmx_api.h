@@ -120,11 +120,11 @@ int mmx_reset(mmx_sim* sim, const uint64_t* seeds, const uint8_t* seed_given, co
 int mmx_step(mmx_sim* sim, const float* action_dev, int32_t action_dim);
 
 /* Host helper of the dataset path (dataset.py collect_episodes, generate_dataset.py:250-260's
- * per-frame PNG files): copies n byte ranges (src[k] = host address, len[k] bytes) back to back into
- * dst; returns the bytes copied, -1 on bad arguments.  One call per episode and camera assembles the
- * episode's PNG files from the per-step packed buffers without a Python object per frame (ctypes
- * releases the GIL for the call). */
-int64_t mmx_gather_bytes(int64_t n, const uint64_t* src, const int64_t* len, uint8_t* dst);
+ * per-frame PNG files): copies n byte ranges, len[k] bytes from host address src[k] to dst[k]
+ * (ranges must not overlap); returns the bytes copied, -1 on bad arguments (nothing copied).  One
+ * call per camera and step appends every slot's new PNG file to its episode's buffer straight out of
+ * the pinned copy of the step, with no Python object per frame (ctypes releases the GIL for the call). */
+int64_t mmx_copy_ranges(int64_t n, const uint64_t* src, const uint64_t* dst, const int64_t* len);
 
 /* Constraint rows the env-step kernel (mmx_step, mmx_rollout_expert) keeps in LDS: 128 (ten envs
  * per CU: the fastest layout when the step kernel alone fills the GPU, C3) or 192 (eight per CU:

@@ -58,7 +58,7 @@ EXPORTED = ("mmx_config_default", "mmx_create", "mmx_destroy", "mmx_last_error",
             "mmx_synchronize", "mmx_get_state", "mmx_set_state", "mmx_episode_seed", "mmx_rollout_lanes",
             "mmx_rollout_steps_per_launch", "mmx_rollout_launches", "mmx_expert_physics", "mmx_eval_reward", "mmx_kernel_timing",
             "mmx_kernel_times", "mmx_png_bound", "mmx_png_scratch", "mmx_png_encode", "mmx_png_pack", "mmx_image_stats",
-            "mmx_queue_init", "mmx_queue_advance", "mmx_set_step_rows", "mmx_step_rows", "mmx_gather_bytes")
+            "mmx_queue_init", "mmx_queue_advance", "mmx_set_step_rows", "mmx_step_rows", "mmx_copy_ranges")
 
 _lib = None
 
@@ -89,8 +89,8 @@ def load(build_if_missing: bool = True):
     L.mmx_physics_step.argtypes = [vp, C.c_int32, C.c_int32]
     L.mmx_rollout_lanes.argtypes = [vp]
     L.mmx_rollout_lanes.restype = C.c_int
-    L.mmx_gather_bytes.argtypes = [C.c_int64, vp, vp, vp]
-    L.mmx_gather_bytes.restype = C.c_int64
+    L.mmx_copy_ranges.argtypes = [C.c_int64, vp, vp, vp]
+    L.mmx_copy_ranges.restype = C.c_int64
     L.mmx_set_step_rows.argtypes = [vp, C.c_int32]
     L.mmx_step_rows.argtypes = [vp]
     L.mmx_step_rows.restype = C.c_int

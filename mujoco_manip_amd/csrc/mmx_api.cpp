@@ -598,15 +598,18 @@ int mmx_image_stats(mmx_sim* sim, const uint8_t* rgb_dev, int64_t img_stride, in
                    "mmx_image_stats");
 }
 
-int64_t mmx_gather_bytes(int64_t n, const uint64_t* src, const int64_t* len, uint8_t* dst) {
-  if (n < 0 || (n > 0 && (!src || !len || !dst))) return -1;
-  int64_t o = 0;
+int64_t mmx_copy_ranges(int64_t n, const uint64_t* src, const uint64_t* dst, const int64_t* len) {
+  if (n < 0 || (n > 0 && (!src || !dst || !len))) return -1;
+  int64_t total = 0;
   for (int64_t k = 0; k < n; k++) {
     if (len[k] < 0) return -1;
-    if (len[k]) std::memcpy(dst + o, reinterpret_cast<const void*>(static_cast<uintptr_t>(src[k])), (size_t)len[k]);
-    o += len[k];
+    total += len[k];
   }
-  return o;
+  for (int64_t k = 0; k < n; k++)
+    if (len[k])
+      std::memcpy(reinterpret_cast<void*>(static_cast<uintptr_t>(dst[k])),
+                  reinterpret_cast<const void*>(static_cast<uintptr_t>(src[k])), (size_t)len[k]);
+  return total;
 }
 
 int mmx_rollout_steps_per_launch(const mmx_sim* sim) {

@@ -468,17 +468,28 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
     cap = [64]
     tpos = np.zeros(N, np.int64)  # rows of the slot's current episode so far
     buf_ep = np.full(N, -1, np.int64)  # the episode whose rows the slot holds
-    # PNG files: each step's packed buffer of a camera is copied once out of the pinned ring (one
-    # large numpy copy, which releases the GIL) and kept while an open episode has a frame in it; a
-    # frame is (step, start, length) in the per-slot buffers, and a finished episode's files are
-    # gathered back to back by one C call per camera (mmx_gather_bytes) into PngFrames
-    png_store = {f: {} for _, f in img_feats}  # camera -> {step: uint8 buffer}
-    png_addr = {f: np.zeros(1024, np.uint64) for _, f in img_feats}  # camera -> step -> buffer address
-    slot_first = np.zeros(N, np.int64)  # the step the slot's current episode's first frame came from
-    step_ctr = [0]  # steps absorbed so far
-    gather = env.sim.L.mmx_gather_bytes
+    # PNG files: every slot's running episode has one growing uint8 buffer per camera; each step's
+    # files are appended to their slots' buffers straight out of the pinned copy of the step by one
+    # C call per camera (mmx_copy_ranges: no Python object per frame, the GIL released for the copy),
+    # and a finished episode hands its buffer over as PngFrames (no further copy)
+    png_buf = {f: [None] * N for _, f in img_feats}  # camera -> slot -> buffer
+    png_addr = {f: np.zeros(N, np.uint64) for _, f in img_feats}  # the buffers' addresses
+    png_fill = {f: np.zeros(N, np.int64) for _, f in img_feats}  # bytes used
+    png_cap = {f: np.zeros(N, np.int64) for _, f in img_feats}  # bytes allocated
+    # first buffer size of an episode: 1.25 x the largest finished episode so far; before any has
+    # finished, 160 frames of the first step's mean file size (grown by doubling when exceeded)
+    png_guess = {f: 0 for _, f in img_feats}
+    copy_ranges = env.sim.L.mmx_copy_ranges
 
-    def absorb(host, slots, ep_ids, step):
+    def png_alloc(f, s, cap, keep=0):
+        buf = np.empty(int(cap), np.uint8)
+        if keep:
+            buf[:keep] = png_buf[f][s][:keep]
+        png_buf[f][s] = buf
+        png_addr[f][s] = buf.ctypes.data
+        png_cap[f][s] = len(buf)
+
+    def absorb(host, slots, ep_ids, png):
         if len(ep_ids) == 0:
             return
         ep_slot[ep_ids] = slots
@@ -487,7 +498,30 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
             ns = slots[new]
             tpos[ns] = 0
             buf_ep[ns] = ep_ids[new]
-            slot_first[ns] = step
+            for f in png_buf:
+                png_fill[f][ns] = 0
+                for s in ns.tolist():
+                    png_alloc(f, s, png_guess[f] or (1 << 16))
+        for f, data in png.items():  # append the step's files to their episodes' buffers
+            ends = host[f + "/ends"]
+            if png_guess[f] == 0:
+                png_guess[f] = 160 * max(1, int(ends[-1]) // max(1, len(ends)))
+                for s in np.nonzero(png_cap[f][slots] < png_guess[f])[0].tolist():
+                    if png_fill[f][slots[s]] == 0:
+                        png_alloc(f, int(slots[s]), png_guess[f])
+            starts = np.zeros_like(ends)
+            starts[1:] = ends[:-1]
+            lens = (ends - starts)[slots].astype(np.int64)
+            need = png_fill[f][slots] + lens
+            for k in np.nonzero(need > png_cap[f][slots])[0].tolist():  # (rare) grow
+                s = int(slots[k])
+                png_alloc(f, s, max(2 * int(need[k]), png_guess[f]), keep=int(png_fill[f][s]))
+            src = (data.ctypes.data + starts[slots].astype(np.uint64)).astype(np.uint64)
+            dst = png_addr[f][slots] + png_fill[f][slots].astype(np.uint64)
+            if copy_ranges(len(slots), src.ctypes.data, dst.ctypes.data, lens.ctypes.data) != int(lens.sum()):
+                raise RuntimeError("mmx_copy_ranges failed")
+            png_fill[f][slots] = need
+            host[f + "/plen"] = (ends - starts).astype(np.int64)
         t = tpos[slots]
         if int(t.max()) >= cap[0]:
             cap[0] *= 2
@@ -516,14 +550,13 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
         for k in feature_keys:
             if k in IMAGE_KEYS:
                 if L:
-                    lens = np.ascontiguousarray(bufs[k + "/plen"][s, :L], np.int64)
-                    src = png_addr[k][bufs[k + "/pstep"][s, :L]] + bufs[k + "/pstart"][s, :L].astype(np.uint64)
                     offs = np.zeros(L + 1, np.int64)
-                    np.cumsum(lens, out=offs[1:])
-                    data = np.empty(int(offs[-1]), np.uint8)
-                    if gather(L, src.ctypes.data, lens.ctypes.data, data.ctypes.data) != offs[-1]:
-                        raise RuntimeError("mmx_gather_bytes failed")
-                    ep.frames[k] = PngFrames(data, offs)
+                    np.cumsum(bufs[k + "/plen"][s, :L], out=offs[1:])
+                    if offs[-1] != png_fill[k][s]:
+                        raise RuntimeError(f"episode {ep.index}: PNG bytes {png_fill[k][s]} != frames {offs[-1]}")
+                    ep.frames[k] = PngFrames(png_buf[k][s][:int(offs[-1])], offs)
+                    png_buf[k][s] = None
+                    png_guess[k] = max(png_guess[k], int(offs[-1]) * 5 // 4)
                 else:
                     ep.frames[k] = []
                 ep.image_stats[k] = _merge_image_stats(bufs[k + "/stats"][s, :L], npx) if L else None
@@ -568,36 +601,16 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
                 state["over"] = state["over"] or state["started"]
                 continue
             state["started"] = True
-            step = step_ctr[0]
-            step_ctr[0] += 1
+            png = {}
             for f, packed in payload.items():  # the step's packed PNG files (copied: a prefix)
-                ends = host[f + "/ends"]
-                total = int(ends[-1])
+                total = int(host[f + "/ends"][-1])
                 data = host[f + "/png"]
                 if total > len(data):  # more than the estimate: fetch the rest (rare)
                     data = np.concatenate([data, packed[len(data):total].cpu().numpy()])
                 png_max[f] = max(png_max.get(f, 0), total)
                 png_est[f] = (png_max[f] * 5) // 4 + (1 << 20)
-                keep = np.empty(total, np.uint8)
-                np.copyto(keep, data[:total])  # out of the pinned ring slot before it is reused
-                png_store[f][step] = keep
-                if step >= len(png_addr[f]):
-                    png_addr[f] = np.concatenate([png_addr[f], np.zeros(len(png_addr[f]), np.uint64)])
-                png_addr[f][step] = keep.ctypes.data
-                starts = np.zeros_like(ends)
-                starts[1:] = ends[:-1]
-                host[f + "/pstart"] = starts
-                host[f + "/plen"] = (ends - starts).astype(np.int64)
-                host[f + "/pstep"] = np.full(len(ends), step, np.int64)
-            absorb(host, act, slot[act].astype(np.int64), step)
-
-    def release_png():
-        # step buffers no open episode has a frame in any more
-        live = slot_first[buf_ep >= 0]
-        oldest = int(live.min()) if len(live) else step_ctr[0]
-        for store in png_store.values():
-            for st in [st for st in store if st < oldest]:
-                del store[st]
+                png[f] = data  # (absorb appends each slot's file to its episode's buffer)
+            absorb(host, act, slot[act].astype(np.int64), png)
 
     step_no = 0
     while not state["over"]:
@@ -643,7 +656,6 @@ def collect_episodes(num_episodes: int, task_list, feature_keys, *, reward_type=
         ring.push(frame, payload)
         process(ring.ready())
         emit_ready()
-        release_png()
         step_no += 1
     process(ring.drain())
     for e in range(E):  # episodes still open when the loop ended (none, unless max_gym_steps cut it)

@@ -232,7 +232,7 @@ def _as_png_frames(frames):
 
 def test_png_frames_sequence_and_writer(tmp_path):
     """PngFrames (an episode's PNG files in one buffer, as collect_episodes builds them with
-    mmx_gather_bytes) reads like the list of files, and the writer's zero-copy per-episode chunks
+    mmx_copy_ranges) reads like the list of files, and the writer's zero-copy per-episode chunks
     give the same dataset (frames, meta/stats.json, info, episode metadata) as list frames."""
     import pyarrow.parquet as pq
 
@@ -273,20 +273,23 @@ def test_png_frames_sequence_and_writer(tmp_path):
     assert meta[0] == meta[1]
 
 
-def test_gather_bytes_host_helper():
-    """mmx_gather_bytes (host code of the C-ABI library, no GPU): byte ranges back to back."""
+def test_copy_ranges_host_helper():
+    """mmx_copy_ranges (host code of the C-ABI library, no GPU): n byte ranges src[k] -> dst[k]."""
     from mujoco_manip_amd import _lib
 
     L = _lib.load(build_if_missing=False)
     a = np.frombuffer(b"0123456789abcdefghij", np.uint8).copy()
+    out = np.zeros(12, np.uint8)
     src = np.array([a.ctypes.data + 10, a.ctypes.data, a.ctypes.data + 5, a.ctypes.data], np.uint64)
+    dst = np.array([out.ctypes.data + 9, out.ctypes.data, out.ctypes.data + 2, out.ctypes.data + 2], np.uint64)
     ln = np.array([3, 2, 0, 4], np.int64)
-    out = np.zeros(9, np.uint8)
-    assert L.mmx_gather_bytes(4, src.ctypes.data, ln.ctypes.data, out.ctypes.data) == 9
-    assert out.tobytes() == b"abc010123"
-    bad = np.array([-1], np.int64)
-    assert L.mmx_gather_bytes(1, src.ctypes.data, bad.ctypes.data, out.ctypes.data) == -1
-    assert L.mmx_gather_bytes(0, None, None, None) == 0
+    assert L.mmx_copy_ranges(4, src.ctypes.data, dst.ctypes.data, ln.ctypes.data) == 9
+    assert out.tobytes() == b"010123\x00\x00\x00abc"
+    bad = np.array([2, -1], np.int64)
+    before = out.copy()
+    assert L.mmx_copy_ranges(2, src.ctypes.data, dst.ctypes.data, bad.ctypes.data) == -1
+    np.testing.assert_array_equal(out, before)  # nothing copied on bad arguments
+    assert L.mmx_copy_ranges(0, None, None, None) == 0
 
 
 def test_threaded_writer_reports_errors(tmp_path):
