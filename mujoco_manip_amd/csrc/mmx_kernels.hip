@@ -75,6 +75,7 @@ static constexpr int kBinBody[3] = {MMX_BODY_BIN_RED, MMX_BODY_BIN_GREEN, MMX_BO
 #endif
 
 // ============================================================================ per-env LDS
+enum { CL_DIST = 0, CL_POS = 1, CL_N = 4, CL_G1 = 7, CL_G2 = 8, CL_F };
 struct EnvSh {
   float qpos[30], qvel[28], ctrl[8], ws[28];
   float target[4];
@@ -85,7 +86,10 @@ struct EnvSh {
   float M9[9][9];
   float Mc[18];
   float qfrc[LD], qacc_s[LD], x[LD], p[LD];
-  float con[MMX_MAXCON][CON_F];
+  // contacts in LDS: 9 floats each (CL_*); the pair's friction and condim are table lookups of the
+  // two geoms (MuJoCo mixing: max), recomputed where needed, so the 13-field HBM record (CON_*,
+  // include/mmx_api.h) is filled only when the contacts are stored
+  float con[MMX_MAXCON][CL_F];
   int conkey[MMX_MAXCON];
   // constraint rows in block format: a row touches at most two dof blocks (arm = 9 dofs,
   // cube k = 6 dofs); J[i][0..n0) holds block b0's columns, J[i][n0..n0+n1) block b1's;
@@ -130,9 +134,9 @@ struct EnvSh {
 // The workgroup's env lives in one file-scope LDS object: the non-inlined substep function below
 // reaches it by symbol (LDS address space), not through a generic pointer.
 static __shared__ EnvSh g_E;
-// ten workgroups (envs) per CU share its 160 KiB of LDS: the occupancy the kernel is tuned for (r05; with
-// 192 LDS rows, MMX_LDSEFC=192, eight)
-static_assert(MMX_LDSEFC != 128 || sizeof(EnvSh) <= 160 * 1024 / 10, "EnvSh no longer fits 10 envs per CU");
+// eleven workgroups (envs) per CU share its 160 KiB of LDS: the occupancy the kernel is tuned for (r05;
+// with 192 LDS rows, MMX_LDSEFC=192, eight)
+static_assert(MMX_LDSEFC != 128 || sizeof(EnvSh) <= 160 * 1024 / 11, "EnvSh no longer fits 11 envs per CU");
 static_assert(sizeof(EnvSh) <= 160 * 1024 / 8, "EnvSh no longer fits 8 envs per CU");
 
 // The scratch region: E.J, E.hdr, E.D and E.NC (contiguous in EnvSh) hold the phases' scratch outside
@@ -141,8 +145,9 @@ static_assert(sizeof(EnvSh) <= 160 * 1024 / 8, "EnvSh no longer fits 8 envs per 
 // dynamics (at COL_WORK) and the observation of the step end.  The Newton Hessian staging tile and
 // Cholesky transpose live in E.con instead (contacts are dead once the rows exist; the last substep
 // stores them to HBM first).
-// r05: 128 LDS rows (MMX_LDSEFC) and this 2,400-float layout bring the env to 15,824 B of LDS, ten
-// per CU (was 20,432 B with 192 rows: eight); rows past 128 go to the HBM overflow block.
+// r05: 128 LDS rows (MMX_LDSEFC), this 2,400-float layout and 9-float contacts bring the env to
+// 14,800 B of LDS, eleven per CU (was 20,432 B with 192 rows: eight); rows past 128 go to the HBM
+// overflow block.
 #define GXS 17        // geom record: world pose (x 3, R 9), rbound, type, box half extents (3)
 #define GX_RB 12
 #define GX_TYPE 13
@@ -164,7 +169,7 @@ static_assert(offsetof(EnvSh, hdr) == offsetof(EnvSh, J) + sizeof(EnvSh::J) &&
               "the scratch region must be contiguous");
 #define SCR_FLOATS ((int)((offsetof(EnvSh, NC) + sizeof(EnvSh::NC) - offsetof(EnvSh, J)) / 4))
 static_assert(COL_EPA + EPA_SCRATCH_FLOATS <= SCR_FLOATS, "EPA scratch exceeds the scratch region");
-static_assert(COL_WORK + MMX_MAXCON * CON_F <= SCR_FLOATS, "contact sort exceeds the scratch region");
+static_assert(COL_WORK + MMX_MAXCON * CL_F <= SCR_FLOATS, "contact sort exceeds the scratch region");
 static_assert(COL_WORK + COL_PLANES * COL_POLY <= SCR_FLOATS, "box-box polygons exceed the scratch region");
 static_assert(MMX_CAND_CAP <= COL_LIST && MMX_NPAIR < 4096, "collision scratch layout");
 
@@ -176,15 +181,17 @@ static_assert(MMX_CAND_CAP <= COL_LIST && MMX_NPAIR < 4096, "collision scratch l
 #define SCR_ACT (COL_WORK + 96)    // raw action of the step (lane 0, before the substeps)
 static_assert(SCR_BIAS + 9 <= SCR_FLOATS && SCR_OBS + MMX_NOBS <= SCR_ACT && SCR_ACT + 12 <= SCR_FLOATS,
               "scratch layout");
-static_assert(27 * 27 <= MMX_MAXCON * CON_F, "Newton Cholesky transpose exceeds E.con");
 DEV float* scr_of(EnvSh& E) { return reinterpret_cast<float*>(&E.J); }
 DEV const float* scr_of(const EnvSh& E) { return reinterpret_cast<const float*>(&E.J); }
 DEV float* obs_of(EnvSh& E) { return scr_of(E) + SCR_OBS; }
 DEV const float* obs_of(const EnvSh& E) { return scr_of(E) + SCR_OBS; }
-DEV float* lrow_of(EnvSh& E) { return &E.con[0][0]; }  // [27][27] Newton factor / staging tile
+DEV float* lrow_of(EnvSh& E) { return &E.con[0][0]; }  // Hessian staging tiles (E.con is dead once the rows exist)
+// the general (cube-cube coupled) Cholesky's 27 x 27 transpose: rare, so in the env's HBM scratch
+// block after the overflow rows (MMX_OVF_F), not in LDS
+DEV float* arrow_of(EnvSh& E) { return E.ovf + 18 * MMX_OVFEFC; }
 // the rows' mu between the row build and the solver setup (E.con is dead once the rows exist)
 DEV float* mu_stage(EnvSh& E) { return &E.con[0][0]; }
-static_assert(MMX_MAXEFC <= MMX_MAXCON * CON_F, "row mu staging exceeds E.con");
+static_assert(MMX_MAXEFC <= MMX_MAXCON * CL_F, "row mu staging exceeds E.con");
 // Constraint row i: J in E.J[.][i] (chunk-major) and D in E.D[i] for i < MMX_LDSEFC, else in the env's HBM
 // overflow block (J rows [OVFEFC][16], then D [OVFEFC]).  For a lane-owned row i = LANE + 64 q the
 // test folds at compile time (LANE's known bits), so the unrolled loops carry no branch.
@@ -222,7 +229,21 @@ DEV void ovf_fence(int nefc) {
 // built: the solver then reuses E.con as scratch
 DEV void store_contacts(float* dst, const EnvSh& E) {
   const int n = E.ncon;
-  for (int k = LANE; k < MMX_MAXCON * CON_F; k += WG) dst[k] = k < n * CON_F ? (&E.con[0][0])[k] : 0.f;
+  for (int c = LANE; c < MMX_MAXCON; c += WG) {  // the 13-field record (CON_*) of LDS contact c
+    float* o = dst + (size_t)c * CON_F;
+    const float* l = E.con[c];
+    const int g1 = c < n ? (int)l[CL_G1] : 0, g2 = c < n ? (int)l[CL_G2] : 0;
+    o[CON_DIST] = c < n ? l[CL_DIST] : 0.f;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+      o[CON_POS + k] = c < n ? l[CL_POS + k] : 0.f;
+      o[CON_N + k] = c < n ? l[CL_N + k] : 0.f;
+      o[CON_MU0 + k] = c < n ? fmaxf(MMX_geom_friction[3 * g1 + k], MMX_geom_friction[3 * g2 + k]) : 0.f;
+    }
+    o[CON_DIM] = c < n ? (float)max(MMX_geom_condim[g1], MMX_geom_condim[g2]) : 0.f;
+    o[CON_G1] = c < n ? (float)g1 : 0.f;
+    o[CON_G2] = c < n ? (float)g2 : 0.f;
+  }
 }
 DEV float* contacts_dst(const MMXState& S, int i) { return S.con + (size_t)i * MMX_MAXCON * CON_F; }
 enum { SHF_ROBOT_OBST = 1, SHF_CON_OVF = 2, SHF_EFC_OVF = 4, SHF_NAN = 8 };
@@ -734,9 +755,7 @@ struct WaveSink {
   EnvSh* E;
   int key;
   bool store;
-  // pair constants, loaded once per pair (MuJoCo mixing: friction max, condim max)
   bool ro;
-  float mu0, mu1, mu2, dim;
   int bodies;  // geom bodies packed above the 16-bit order key: b1 << 16 | b2 << 24
   int key0;
   DEV WaveSink(EnvSh* e, int p, bool st, int g1, int g2) : E(e), key(p * 8), store(st) {
@@ -744,10 +763,6 @@ struct WaveSink {
     bodies = (MMX_geom_body[g1] << 16) | (MMX_geom_body[g2] << 24);
     const int c1 = MMX_geom_class[g1], c2 = MMX_geom_class[g2];
     ro = (c1 == 1 && c2 == 2) || (c1 == 2 && c2 == 1);
-    mu0 = fmaxf(MMX_geom_friction[3 * g1], MMX_geom_friction[3 * g2]);
-    mu1 = fmaxf(MMX_geom_friction[3 * g1 + 1], MMX_geom_friction[3 * g2 + 1]);
-    mu2 = fmaxf(MMX_geom_friction[3 * g1 + 2], MMX_geom_friction[3 * g2 + 2]);
-    dim = (float)max(MMX_geom_condim[g1], MMX_geom_condim[g2]);
   }
   DEV void add(int g1, int g2, float dist, V3 pos, V3 nrm) { put(reserve(1), g1, g2, dist, pos, nrm); }
   // contact `order` of the pair (its key = pair * 8 + order, as the sequential put would give it)
@@ -772,15 +787,11 @@ struct WaveSink {
     if (slot >= MMX_MAXCON) return;
     nrm = normalize(nrm);
     float* c = E->con[slot];
-    c[CON_DIST] = dist;
-    c[CON_POS] = pos.x; c[CON_POS + 1] = pos.y; c[CON_POS + 2] = pos.z;
-    c[CON_N] = nrm.x; c[CON_N + 1] = nrm.y; c[CON_N + 2] = nrm.z;
-    c[CON_MU0] = mu0;
-    c[CON_MU1] = mu1;
-    c[CON_MU2] = mu2;
-    c[CON_DIM] = dim;
-    c[CON_G1] = (float)g1;
-    c[CON_G2] = (float)g2;
+    c[CL_DIST] = dist;
+    c[CL_POS] = pos.x; c[CL_POS + 1] = pos.y; c[CL_POS + 2] = pos.z;
+    c[CL_N] = nrm.x; c[CL_N + 1] = nrm.y; c[CL_N + 2] = nrm.z;
+    c[CL_G1] = (float)g1;
+    c[CL_G2] = (float)g2;
     E->conkey[slot] = (key++) | bodies;
   }
 };
@@ -1068,11 +1079,11 @@ DEV void collide_sort(EnvSh& E) {
     const int key = kb & 0xFFFF;
     for (int j = 0; j < n; j++) rank += (E.conkey[j] & 0xFFFF) < key;
 #pragma unroll
-    for (int f = 0; f < CON_F; f++) tmp[rank * CON_F + f] = E.con[LANE][f];
+    for (int f = 0; f < CL_F; f++) tmp[rank * CL_F + f] = E.con[LANE][f];
   }
   SYNC();
   if (LANE < n) E.conkey[rank] = kb;
-  for (int k = LANE; k < n * CON_F; k += WG) (&E.con[0][0])[k] = tmp[k];
+  for (int k = LANE; k < n * CL_F; k += WG) (&E.con[0][0])[k] = tmp[k];
   if (LANE == 0) E.ncon = n;
   SYNC();
   PROBE(5, stats, STAT_T_AUX3);
@@ -1114,11 +1125,34 @@ DEV void store_row(EnvSh& E, int row, const float* jv, int hdr, float vel, float
   dset(E, row, 1.f / fmaxf(imp_ratio * diag, 1e-15f));
 }
 
-// per-contact row generator, written by the contact's lane into fields of its own contact record
-// that the rows no longer need (distance, torsional friction, geom ids) and read by its rows'
-// lanes: impedance ratio x translational invweight, K imp pos, B.  The contacts are
-// copied to HBM (last substep) before this overwrite.
-enum { CG_IT = CON_DIST, CG_KID = CON_G1, CG_B = CON_G2 };
+// A contact's mixed parameters (MuJoCo: friction and condim the max of the two geoms', solref /
+// solimp their mean) and reference terms: computed by each of its basis rows' lanes from the
+// 9-float LDS record (the rows of one contact are built by up to four lanes; the same inputs and
+// arithmetic give each the same values)
+struct ConPar {
+  int dim;
+  float mu0, mu1, kid, B, idiag;
+};
+DEV ConPar contact_params(const float* cc, int b1, int b2) {
+  const int g1 = (int)cc[CL_G1], g2 = (int)cc[CL_G2];
+  ConPar P;
+  P.dim = max(MMX_geom_condim[g1], MMX_geom_condim[g2]);
+  P.mu0 = fmaxf(MMX_geom_friction[3 * g1], MMX_geom_friction[3 * g2]);
+  P.mu1 = fmaxf(MMX_geom_friction[3 * g1 + 1], MMX_geom_friction[3 * g2 + 1]);
+  float solref[2], solimp[5];
+#pragma unroll
+  for (int k = 0; k < 2; k++) solref[k] = 0.5f * (MMX_geom_solref[2 * g1 + k] + MMX_geom_solref[2 * g2 + k]);
+#pragma unroll
+  for (int k = 0; k < 5; k++) solimp[k] = 0.5f * (MMX_geom_solimp[5 * g1 + k] + MMX_geom_solimp[5 * g2 + k]);
+  float impr;
+  row_ref(solref, solimp, cc[CL_DIST], impr, P.kid, P.B);
+  const float tran = MMX_body_invweight0[2 * b1] + MMX_body_invweight0[2 * b2];
+  const float it = impr * tran;  // (the pyramid's common R needs only the translational invweight)
+  // pyramidal cone: one R for every edge, A_hat = 2 mu0^2 (tran + mu0^2 tran) / impratio (impratio
+  // = 1), R = (1 - d) / d A_hat; pinned by the closed-form scenes of tests/test_physics_kat.py
+  P.idiag = P.dim > 1 ? 2.f * P.mu0 * P.mu0 * (it + P.mu0 * P.mu0 * it) : it;
+  return P;
+}
 DEV V3 contact_t1(V3 n) {  // mju_makeFrame's first tangent
   const V3 y = (n.y < 0.5f && n.y > -0.5f) ? V3{0.f, 1.f, 0.f} : V3{0.f, 0.f, 1.f};
   return normalize(y - n * dot(n, y));
@@ -1133,21 +1167,16 @@ DEV V3 contact_t1(V3 n) {  // mju_makeFrame's first tangent
 // contact's condim does not use are zero rows with D = 0.  Returns the row's mu (-1: no edges).
 DEV float contact_row(EnvSh& E, int row, int c, int rr) {
   const float* cc = E.con[c];
-  const V3 p = V3{cc[CON_POS], cc[CON_POS + 1], cc[CON_POS + 2]};
-  const V3 n = V3{cc[CON_N], cc[CON_N + 1], cc[CON_N + 2]};
-  const int dim = (int)cc[CON_DIM];
+  const V3 p = V3{cc[CL_POS], cc[CL_POS + 1], cc[CL_POS + 2]};
+  const V3 n = V3{cc[CL_N], cc[CL_N + 1], cc[CL_N + 2]};
   const int b1 = (E.conkey[c] >> 16) & 255, b2 = (E.conkey[c] >> 24) & 255;
+  const ConPar P = contact_params(cc, b1, b2);
+  const int dim = P.dim;
   const bool used = rr == 0 || (rr < 3 && dim >= 3) || (rr == 3 && dim >= 4);
   const V3 t1 = contact_t1(n);
   const V3 u = rr == 0 ? n : (rr == 1 ? t1 : (rr == 2 ? cross(n, t1) : V3{0.f, 0.f, 0.f}));
   const V3 w = rr == 3 ? n : V3{0.f, 0.f, 0.f};
-  // pyramidal cone: one R for every edge, A_hat = 2 mu0^2 (tran + mu0^2 tran) / impratio (impratio
-  // = 1), R = (1 - d) / d A_hat; pinned by the closed-form scenes of tests/test_physics_kat.py
-  float idiag = cc[CG_IT];  // impedance ratio x diagApprox
-  if (dim > 1) {
-    const float mu0 = cc[CON_MU0];
-    idiag = 2.f * mu0 * mu0 * (cc[CG_IT] + mu0 * mu0 * cc[CG_IT]);
-  }
+  const float idiag = P.idiag;  // impedance ratio x diagApprox
   const int k1 = body_block(b1), k2 = body_block(b2);
   int rb0 = k1 >= 0 ? k1 : k2, rb1 = (k1 >= 0 && k2 >= 0 && k2 != k1) ? k2 : BLK_NONE;
   if (rb1 != BLK_NONE && rb1 < rb0) {
@@ -1206,9 +1235,9 @@ DEV float contact_row(EnvSh& E, int row, int c, int rr) {
     const float vc = j < 6 ? cubeA[j] : (j < 12 ? cubeB[j - 6] : 0.f);
     jv[j] = armrow ? va : vc;
   }
-  store_row(E, row, jv, rb0 | (rb1 << 4), vel, 1.f, rr == 0 ? cc[CG_KID] : 0.f, cc[CG_B], idiag);
+  store_row(E, row, jv, rb0 | (rb1 << 4), vel, 1.f, rr == 0 ? P.kid : 0.f, P.B, idiag);
   if (!used) dset(E, row, 0.f);  // (its J is zero as well: u = w = 0)
-  return !used || rr == 0 ? (rr == 0 ? 0.f : -1.f) : (rr < 3 ? cc[CON_MU0] : cc[CON_MU1]);
+  return !used || rr == 0 ? (rr == 0 ? 0.f : -1.f) : (rr < 3 ? P.mu0 : P.mu1);
 }
 
 // Constraint rows in MuJoCo's order per lane scan: finger equality (lane 0), joint limits
@@ -1236,7 +1265,7 @@ DEV void make_constraints_wave(EnvSh& E) {
     nlim = (int)lo_act + (int)hi_act;
   }
   if (LANE < ncon) {
-    const int dim = (int)E.con[LANE][CON_DIM];
+    const int dim = max(MMX_geom_condim[(int)E.con[LANE][CL_G1]], MMX_geom_condim[(int)E.con[LANE][CL_G2]]);
     nedge = dim == 1 ? 1 : 2 * (dim - 1);
     const int kb = E.conkey[LANE];
     const int k1 = body_block((kb >> 16) & 255), k2 = body_block((kb >> 24) & 255);
@@ -1288,21 +1317,7 @@ DEV void make_constraints_wave(EnvSh& E) {
       if ((side == 0 ? lo_act : hi_act) && row < MMX_MAXEFC) rowmap_set(row++, -1);  // joint limits
   }
   PROBE(3, stats, STAT_T_AUX1);
-  if (LANE < ncon) {  // contact generator: mixed parameters, reference terms
-    float* c = E.con[LANE];
-    const int g1 = (int)c[CON_G1], g2 = (int)c[CON_G2];
-    const int b1 = (E.conkey[LANE] >> 16) & 255, b2 = (E.conkey[LANE] >> 24) & 255;
-    float solref[2], solimp[5];
-#pragma unroll
-    for (int k = 0; k < 2; k++) solref[k] = 0.5f * (MMX_geom_solref[2 * g1 + k] + MMX_geom_solref[2 * g2 + k]);
-#pragma unroll
-    for (int k = 0; k < 5; k++) solimp[k] = 0.5f * (MMX_geom_solimp[5 * g1 + k] + MMX_geom_solimp[5 * g2 + k]);
-    float impr, kid, B;
-    row_ref(solref, solimp, c[CON_DIST], impr, kid, B);
-    const float tran = MMX_body_invweight0[2 * b1] + MMX_body_invweight0[2 * b2];
-    c[CG_IT] = impr * tran;  // (the pyramid's common R needs only the translational invweight)
-    c[CG_KID] = kid;
-    c[CG_B] = B;
+  if (LANE < ncon) {  // the contact's 4 basis rows in the row -> (contact, basis row) map
 #pragma unroll
     for (int rr = 0; rr < 4; rr++)
       if (brow + rr < MMX_MAXEFC) rowmap_set(brow + rr, LANE | (rr << 8));
@@ -1554,7 +1569,7 @@ DEV void tile_gather(const float* G, int t, int bd, int od, float* hrow, float& 
 // row types staged per barrier round (E.con holds up to three 16 x 16 tiles; 3 measured -1.3 % in the
 // r03 A/B: the unrolled rounds grow the substep's register save area)
 #define HESS_TILES 1
-static_assert(HESS_TILES * 16 * GST <= MMX_MAXCON * CON_F, "Hessian staging tiles exceed E.con");
+static_assert(HESS_TILES * 16 * GST <= MMX_MAXCON * CL_F, "Hessian staging tiles exceed E.con");
 DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
   float* stats = E.stats;
   CLK_DECL;
@@ -1945,12 +1960,13 @@ DEV float chol_solve_arrow(EnvSh& E, const float* hrow, float v, int cpl) {
   const int jc = max(j, 0);
   if (j >= 0) {
 #pragma unroll
-    for (int m = 0; m < 27; m++) lrow_of(E)[27 * j + m] = h[m];
+    for (int m = 0; m < 27; m++) arrow_of(E)[27 * j + m] = h[m];
   }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // (HBM: the stores complete before the reads)
   SYNC();
   float c[27];
 #pragma unroll
-  for (int k = 0; k < 27; k++) c[k] = lrow_of(E)[27 * k + jc];  // L[k][j]
+  for (int k = 0; k < 27; k++) c[k] = arrow_of(E)[27 * k + jc];  // L[k][j]
 #pragma unroll
   for (int pi = 26; pi >= 0; pi--) {  // L' z = y
     const int p = pi < 18 ? pi + 9 : pi - 18;

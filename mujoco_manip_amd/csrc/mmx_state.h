@@ -17,13 +17,15 @@
 // constraint rows (basis rows: 4 per contact + equality / limits padded to 4; <= 64 x 4 + 20)
 #define MMX_MAXEFC 320
 // constraint rows [0, MMX_LDSEFC) live in the workgroup's LDS, rows [MMX_LDSEFC, MMX_MAXEFC) in the
-// env's HBM overflow block (efc_ovf); 128 rows keep the env's LDS under 16 KB (10 envs per CU; r01-r04:
-// 192 rows, 20 KB, 8 per CU)
+// env's HBM overflow block (efc_ovf); 128 rows (with 9-float LDS contacts) keep the env's LDS at
+// 14,800 B (11 envs per CU; r01-r04: 192 rows, 20 KB, 8 per CU)
 #ifndef MMX_LDSEFC
 #define MMX_LDSEFC 128
 #endif
 #define MMX_OVFEFC (MMX_MAXEFC - MMX_LDSEFC)
-#define MMX_OVF_F (MMX_OVFEFC * 18)  // floats per env: J rows [OVFEFC][16], then D, NC [OVFEFC]
+// floats per env: J rows [OVFEFC][16], then D, NC [OVFEFC], then the general Cholesky's 27 x 27
+// transpose (+3: 16-byte aligned blocks)
+#define MMX_OVF_F (MMX_OVFEFC * 18 + 27 * 27 + 3)
 #define MMX_NSUBSTEP 16
 
 // stale kinematics cache read by the IK (controller.py:99-108 reads data.xpos / mj_jac
