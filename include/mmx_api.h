@@ -126,12 +126,13 @@ int mmx_step(mmx_sim* sim, const float* action_dev, int32_t action_dim);
  * the pinned copy of the step, with no Python object per frame (ctypes releases the GIL for the call). */
 int64_t mmx_copy_ranges(int64_t n, const uint64_t* src, const uint64_t* dst, const int64_t* len);
 
-/* Constraint rows the env-step kernel (mmx_step, mmx_rollout_expert) keeps in LDS: 128 (ten envs
- * per CU: the fastest layout when the step kernel alone fills the GPU, C3) or 192 (eight per CU:
- * faster with cameras, C5, and with fewer envs than the GPU's workgroup slots, C2).  Default 192
- * with cameras, 128 without; env MMX_STEP_ROWS overrides at create.  The rows past the LDS ones live
- * in the env's HBM overflow block; results agree within fp32 rounding (the parity tests run both).
- * MMX_EINVAL for any other value.  (No reference counterpart: a layout choice of this port.) */
+/* Constraint rows the env-step kernel (mmx_step, mmx_rollout_expert) keeps in LDS: 128 (eleven envs
+ * per CU, the default: the fastest layout once the batch fills the GPU's workgroup slots, C3 / C5 /
+ * dataset generation) or 192 (eight per CU: faster per env, so for batches that leave slots empty,
+ * e.g. C2's 1024 envs).  Env MMX_STEP_ROWS overrides at create.  The rows past the LDS ones live in
+ * the env's HBM overflow block; the two layouts agree to fp32 rounding (the parity tests run both),
+ * so keep one layout per experiment.  MMX_EINVAL for any other value.  (No reference counterpart: a
+ * layout choice of this implementation.) */
 int mmx_set_step_rows(mmx_sim* sim, int32_t rows);
 int mmx_step_rows(const mmx_sim* sim);
 

@@ -59,8 +59,9 @@ struct mmx_sim {
   int nlanes = 1;
   // env steps per mmx_env_step_kernel launch in expert rollouts without cameras (MMX_FUSE overrides)
   int fuse = 16;
-  // constraint rows the env-step kernel keeps in LDS: 128 (ten envs per CU) or 192 (eight per CU,
-  // mmx_step_l192.hip); by default 192 with cameras, 128 without (mmx_set_step_rows, MMX_STEP_ROWS)
+  // constraint rows the env-step kernel keeps in LDS: 128 (eleven envs per CU, the default) or 192
+  // (eight per CU, mmx_step_l192.hip: faster when the batch leaves CU slots empty; mmx_set_step_rows,
+  // MMX_STEP_ROWS)
   int step_rows = 128;
   hipStream_t lane[kMaxLanes] = {};
   hipEvent_t ev_fork = nullptr, ev_join[kMaxLanes] = {};
@@ -335,7 +336,7 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
   int lanes = std::min(N / 1024, 4);
   if (const char* v = std::getenv("MMX_STREAMS")) lanes = std::atoi(v);
   if (const char* v = std::getenv("MMX_FUSE")) sim->fuse = std::max(1, std::atoi(v));
-  sim->step_rows = cfg->image_size > 0 ? 192 : 128;
+  sim->step_rows = 128;
   if (const char* v = std::getenv("MMX_STEP_ROWS")) {
     const int r = std::atoi(v);
     if (r == 128 || r == 192) sim->step_rows = r;

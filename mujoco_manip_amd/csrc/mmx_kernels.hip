@@ -1165,12 +1165,14 @@ DEV V3 contact_t1(V3 n) {  // mju_makeFrame's first tangent
 // term belongs to the normal); the solver forms them from these rows.  An arm block entry is the
 // motion subspace of dof d seen at the contact point, a cube block the free-body Jacobian.  Rows the
 // contact's condim does not use are zero rows with D = 0.  Returns the row's mu (-1: no edges).
-DEV float contact_row(EnvSh& E, int row, int c, int rr) {
+#ifndef MMX_CONPAR_SHFL
+#define MMX_CONPAR_SHFL 1  // 1: each contact's parameters computed once (its lane), read by its rows' lanes
+#endif
+DEV float contact_row(EnvSh& E, int row, int c, int rr, const ConPar& P) {
   const float* cc = E.con[c];
   const V3 p = V3{cc[CL_POS], cc[CL_POS + 1], cc[CL_POS + 2]};
   const V3 n = V3{cc[CL_N], cc[CL_N + 1], cc[CL_N + 2]};
   const int b1 = (E.conkey[c] >> 16) & 255, b2 = (E.conkey[c] >> 24) & 255;
-  const ConPar P = contact_params(cc, b1, b2);
   const int dim = P.dim;
   const bool used = rr == 0 || (rr < 3 && dim >= 3) || (rr == 3 && dim >= 4);
   const V3 t1 = contact_t1(n);
@@ -1317,6 +1319,8 @@ DEV void make_constraints_wave(EnvSh& E) {
       if ((side == 0 ? lo_act : hi_act) && row < MMX_MAXEFC) rowmap_set(row++, -1);  // joint limits
   }
   PROBE(3, stats, STAT_T_AUX1);
+  ConPar Pc{1, 0.f, 0.f, 0.f, 0.f, 1.f};  // lane c: contact c's parameters (MMX_CONPAR_SHFL)
+  if (MMX_CONPAR_SHFL && LANE < ncon) Pc = contact_params(E.con[LANE], (E.conkey[LANE] >> 16) & 255, (E.conkey[LANE] >> 24) & 255);
   if (LANE < ncon) {  // the contact's 4 basis rows in the row -> (contact, basis row) map
 #pragma unroll
     for (int rr = 0; rr < 4; rr++)
@@ -1331,10 +1335,21 @@ DEV void make_constraints_wave(EnvSh& E) {
   for (int q = 0; q < RPB; q++) {
     const int r = LANE + WG * q;
     mu[q] = 0.f;
-    if (r < nefc) {
-      const int m = __float_as_int(dget(E, r));
-      if (m >= 0) mu[q] = contact_row(E, r, m & 255, m >> 8);
+    if (WG * q >= nefc) continue;  // uniform: no row in this slice
+    const int m = r < nefc ? __float_as_int(dget(E, r)) : -1;
+    const int c = m >= 0 ? (m & 255) : 0;
+    ConPar P;
+    if (MMX_CONPAR_SHFL) {  // contact c's parameters from lane c (every lane takes part in the exchange)
+      P.dim = __shfl(Pc.dim, c);
+      P.mu0 = __shfl(Pc.mu0, c);
+      P.mu1 = __shfl(Pc.mu1, c);
+      P.kid = __shfl(Pc.kid, c);
+      P.B = __shfl(Pc.B, c);
+      P.idiag = __shfl(Pc.idiag, c);
+    } else if (m >= 0) {
+      P = contact_params(E.con[c], (E.conkey[c] >> 16) & 255, (E.conkey[c] >> 24) & 255);
     }
+    if (m >= 0) mu[q] = contact_row(E, r, c, m >> 8, P);
   }
   row = arow;
   float jv[16];

@@ -87,14 +87,14 @@ def test_physics_parity_one_substep(margin):  # L1: fp32 GPU vs fp64 oracle, con
 
 
 def test_step_layout_api():
-    """mmx_set_step_rows / mmx_step_rows: 128 rows (ten envs per CU) without cameras, 192 (eight)
-    with them, settable to either, anything else rejected."""
+    """mmx_set_step_rows / mmx_step_rows: 128 rows (eleven envs per CU) by default, with or without
+    cameras, 192 (eight) on request, anything else rejected."""
     from mujoco_manip_amd import _lib
 
     a = _lib.Sim(8, action_mode="abs_pos", image_size=0)
     b = _lib.Sim(8, action_mode="abs_pos", image_size=32)
     try:
-        assert a.step_rows == 128 and b.step_rows == 192
+        assert a.step_rows == 128 and b.step_rows == 128
         a.step_rows = 192
         assert a.step_rows == 192
         with pytest.raises(RuntimeError):
