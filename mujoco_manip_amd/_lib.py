@@ -391,7 +391,7 @@ class Sim:
 
     @property
     def step_rows(self) -> int:
-        """Constraint rows the env-step kernel keeps in LDS (128: ten envs per CU; 192: eight)."""
+        """Constraint rows the env-step kernel keeps in LDS (128: eleven envs per CU; 192: eight)."""
         return int(self.L.mmx_step_rows(self.ptr))
 
     @step_rows.setter

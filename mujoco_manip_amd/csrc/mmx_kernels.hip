@@ -62,7 +62,7 @@ static constexpr int kBinBody[3] = {MMX_BODY_BIN_RED, MMX_BODY_BIN_GREEN, MMX_BO
 
 #define NSLOT 14  // arm bodies 1..11 -> slots 0..10, cubes 16..18 -> slots 11..13
 #ifndef MMX_CAND_CAP
-#define MMX_CAND_CAP 160      // persistent broadphase list entries (pair indices)
+#define MMX_CAND_CAP 144      // persistent broadphase list entries (pair indices; a longer list is not kept: full prune)
 #endif
 #ifndef MMX_CAND_MARGIN
 #define MMX_CAND_MARGIN 0.08f  // m: the list's inflation of the sphere / plane test (A/B: 0.04 +0.2 %, 0.08 +0.8 %, 0.15 -0.6 %)
@@ -75,22 +75,28 @@ static constexpr int kBinBody[3] = {MMX_BODY_BIN_RED, MMX_BODY_BIN_GREEN, MMX_BO
 #endif
 
 // ============================================================================ per-env LDS
-enum { CL_DIST = 0, CL_POS = 1, CL_N = 4, CL_G1 = 7, CL_G2 = 8, CL_F };
+// LDS contact record: distance, position, normal and one int (bits): the 15-bit order key (pair x 8 +
+// local order, the sort key) | geom 1 << 16 | geom 2 << 22 (the bodies are the geoms' bodies)
+enum { CL_DIST = 0, CL_POS = 1, CL_N = 4, CL_KEY = 7, CL_F };
+static_assert(MMX_NGEOM <= 64 && MMX_NPAIR * 8 < 65536, "contact key packing");
+DEV int con_key(const float* c) { return __float_as_int(c[CL_KEY]); }
+DEV int con_g1(const float* c) { return (con_key(c) >> 16) & 63; }
+DEV int con_g2(const float* c) { return (con_key(c) >> 22) & 63; }
 struct EnvSh {
-  float qpos[30], qvel[28], ctrl[8], ws[28];
+  float qpos[30], qvel[28], ctrl[8];
   float target[4];
   float bx[NSLOT][3], bR[NSLOT][9];
   float S[9][6];
   // mass matrix: the arm's 9 x 9 block (the 3 free cubes are separate trees whose 6 x 6 blocks are
   // diagonal: mass x3, principal inertia x3, centre of mass at the joint)
   float M9[9][9];
-  float Mc[18];
+  // x: the Newton solution; between solves it holds the warm start for the next one (MuJoCo's
+  // qacc_warmstart: the record's qacc_ws is loaded into it and stored from it)
   float qfrc[LD], qacc_s[LD], x[LD], p[LD];
-  // contacts in LDS: 9 floats each (CL_*); the pair's friction and condim are table lookups of the
+  // contacts in LDS: 8 floats each (CL_*); the pair's friction and condim are table lookups of the
   // two geoms (MuJoCo mixing: max), recomputed where needed, so the 13-field HBM record (CON_*,
   // include/mmx_api.h) is filled only when the contacts are stored
   float con[MMX_MAXCON][CL_F];
-  int conkey[MMX_MAXCON];
   // constraint rows in block format: a row touches at most two dof blocks (arm = 9 dofs,
   // cube k = 6 dofs); J[i][0..n0) holds block b0's columns, J[i][n0..n0+n1) block b1's;
   // J doubles as the contact-sort scratch in collide_wave (rows are built after it).
@@ -134,10 +140,12 @@ struct EnvSh {
 // The workgroup's env lives in one file-scope LDS object: the non-inlined substep function below
 // reaches it by symbol (LDS address space), not through a generic pointer.
 static __shared__ EnvSh g_E;
-// eleven workgroups (envs) per CU share its 160 KiB of LDS: the occupancy the kernel is tuned for (r05;
+// eleven workgroups (envs) per CU share its 160 KiB of LDS, allocated in 1,280-byte blocks (measured:
+// tools/calib/lds_occ.hip, profiles/r05_lds_residency.json): the occupancy the kernel is tuned for (r05;
 // with 192 LDS rows, MMX_LDSEFC=192, eight)
-static_assert(MMX_LDSEFC != 128 || sizeof(EnvSh) <= 160 * 1024 / 11, "EnvSh no longer fits 11 envs per CU");
-static_assert(sizeof(EnvSh) <= 160 * 1024 / 8, "EnvSh no longer fits 8 envs per CU");
+static_assert(MMX_LDSEFC != 128 || (sizeof(EnvSh) + 1279) / 1280 * 1280 * 11 <= 160 * 1024,
+              "EnvSh no longer fits 11 envs per CU");
+static_assert((sizeof(EnvSh) + 1279) / 1280 * 1280 * 8 <= 160 * 1024, "EnvSh no longer fits 8 envs per CU");
 
 // The scratch region: E.J, E.hdr, E.D and E.NC (contiguous in EnvSh) hold the phases' scratch outside
 // the constraint build + Newton solve (rows are rebuilt every substep): the collision layout below,
@@ -145,9 +153,9 @@ static_assert(sizeof(EnvSh) <= 160 * 1024 / 8, "EnvSh no longer fits 8 envs per 
 // dynamics (at COL_WORK) and the observation of the step end.  The Newton Hessian staging tile and
 // Cholesky transpose live in E.con instead (contacts are dead once the rows exist; the last substep
 // stores them to HBM first).
-// r05: 128 LDS rows (MMX_LDSEFC), this 2,400-float layout and 9-float contacts bring the env to
-// 14,800 B of LDS, eleven per CU (was 20,432 B with 192 rows: eight); rows past 128 go to the HBM
-// overflow block.
+// r05: 128 LDS rows (MMX_LDSEFC), this scratch layout, 8-float contacts, the warm start kept in E.x,
+// the cubes' mass entries as constants and a 144-pair broadphase list bring the env to 14,064 B of
+// LDS, eleven per CU (was 20,432 B with 192 rows: eight); rows past 128 go to the HBM overflow block.
 #define GXS 17        // geom record: world pose (x 3, R 9), rbound, type, box half extents (3)
 #define GX_RB 12
 #define GX_TYPE 13
@@ -189,6 +197,7 @@ DEV float* lrow_of(EnvSh& E) { return &E.con[0][0]; }  // Hessian staging tiles 
 // the general (cube-cube coupled) Cholesky's 27 x 27 transpose: rare, so in the env's HBM scratch
 // block after the overflow rows (MMX_OVF_F), not in LDS
 DEV float* arrow_of(EnvSh& E) { return E.ovf + 18 * MMX_OVFEFC; }
+
 // the rows' mu between the row build and the solver setup (E.con is dead once the rows exist)
 DEV float* mu_stage(EnvSh& E) { return &E.con[0][0]; }
 static_assert(MMX_MAXEFC <= MMX_MAXCON * CL_F, "row mu staging exceeds E.con");
@@ -232,7 +241,7 @@ DEV void store_contacts(float* dst, const EnvSh& E) {
   for (int c = LANE; c < MMX_MAXCON; c += WG) {  // the 13-field record (CON_*) of LDS contact c
     float* o = dst + (size_t)c * CON_F;
     const float* l = E.con[c];
-    const int g1 = c < n ? (int)l[CL_G1] : 0, g2 = c < n ? (int)l[CL_G2] : 0;
+    const int g1 = c < n ? con_g1(l) : 0, g2 = c < n ? con_g2(l) : 0;
     o[CON_DIST] = c < n ? l[CL_DIST] : 0.f;
 #pragma unroll
     for (int k = 0; k < 3; k++) {
@@ -669,10 +678,7 @@ DEV void dynamics_wave(EnvSh& E) {
     if (d == e) v += MMX_dof_armature[d];
     E.M9[d][e] = v;
     E.M9[e][d] = v;
-  } else if (LANE < 45 + 18) {
-    const int k = LANE - 45, c = k / 6, rr = k % 6, b = 16 + c;
-    E.Mc[k] = rr < 3 ? MMX_body_mass[b] : MMX_body_inertia[9 * b + 4 * (rr - 3)];
-  }
+  }  // (the cubes' diagonal blocks are model constants: mass_cube)
   SYNC();
   PROBE(11, stats, STAT_T_AUX1);
   // smooth force: passive damping - bias + actuation (arm; one lane per actuator, then per dof),
@@ -756,11 +762,11 @@ struct WaveSink {
   int key;
   bool store;
   bool ro;
-  int bodies;  // geom bodies packed above the 16-bit order key: b1 << 16 | b2 << 24
+  int geoms;  // the geoms packed above the order key: g1 << 16 | g2 << 22
   int key0;
   DEV WaveSink(EnvSh* e, int p, bool st, int g1, int g2) : E(e), key(p * 8), store(st) {
     key0 = p * 8;
-    bodies = (MMX_geom_body[g1] << 16) | (MMX_geom_body[g2] << 24);
+    geoms = (g1 << 16) | (g2 << 22);
     const int c1 = MMX_geom_class[g1], c2 = MMX_geom_class[g2];
     ro = (c1 == 1 && c2 == 2) || (c1 == 2 && c2 == 1);
   }
@@ -790,9 +796,7 @@ struct WaveSink {
     c[CL_DIST] = dist;
     c[CL_POS] = pos.x; c[CL_POS + 1] = pos.y; c[CL_POS + 2] = pos.z;
     c[CL_N] = nrm.x; c[CL_N + 1] = nrm.y; c[CL_N + 2] = nrm.z;
-    c[CL_G1] = (float)g1;
-    c[CL_G2] = (float)g2;
-    E->conkey[slot] = (key++) | bodies;
+    c[CL_KEY] = __int_as_float((key++) | geoms);
   }
 };
 
@@ -1074,15 +1078,14 @@ DEV void collide_sort(EnvSh& E) {
   const int n = min(E.ncon, MMX_MAXCON);
   float* tmp = scr + COL_WORK;
   int kb = 0, rank = 0;
-  if (LANE < n) {  // rank by the 16-bit order key; the packed bodies travel with the record
-    kb = E.conkey[LANE];
+  if (LANE < n) {  // rank by the order key (the key word, with the geoms, travels with the record)
+    kb = con_key(E.con[LANE]);
     const int key = kb & 0xFFFF;
-    for (int j = 0; j < n; j++) rank += (E.conkey[j] & 0xFFFF) < key;
+    for (int j = 0; j < n; j++) rank += (con_key(E.con[j]) & 0xFFFF) < key;
 #pragma unroll
     for (int f = 0; f < CL_F; f++) tmp[rank * CL_F + f] = E.con[LANE][f];
   }
   SYNC();
-  if (LANE < n) E.conkey[rank] = kb;
   for (int k = LANE; k < n * CL_F; k += WG) (&E.con[0][0])[k] = tmp[k];
   if (LANE == 0) E.ncon = n;
   SYNC();
@@ -1133,8 +1136,8 @@ struct ConPar {
   int dim;
   float mu0, mu1, kid, B, idiag;
 };
-DEV ConPar contact_params(const float* cc, int b1, int b2) {
-  const int g1 = (int)cc[CL_G1], g2 = (int)cc[CL_G2];
+DEV ConPar contact_params(const float* cc) {
+  const int g1 = con_g1(cc), g2 = con_g2(cc);
   ConPar P;
   P.dim = max(MMX_geom_condim[g1], MMX_geom_condim[g2]);
   P.mu0 = fmaxf(MMX_geom_friction[3 * g1], MMX_geom_friction[3 * g2]);
@@ -1146,6 +1149,7 @@ DEV ConPar contact_params(const float* cc, int b1, int b2) {
   for (int k = 0; k < 5; k++) solimp[k] = 0.5f * (MMX_geom_solimp[5 * g1 + k] + MMX_geom_solimp[5 * g2 + k]);
   float impr;
   row_ref(solref, solimp, cc[CL_DIST], impr, P.kid, P.B);
+  const int b1 = MMX_geom_body[g1], b2 = MMX_geom_body[g2];
   const float tran = MMX_body_invweight0[2 * b1] + MMX_body_invweight0[2 * b2];
   const float it = impr * tran;  // (the pyramid's common R needs only the translational invweight)
   // pyramidal cone: one R for every edge, A_hat = 2 mu0^2 (tran + mu0^2 tran) / impratio (impratio
@@ -1172,7 +1176,7 @@ DEV float contact_row(EnvSh& E, int row, int c, int rr, const ConPar& P) {
   const float* cc = E.con[c];
   const V3 p = V3{cc[CL_POS], cc[CL_POS + 1], cc[CL_POS + 2]};
   const V3 n = V3{cc[CL_N], cc[CL_N + 1], cc[CL_N + 2]};
-  const int b1 = (E.conkey[c] >> 16) & 255, b2 = (E.conkey[c] >> 24) & 255;
+  const int b1 = MMX_geom_body[con_g1(cc)], b2 = MMX_geom_body[con_g2(cc)];
   const int dim = P.dim;
   const bool used = rr == 0 || (rr < 3 && dim >= 3) || (rr == 3 && dim >= 4);
   const V3 t1 = contact_t1(n);
@@ -1267,10 +1271,10 @@ DEV void make_constraints_wave(EnvSh& E) {
     nlim = (int)lo_act + (int)hi_act;
   }
   if (LANE < ncon) {
-    const int dim = max(MMX_geom_condim[(int)E.con[LANE][CL_G1]], MMX_geom_condim[(int)E.con[LANE][CL_G2]]);
+    const int g1 = con_g1(E.con[LANE]), g2 = con_g2(E.con[LANE]);
+    const int dim = max(MMX_geom_condim[g1], MMX_geom_condim[g2]);
     nedge = dim == 1 ? 1 : 2 * (dim - 1);
-    const int kb = E.conkey[LANE];
-    const int k1 = body_block((kb >> 16) & 255), k2 = body_block((kb >> 24) & 255);
+    const int k1 = body_block(MMX_geom_body[g1]), k2 = body_block(MMX_geom_body[g2]);
     int rb0 = k1 >= 0 ? k1 : k2, rb1 = (k1 >= 0 && k2 >= 0 && k2 != k1) ? k2 : BLK_NONE;
     if (rb1 != BLK_NONE && rb1 < rb0) {
       const int t = rb0;
@@ -1320,7 +1324,7 @@ DEV void make_constraints_wave(EnvSh& E) {
   }
   PROBE(3, stats, STAT_T_AUX1);
   ConPar Pc{1, 0.f, 0.f, 0.f, 0.f, 1.f};  // lane c: contact c's parameters (MMX_CONPAR_SHFL)
-  if (MMX_CONPAR_SHFL && LANE < ncon) Pc = contact_params(E.con[LANE], (E.conkey[LANE] >> 16) & 255, (E.conkey[LANE] >> 24) & 255);
+  if (MMX_CONPAR_SHFL && LANE < ncon) Pc = contact_params(E.con[LANE]);
   if (LANE < ncon) {  // the contact's 4 basis rows in the row -> (contact, basis row) map
 #pragma unroll
     for (int rr = 0; rr < 4; rr++)
@@ -1347,7 +1351,7 @@ DEV void make_constraints_wave(EnvSh& E) {
       P.B = __shfl(Pc.B, c);
       P.idiag = __shfl(Pc.idiag, c);
     } else if (m >= 0) {
-      P = contact_params(E.con[c], (E.conkey[c] >> 16) & 255, (E.conkey[c] >> 24) & 255);
+      P = contact_params(E.con[c]);
     }
     if (m >= 0) mu[q] = contact_row(E, r, c, m >> 8, P);
   }
@@ -1446,6 +1450,12 @@ DEV float row_dot16(const EnvSh& E, int i, const float* x) {
   return s;
 }
 
+// the cubes' diagonal mass matrix entry of free dof k (0..17: cube k / 6, mass x3 then principal
+// inertia x3): model constants, not per env
+DEV float mass_cube(int k) {
+  const int b = 16 + k / 6, rr = k % 6;
+  return rr < 3 ? MMX_body_mass[b] : MMX_body_inertia[9 * b + 4 * (rr - 3)];
+}
 // (M v) of the lane's dof (Newton lane layout; arm rows: the 9 x 9 block; cube rows: the diagonal)
 DEV float mass_mul(const EnvSh& E, const float* v) {
   const int nd = newton_dof(LANE);
@@ -1455,7 +1465,7 @@ DEV float mass_mul(const EnvSh& E, const float* v) {
     for (int b = 0; b < 9; b++) m = fmaf(E.M9[LANE][b], v[b], m);
     return m;
   }
-  return nd >= 0 ? E.Mc[nd - 9] * v[nd] : 0.f;
+  return nd >= 0 ? mass_cube(nd - 9) * v[nd] : 0.f;
 }
 // (M (xa - xb)) of the lane's dof, same layout
 DEV float mass_mul_diff(const EnvSh& E, const float* xa, const float* xb) {
@@ -1466,7 +1476,7 @@ DEV float mass_mul_diff(const EnvSh& E, const float* xa, const float* xb) {
     for (int b = 0; b < 9; b++) m = fmaf(E.M9[LANE][b], xa[b] - xb[b], m);
     return m;
   }
-  return nd >= 0 ? E.Mc[nd - 9] * (xa[nd] - xb[nd]) : 0.f;
+  return nd >= 0 ? mass_cube(nd - 9) * (xa[nd] - xb[nd]) : 0.f;
 }
 
 // Pyramid edges from basis rows.  Lane l owns rows l + 64 q; rows are 4-aligned groups, so a
@@ -1594,7 +1604,7 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
   const int nd = newton_dof(LANE), d = max(nd, 0);
   const int bd = nd >= 0 ? LANE >> 4 : -2, od = LANE & 15;
 #pragma unroll
-  for (int i = 0; i < 27; i++) hrow[i] = d < 9 ? (i < 9 ? E.M9[d][i] : 0.f) : (i == d ? E.Mc[d - 9] : 0.f);
+  for (int i = 0; i < 27; i++) hrow[i] = d < 9 ? (i < 9 ? E.M9[d][i] : 0.f) : (i == d ? mass_cube(d - 9) : 0.f);
   float gacc = 0.f;
   PROBE(6, stats, STAT_T_AUX3);
   // The non-empty row types go in rounds of up to HESS_TILES: each type's tile is staged in its
@@ -2023,10 +2033,10 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid, int& exit) 
   }
   // start from the cheaper of the warm start and qacc_smooth (as MuJoCo does)
   float c_ws, c_s, ra[RPL], rs[RPL], mws, ms;
-  cost2_wave(E, E.ws, E.qacc_s, mu, dd, c_ws, c_s, ra, rs, mws, ms);
+  cost2_wave(E, E.x, E.qacc_s, mu, dd, c_ws, c_s, ra, rs, mws, ms);
   const bool from_ws = c_ws < c_s;
   const int nd = newton_dof(LANE);  // the lane's dof in the Newton lane layout (-1: none)
-  if (nd >= 0) E.x[nd] = from_ws ? E.ws[nd] : E.qacc_s[nd];
+  if (nd >= 0) E.x[nd] = from_ws ? E.x[nd] : E.qacc_s[nd];
   float mdx = from_ws ? mws : ms;  // (M (x - xs))_lane, kept current through the iterations
   float scale = nd >= 0 ? E.qfrc[nd] * E.qfrc[nd] : 0.f;
   scale = sqrtf(wave_sum(scale)) + 1.f;
@@ -2264,7 +2274,7 @@ DEV void integrate_wave(EnvSh& E) {
   bool bad = false;
   if (LANE < 27) {
     const float qa = LANE < 9 ? qa_arm : E.x[LANE];
-    E.ws[LANE] = E.x[LANE];  // warm start keeps the constraint solver's qacc
+    // (E.x stays: it is the next solve's warm start, MuJoCo's qacc_warmstart)
     const float v = E.qvel[LANE] + kDt * qa;
     E.qvel[LANE] = v;
     // |v| or |qacc| >= 1e10, Inf or NaN (MuJoCo's mj_checkVel / mj_checkAcc bound mjMAXVAL): an
@@ -2673,7 +2683,7 @@ DEV void reset_lane0(const MMXState& S, int i, EnvSh& E, int task_override) {
 #pragma unroll
   for (int k = 0; k < 27; k++) {
     E.qvel[k] = 0.f;
-    E.ws[k] = 0.f;
+    E.x[k] = 0.f;
   }
 #pragma unroll
   for (int k = 0; k < 8; k++) E.ctrl[k] = MMX_key_ctrl[k];
@@ -2886,7 +2896,7 @@ DEV void load_env(const MMXState& S, int i, EnvSh& E) {
   if (LANE < 30) E.qpos[LANE] = S.qpos[(size_t)i * 30 + LANE];
   if (LANE < 27) {
     E.qvel[LANE] = S.qvel[(size_t)i * 27 + LANE];
-    E.ws[LANE] = S.qacc_ws[(size_t)i * 27 + LANE];
+    E.x[LANE] = S.qacc_ws[(size_t)i * 27 + LANE];
   }
   if (LANE < 8) E.ctrl[LANE] = S.ctrl[(size_t)i * 8 + LANE];
   if (LANE < KIN_N) kin_ref(E, LANE) = S.kin[(size_t)i * KIN_N + LANE];
@@ -2909,7 +2919,7 @@ DEV void store_env(const MMXState& S, int i, const EnvSh& E) {
   if (LANE < 30) S.qpos[(size_t)i * 30 + LANE] = E.qpos[LANE];
   if (LANE < 27) {
     S.qvel[(size_t)i * 27 + LANE] = E.qvel[LANE];
-    S.qacc_ws[(size_t)i * 27 + LANE] = E.ws[LANE];
+    S.qacc_ws[(size_t)i * 27 + LANE] = E.x[LANE];
   }
   if (LANE < 8) S.ctrl[(size_t)i * 8 + LANE] = E.ctrl[LANE];
   if (LANE < KIN_N) S.kin[(size_t)i * KIN_N + LANE] = kin_get(E, LANE);

@@ -17,8 +17,8 @@
 // constraint rows (basis rows: 4 per contact + equality / limits padded to 4; <= 64 x 4 + 20)
 #define MMX_MAXEFC 320
 // constraint rows [0, MMX_LDSEFC) live in the workgroup's LDS, rows [MMX_LDSEFC, MMX_MAXEFC) in the
-// env's HBM overflow block (efc_ovf); 128 rows (with 9-float LDS contacts) keep the env's LDS at
-// 14,800 B (11 envs per CU; r01-r04: 192 rows, 20 KB, 8 per CU)
+// env's HBM overflow block (efc_ovf); 128 rows keep the env's LDS at 14,064 B (11 envs per CU: the
+// LDS is allocated in 1,280-byte blocks, tools/calib/lds_occ.hip; r01-r04: 192 rows, 20 KB, 8 per CU)
 #ifndef MMX_LDSEFC
 #define MMX_LDSEFC 128
 #endif

@@ -106,7 +106,7 @@ def test_step_layout_api():
 
 
 def test_step_layouts_agree(margin):
-    """The two env-step kernel layouts (128 LDS rows + HBM overflow at ten envs per CU; 192 LDS rows
+    """The two env-step kernel layouts (128 LDS rows + HBM overflow at eleven envs per CU; 192 LDS rows
     at eight) run the same arithmetic: 1024 C3 envs in lockstep through their approach and grasp
     phases, where the contact piles put rows past 128 into the overflow block of the first layout
     only.  Over the first 20 env steps (approach, resting contacts) the states agree to 5e-4; over
