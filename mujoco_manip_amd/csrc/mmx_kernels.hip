@@ -79,9 +79,21 @@ static constexpr int kBinBody[3] = {MMX_BODY_BIN_RED, MMX_BODY_BIN_GREEN, MMX_BO
 // local order, the sort key) | geom 1 << 16 | geom 2 << 22 (the bodies are the geoms' bodies)
 enum { CL_DIST = 0, CL_POS = 1, CL_N = 4, CL_KEY = 7, CL_F };
 static_assert(MMX_NGEOM <= 64 && MMX_NPAIR * 8 < 65536, "contact key packing");
-DEV int con_key(const float* c) { return __float_as_int(c[CL_KEY]); }
-DEV int con_g1(const float* c) { return (con_key(c) >> 16) & 63; }
-DEV int con_g2(const float* c) { return (con_key(c) >> 22) & 63; }
+// contact c's record in the field-major array E.con[field][contact] (a lane reading its own contact
+// reads consecutive words: no LDS bank conflicts at the 8-float record size)
+struct CRec {
+  const float* b;
+  int c;
+  DEV float operator[](int k) const { return b[k * MMX_MAXCON + c]; }
+};
+struct CRecW {
+  float* b;
+  int c;
+  DEV float& operator[](int k) const { return b[k * MMX_MAXCON + c]; }
+};
+DEV int con_key(CRec c) { return __float_as_int(c[CL_KEY]); }
+DEV int con_g1(CRec c) { return (con_key(c) >> 16) & 63; }
+DEV int con_g2(CRec c) { return (con_key(c) >> 22) & 63; }
 struct EnvSh {
   float qpos[30], qvel[28], ctrl[8];
   float target[4];
@@ -96,7 +108,7 @@ struct EnvSh {
   // contacts in LDS: 8 floats each (CL_*); the pair's friction and condim are table lookups of the
   // two geoms (MuJoCo mixing: max), recomputed where needed, so the 13-field HBM record (CON_*,
   // include/mmx_api.h) is filled only when the contacts are stored
-  float con[MMX_MAXCON][CL_F];
+  float con[CL_F][MMX_MAXCON];  // field-major: E.con[k][c] = field k of contact c (crec)
   // constraint rows in block format: a row touches at most two dof blocks (arm = 9 dofs,
   // cube k = 6 dofs); J[i][0..n0) holds block b0's columns, J[i][n0..n0+n1) block b1's;
   // J doubles as the contact-sort scratch in collide_wave (rows are built after it).
@@ -193,6 +205,7 @@ DEV float* scr_of(EnvSh& E) { return reinterpret_cast<float*>(&E.J); }
 DEV const float* scr_of(const EnvSh& E) { return reinterpret_cast<const float*>(&E.J); }
 DEV float* obs_of(EnvSh& E) { return scr_of(E) + SCR_OBS; }
 DEV const float* obs_of(const EnvSh& E) { return scr_of(E) + SCR_OBS; }
+DEV CRec crec(const EnvSh& E, int c) { return CRec{&E.con[0][0], c}; }
 DEV float* lrow_of(EnvSh& E) { return &E.con[0][0]; }  // Hessian staging tiles (E.con is dead once the rows exist)
 // the general (cube-cube coupled) Cholesky's 27 x 27 transpose: rare, so in the env's HBM scratch
 // block after the overflow rows (MMX_OVF_F), not in LDS
@@ -240,7 +253,7 @@ DEV void store_contacts(float* dst, const EnvSh& E) {
   const int n = E.ncon;
   for (int c = LANE; c < MMX_MAXCON; c += WG) {  // the 13-field record (CON_*) of LDS contact c
     float* o = dst + (size_t)c * CON_F;
-    const float* l = E.con[c];
+    const CRec l = crec(E, c);
     const int g1 = c < n ? con_g1(l) : 0, g2 = c < n ? con_g2(l) : 0;
     o[CON_DIST] = c < n ? l[CL_DIST] : 0.f;
 #pragma unroll
@@ -792,7 +805,7 @@ struct WaveSink {
   DEV void put(int slot, int g1, int g2, float dist, V3 pos, V3 nrm) {
     if (slot >= MMX_MAXCON) return;
     nrm = normalize(nrm);
-    float* c = E->con[slot];
+    const CRecW c{&E->con[0][0], slot};
     c[CL_DIST] = dist;
     c[CL_POS] = pos.x; c[CL_POS + 1] = pos.y; c[CL_POS + 2] = pos.z;
     c[CL_N] = nrm.x; c[CL_N + 1] = nrm.y; c[CL_N + 2] = nrm.z;
@@ -1079,14 +1092,14 @@ DEV void collide_sort(EnvSh& E) {
   float* tmp = scr + COL_WORK;
   int kb = 0, rank = 0;
   if (LANE < n) {  // rank by the order key (the key word, with the geoms, travels with the record)
-    kb = con_key(E.con[LANE]);
+    kb = con_key(crec(E, LANE));
     const int key = kb & 0xFFFF;
-    for (int j = 0; j < n; j++) rank += (con_key(E.con[j]) & 0xFFFF) < key;
+    for (int j = 0; j < n; j++) rank += (con_key(crec(E, j)) & 0xFFFF) < key;
 #pragma unroll
-    for (int f = 0; f < CL_F; f++) tmp[rank * CL_F + f] = E.con[LANE][f];
+    for (int f = 0; f < CL_F; f++) tmp[f * MMX_MAXCON + rank] = E.con[f][LANE];
   }
   SYNC();
-  for (int k = LANE; k < n * CL_F; k += WG) (&E.con[0][0])[k] = tmp[k];
+  for (int k = LANE; k < MMX_MAXCON * CL_F; k += WG) (&E.con[0][0])[k] = tmp[k];
   if (LANE == 0) E.ncon = n;
   SYNC();
   PROBE(5, stats, STAT_T_AUX3);
@@ -1136,7 +1149,7 @@ struct ConPar {
   int dim;
   float mu0, mu1, kid, B, idiag;
 };
-DEV ConPar contact_params(const float* cc) {
+DEV ConPar contact_params(CRec cc) {
   const int g1 = con_g1(cc), g2 = con_g2(cc);
   ConPar P;
   P.dim = max(MMX_geom_condim[g1], MMX_geom_condim[g2]);
@@ -1173,7 +1186,7 @@ DEV V3 contact_t1(V3 n) {  // mju_makeFrame's first tangent
 #define MMX_CONPAR_SHFL 1  // 1: each contact's parameters computed once (its lane), read by its rows' lanes
 #endif
 DEV float contact_row(EnvSh& E, int row, int c, int rr, const ConPar& P) {
-  const float* cc = E.con[c];
+  const CRec cc = crec(E, c);
   const V3 p = V3{cc[CL_POS], cc[CL_POS + 1], cc[CL_POS + 2]};
   const V3 n = V3{cc[CL_N], cc[CL_N + 1], cc[CL_N + 2]};
   const int b1 = MMX_geom_body[con_g1(cc)], b2 = MMX_geom_body[con_g2(cc)];
@@ -1271,7 +1284,7 @@ DEV void make_constraints_wave(EnvSh& E) {
     nlim = (int)lo_act + (int)hi_act;
   }
   if (LANE < ncon) {
-    const int g1 = con_g1(E.con[LANE]), g2 = con_g2(E.con[LANE]);
+    const int g1 = con_g1(crec(E, LANE)), g2 = con_g2(crec(E, LANE));
     const int dim = max(MMX_geom_condim[g1], MMX_geom_condim[g2]);
     nedge = dim == 1 ? 1 : 2 * (dim - 1);
     const int k1 = body_block(MMX_geom_body[g1]), k2 = body_block(MMX_geom_body[g2]);
@@ -1324,7 +1337,7 @@ DEV void make_constraints_wave(EnvSh& E) {
   }
   PROBE(3, stats, STAT_T_AUX1);
   ConPar Pc{1, 0.f, 0.f, 0.f, 0.f, 1.f};  // lane c: contact c's parameters (MMX_CONPAR_SHFL)
-  if (MMX_CONPAR_SHFL && LANE < ncon) Pc = contact_params(E.con[LANE]);
+  if (MMX_CONPAR_SHFL && LANE < ncon) Pc = contact_params(crec(E, LANE));
   if (LANE < ncon) {  // the contact's 4 basis rows in the row -> (contact, basis row) map
 #pragma unroll
     for (int rr = 0; rr < 4; rr++)
@@ -1351,7 +1364,7 @@ DEV void make_constraints_wave(EnvSh& E) {
       P.B = __shfl(Pc.B, c);
       P.idiag = __shfl(Pc.idiag, c);
     } else if (m >= 0) {
-      P = contact_params(E.con[c]);
+      P = contact_params(crec(E, c));
     }
     if (m >= 0) mu[q] = contact_row(E, r, c, m >> 8, P);
   }
