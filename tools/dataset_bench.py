@@ -55,8 +55,8 @@ def main():
         if ep.index % 64 == 0:
             sample_memory()
         frames[0] += ep.length
-        if ep.index % 16 == 0:  # PNG size from every 16th episode (a per-frame sum costs the loop ~0.4 s)
-            png_bytes[0] += 16 * sum(len(b) for k in D.IMAGE_KEYS for b in ep.frames.get(k, []))
+        if ep.index % 16 == 0:  # PNG size from every 16th episode (PngFrames: its buffer's size)
+            png_bytes[0] += 16 * sum(D._png_nbytes(ep.frames.get(k, [])) for k in D.IMAGE_KEYS)
         if a.no_write:
             return
         writer.add_episode(ep)
