@@ -1932,8 +1932,13 @@ DEV float chol_block_arm(const float* hrow, float v, int cpla) {
       y = kk == k ? zk : (kk < k ? fmaf(-c[k], zk, y) : y);
     }
   }
+  // the coupled cube rows take the arm's final z: the arm lanes' y no longer changes here (cx = 0 off
+  // the coupled cubes), so the 9 reads are independent of the updates and issue back to back
+  float za[9];
 #pragma unroll
-  for (int i = 0; i < 9; i++) y = fmaf(-cx[i], readlane_f(y, i), y);  // (cx = 0 off the coupled cubes)
+  for (int i = 0; i < 9; i++) za[i] = readlane_f(y, i);
+#pragma unroll
+  for (int i = 0; i < 9; i++) y = fmaf(-cx[i], za[i], y);
 #pragma unroll
   for (int k = 5; k >= 0; k--) {
     const float zk = row_bcast(y, k) * dinv[k];
