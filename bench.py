@@ -455,14 +455,18 @@ def main():
         # mmx_render_kernel: per env of a launch, 2 cameras x S^2 x (RGB + segment id) bytes written
         # and the 14 body poses read; one launch per rollout lane and env step, lanes side by side
         S = args.image_size
-        rbytes = envs_per_launch * (2 * S * S * 4 + 14 * 12 * 4)
-        r_achieved = lanes * rbytes / (med["render_ms"] * 1e-3) / 1e9
+        # render launches per step: one over all envs after every lane's step (the default), or one
+        # per lane (MMX_RENDER_PHASED=0)
+        rl = max(1, env.sim.rollout_render_launches)
+        r_envs = N / rl
+        rbytes = r_envs * (2 * S * S * 4 + 14 * 12 * 4)
+        r_achieved = rl * rbytes / (med["render_ms"] * 1e-3) / 1e9
         rpmc = pmc_evidence("render", N, lanes)
-        render = {"kernel": "mmx_render_kernel", "kernel_ms": med["render_ms"], "concurrent_launches": lanes,
-                  "envs_per_launch": envs_per_launch, "image_size": S, "bytes_per_launch": rbytes,
+        render = {"kernel": "mmx_render_kernel", "kernel_ms": med["render_ms"], "launches_per_step": rl,
+                  "envs_per_launch": r_envs, "image_size": S, "bytes_per_launch": rbytes,
                   "bound": "valu", "hbm_achieved_GBs": r_achieved, "hbm_frac": r_achieved / HBM_PEAK_GBS,
                   "share_of_kernel_time": med["render_ms"] / (med["render_ms"] + kern_ms),
-                  "pixels_per_s": lanes * envs_per_launch * 2 * S * S / (med["render_ms"] * 1e-3),
+                  "pixels_per_s": rl * r_envs * 2 * S * S / (med["render_ms"] * 1e-3),
                   "valu": None if rpmc is None else rpmc.get("valu"), "isolated": isolated,
                   "note": "HBM is not the render kernel's roof (it writes 4 B per pixel); VALU issue is "
                           "(valu: SQ counters of tools/render_pmc.sh for this configuration)"}

@@ -156,6 +156,11 @@ int mmx_rollout_launches(const mmx_sim* sim, int32_t n_env_steps);
  * range per 1024 envs, at most 4).  Single-step calls always run as one launch on cfg.stream. */
 int mmx_rollout_lanes(const mmx_sim* sim);
 
+/* Render launches per rollout step with cameras: 1 (every lane's env-step launch first, then one
+ * render launch over all envs; the default) or mmx_rollout_lanes (a render per lane after its step,
+ * env MMX_RENDER_PHASED=0); 0 without cameras.  Timing only: the images are the same. */
+int mmx_rollout_render_launches(const mmx_sim* sim);
+
 /* Upper bound of the env steps one mmx_env_step_kernel launch runs per env in mmx_rollout_expert: 1
  * with cameras (every step is rendered), else 16 (env MMX_FUSE overrides).  A fused launch runs its
  * envs' steps back to back inside each workgroup; the trajectories are bit-identical to one

@@ -58,7 +58,7 @@ EXPORTED = ("mmx_config_default", "mmx_create", "mmx_destroy", "mmx_last_error",
             "mmx_synchronize", "mmx_get_state", "mmx_set_state", "mmx_episode_seed", "mmx_rollout_lanes",
             "mmx_rollout_steps_per_launch", "mmx_rollout_launches", "mmx_expert_physics", "mmx_eval_reward", "mmx_kernel_timing",
             "mmx_kernel_times", "mmx_png_bound", "mmx_png_scratch", "mmx_png_encode", "mmx_png_pack", "mmx_image_stats",
-            "mmx_queue_init", "mmx_queue_advance", "mmx_set_step_rows", "mmx_step_rows", "mmx_copy_ranges")
+            "mmx_queue_init", "mmx_queue_advance", "mmx_set_step_rows", "mmx_step_rows", "mmx_copy_ranges", "mmx_rollout_render_launches")
 
 _lib = None
 
@@ -89,6 +89,8 @@ def load(build_if_missing: bool = True):
     L.mmx_physics_step.argtypes = [vp, C.c_int32, C.c_int32]
     L.mmx_rollout_lanes.argtypes = [vp]
     L.mmx_rollout_lanes.restype = C.c_int
+    L.mmx_rollout_render_launches.argtypes = [vp]
+    L.mmx_rollout_render_launches.restype = C.c_int
     L.mmx_copy_ranges.argtypes = [C.c_int64, vp, vp, vp]
     L.mmx_copy_ranges.restype = C.c_int64
     L.mmx_set_step_rows.argtypes = [vp, C.c_int32]
@@ -388,6 +390,11 @@ class Sim:
     @property
     def rollout_lanes(self) -> int:
         return int(self.L.mmx_rollout_lanes(self.ptr))
+
+    @property
+    def rollout_render_launches(self) -> int:
+        """Render launches per rollout step with cameras (1: one over all envs after every lane's step)."""
+        return int(self.L.mmx_rollout_render_launches(self.ptr))
 
     @property
     def step_rows(self) -> int:

@@ -524,6 +524,14 @@ int mmx_rollout_launches(const mmx_sim* sim, int32_t n_env_steps) {
   return sim ? rollout_launches(sim, n_env_steps) : 0;
 }
 
+static bool render_phased() {
+  static const bool on = [] {
+    const char* v = std::getenv("MMX_RENDER_PHASED");
+    return !(v && std::atoi(v) == 0);
+  }();
+  return on;
+}
+
 int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
   if (!sim || sim->S.action_mode != MMX_ACTION_ABS_POS) return MMX_EINVAL;
   DeviceGuard guard(sim);
@@ -537,6 +545,10 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
   // k-1 of range l.  Without cameras a launch runs up to `fuse` consecutive steps of its envs
   // (mmx_rollout_steps_per_launch); with cameras every step is rendered, one step per launch.
   const int nl = rollout_launches(sim, n_env_steps);
+  // with cameras: every lane's step, then ONE render launch over all envs (the render's 80 KB
+  // workgroups cannot share a CU with the step kernel's, so a render per lane beside the other lanes'
+  // steps ran as a trickle: C5 +2.8 % phased); MMX_RENDER_PHASED=0 restores per-lane
+  const bool phased = render_phased();
   for (int r = 0; r < nl && e == hipSuccess; r++) {
     const int ns = n_env_steps / nl + (r < n_env_steps % nl ? 1 : 0);
     for (int l = 0; l < L && e == hipSuccess; l++) {
@@ -544,8 +556,18 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
       hipStream_t st = l ? sim->lane[l] : sim->stream;
       e = timed(sim, st, sim->t_step,
                 [&] { return launch_step(sim, sim->expert_action, 4, 1, b0, b1 - b0, ns, st); });
-      if (e == hipSuccess && sim->S.image_size > 0)
+      if (e == hipSuccess && sim->S.image_size > 0 && !(phased && L > 1))
         e = timed(sim, st, sim->t_render, [&] { return mmx_launch_render(&sim->S, b0, b1 - b0, st); });
+    }
+    if (e == hipSuccess && sim->S.image_size > 0 && phased && L > 1) {
+      for (int l = 1; l < L && e == hipSuccess; l++) {  // join the lanes' steps
+        e = hipEventRecord(sim->ev_join[l], sim->lane[l]);
+        if (e == hipSuccess) e = hipStreamWaitEvent(sim->stream, sim->ev_join[l], 0);
+      }
+      if (e == hipSuccess)
+        e = timed(sim, sim->stream, sim->t_render, [&] { return mmx_launch_render(&sim->S, 0, N, sim->stream); });
+      if (e == hipSuccess) e = hipEventRecord(sim->ev_fork, sim->stream);  // fork again
+      for (int l = 1; l < L && e == hipSuccess; l++) e = hipStreamWaitEvent(sim->lane[l], sim->ev_fork, 0);
     }
   }
   if (L > 1)  // join: the caller's stream sees the whole rollout, as with a single launch chain
@@ -558,6 +580,10 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
 }
 
 int mmx_rollout_lanes(const mmx_sim* sim) { return sim ? sim->nlanes : 0; }
+int mmx_rollout_render_launches(const mmx_sim* sim) {
+  if (!sim || sim->S.image_size <= 0) return 0;
+  return (render_phased() || sim->nlanes <= 1) ? 1 : sim->nlanes;
+}
 
 // the row-above match uses deflate distance 3 W + 1, which deflate caps at 32768: W <= 10922
 static bool png_size_ok(int32_t width, int32_t height) {
