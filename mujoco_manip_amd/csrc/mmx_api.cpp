@@ -18,9 +18,10 @@
 
 extern "C" hipError_t mmx_launch_reset(const MMXState* S, const unsigned char* mask, const int* task, hipStream_t st);
 extern "C" hipError_t mmx_launch_step(const MMXState* S, const float* action, int adim, int expert_autoreset,
-                                      int base, int count, int nsteps, hipStream_t st);
+                                      int base, int count, int nsteps, hipStream_t st, const int* order);
 extern "C" hipError_t mmx_launch_step_l192(const MMXState* S, const float* action, int adim, int expert_autoreset,
-                                           int base, int count, int nsteps, hipStream_t st);
+                                           int base, int count, int nsteps, hipStream_t st, const int* order);
+extern "C" hipError_t mmx_launch_order(const MMXState* S, int base, int count, int* order, hipStream_t st);
 extern "C" hipError_t mmx_launch_expert(const MMXState* S, int n, float* action, hipStream_t st);
 extern "C" hipError_t mmx_launch_physics(const MMXState* S, int n, int with_ik, hipStream_t st);
 extern "C" hipError_t mmx_launch_forward(const MMXState* S, hipStream_t st);
@@ -52,6 +53,7 @@ struct mmx_sim {
   float* expert_action;  // [N][4]
   unsigned char* d_mask;
   int* d_task;
+  int* d_order;  // [N] dispatch order of the rollout's step launches (MMX_STEP_ORDER)
   // Multi-step rollouts split the envs into `nlanes` independent ranges, each stepped on its own
   // stream (lane 0 = the caller's stream): the ranges never wait for each other between steps,
   // so one range's last-wave tail overlaps the next step of the others.
@@ -301,6 +303,7 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
   sim->expert_action = dalloc<float>(sim, 4 * n);
   sim->d_mask = dalloc<unsigned char>(sim, n);
   sim->d_task = dalloc<int>(sim, n);
+  sim->d_order = dalloc<int>(sim, n);
   if (cfg->image_size > 0) {  // camera renderer (mmx_render.hip): poses + RGB + segment ids
     const size_t px = static_cast<size_t>(cfg->image_size) * cfg->image_size;
     S.rpose = dalloc<float>(sim, 14 * 12 * n);
@@ -314,7 +317,7 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
       mmx_destroy(sim);
       return MMX_ENOMEM;
     }
-  if (!S.qpos || !S.con || !S.efc_ovf || !sim->d_task) {
+  if (!S.qpos || !S.con || !S.efc_ovf || !sim->d_task || !sim->d_order) {
     mmx_destroy(sim);
     return MMX_ENOMEM;
   }
@@ -432,9 +435,18 @@ int mmx_reset(mmx_sim* sim, const uint64_t* seeds, const uint8_t* seed_given, co
 
 namespace {
 static hipError_t launch_step(const mmx_sim* sim, const float* action, int adim, int expert, int base, int count, int nsteps,
-                       hipStream_t st) {
-  return sim->step_rows == 192 ? mmx_launch_step_l192(&sim->S, action, adim, expert, base, count, nsteps, st)
-                               : mmx_launch_step(&sim->S, action, adim, expert, base, count, nsteps, st);
+                              hipStream_t st, const int* order = nullptr) {
+  return sim->step_rows == 192 ? mmx_launch_step_l192(&sim->S, action, adim, expert, base, count, nsteps, st, order)
+                               : mmx_launch_step(&sim->S, action, adim, expert, base, count, nsteps, st, order);
+}
+// the rollout launches each env range longest-first (mmx_order_kernel: C3 / C5 +1.5 %);
+// MMX_STEP_ORDER=0 launches it in index order
+static bool step_order() {
+  static const bool on = [] {
+    const char* v = std::getenv("MMX_STEP_ORDER");
+    return !(v && std::atoi(v) == 0);
+  }();
+  return on;
 }
 }  // namespace
 
@@ -554,8 +566,11 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
     for (int l = 0; l < L && e == hipSuccess; l++) {
       const int b0 = (int)((long)N * l / L), b1 = (int)((long)N * (l + 1) / L);
       hipStream_t st = l ? sim->lane[l] : sim->stream;
-      e = timed(sim, st, sim->t_step,
-                [&] { return launch_step(sim, sim->expert_action, 4, 1, b0, b1 - b0, ns, st); });
+      int* ord = step_order() ? sim->d_order + b0 : nullptr;  // the lane's slice of the order buffer
+      if (ord) e = mmx_launch_order(&sim->S, b0, b1 - b0, ord, st);
+      if (e == hipSuccess)
+        e = timed(sim, st, sim->t_step,
+                  [&] { return launch_step(sim, sim->expert_action, 4, 1, b0, b1 - b0, ns, st, ord); });
       if (e == hipSuccess && sim->S.image_size > 0 && !(phased && L > 1))
         e = timed(sim, st, sim->t_render, [&] { return mmx_launch_render(&sim->S, b0, b1 - b0, st); });
     }

@@ -3158,8 +3158,10 @@ extern "C" int mmx_fsm_profile_fields() { return FSMP_N; }
 #define MMX_CAT_(a, b) MMX_CAT2_(a, b)
 #define MMX_STEP_SYM(name) MMX_CAT_(name, MMX_STEP_SUFFIX)
 extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MMX_STEP_WAVES, MMX_STEP_WAVES)))
-MMX_STEP_SYM(mmx_env_step_kernel)(MMXState S, const float* action, int adim, int expert, int base, int nsteps) {
-  const int i = base + blockIdx.x;
+MMX_STEP_SYM(mmx_env_step_kernel)(MMXState S, const float* action, int adim, int expert, int base, int nsteps,
+                                  const int* order) {
+  // order (optional): the launch's envs in dispatch order, the grasp-carrying ones first (mmx_order_kernel)
+  const int i = order ? order[blockIdx.x] : base + blockIdx.x;
   if (i >= S.N) return;
   for (int k = 0; k < nsteps; k++) {
     if (k) {  // the previous step's record stores complete before this step reloads it
@@ -3369,7 +3371,41 @@ extern "C" __global__ void __launch_bounds__(QWG) mmx_queue_kernel(MMXState S, M
   if (t == 0) *Q.next = min(Q.n_ep, base + scan[QWG - 1]);
 }
 
+// Dispatch order of an env range for the step kernel, longest first.  An env step's cycles follow its
+// FSM phase (profiles/r05_fsm_profile.json, cycles per env step): lift / move to bin / lower to bin
+// ~2.35 M, close gripper / settle ~2.0 M, release / retreat ~1.63 M, the rest ~1.3-1.42 M.  A counting
+// sort over those four classes puts the long ones at the front of order[], so the launch's last
+// workgroups are short ones (C3 / C5 +1.5 %).  One workgroup; the order within a class is
+// whatever the atomics give (the envs are independent: results do not depend on it).
+DEV int step_cost_class(int fsm_state) {
+  switch (fsm_state) {
+    case 4: case 5: case 7: return 0;  // lift, move to bin, lower to bin (the object held)
+    case 3: case 6: return 1;          // close gripper, settle at bin
+    case 8: case 9: return 2;          // release, retreat
+    default: return 3;
+  }
+}
+extern "C" __global__ void __launch_bounds__(1024) mmx_order_kernel(MMXState S, int base, int count, int* order) {
+  __shared__ int cnt[4], off[4];
+  if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  for (int k = threadIdx.x; k < count; k += 1024)
+    atomicAdd(&cnt[step_cost_class(S.epi[(size_t)(base + k) * EPI_N + EPI_FSM_STATE])], 1);
+  __syncthreads();
+  if (threadIdx.x == 0) off[0] = 0, off[1] = cnt[0], off[2] = cnt[0] + cnt[1], off[3] = cnt[0] + cnt[1] + cnt[2];
+  __syncthreads();
+  for (int k = threadIdx.x; k < count; k += 1024) {
+    const int i = base + k;
+    order[atomicAdd(&off[step_cost_class(S.epi[(size_t)i * EPI_N + EPI_FSM_STATE])], 1)] = i;
+  }
+}
+
 // =========================================================================== host launchers
+extern "C" hipError_t mmx_launch_order(const MMXState* S, int base, int count, int* order, hipStream_t st) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(mmx_order_kernel, dim3(1), dim3(1024), 0, st, *S, base, count, order);
+  return hipGetLastError();
+}
 extern "C" hipError_t mmx_launch_queue(const MMXState* S, int* slot, int* next, int n_ep, const unsigned long long* rng,
                                        const int* qtask, unsigned char* mask, int* task, int* slot_out, int* fin_out,
                                        hipStream_t st) {
@@ -3393,11 +3429,11 @@ static size_t step_lds_pad() {
 }
 // envs [base, base+count): independent env ranges may run on separate streams
 extern "C" hipError_t MMX_STEP_SYM(mmx_launch_step)(const MMXState* S, const float* action, int adim, int expert, int base,
-                                                    int count, int nsteps, hipStream_t st) {
+                                                    int count, int nsteps, hipStream_t st, const int* order) {
   if (count <= 0 || nsteps <= 0) return hipSuccess;
   if (nsteps > 1 && !expert) return hipErrorInvalidValue;  // host actions: one env step per launch
   hipLaunchKernelGGL(MMX_STEP_SYM(mmx_env_step_kernel), dim3(count), dim3(64), step_lds_pad(), st, *S, action, adim, expert, base,
-                     nsteps);
+                     nsteps, order);
   return hipGetLastError();
 }
 #ifndef MMX_STEP_ONLY
