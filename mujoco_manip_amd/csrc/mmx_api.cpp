@@ -462,7 +462,11 @@ int mmx_step(mmx_sim* sim, const float* action_dev, int32_t action_dim) {
   DeviceGuard guard(sim);
   static const int kDim[5] = {4, 8, 10, 8, 10};
   if (action_dim < kDim[sim->S.action_mode]) return fail(sim, MMX_EINVAL, "action_dim too small for action_mode");
-  hipError_t e = launch_step(sim, action_dev, action_dim, 0, 0, sim->S.N, 1, sim->stream);
+  // longest first by FSM phase (the expert's plan keeps it current; with policy actions it stays idle
+  // and the order is index order up to ties)
+  int* ord = step_order() ? sim->d_order : nullptr;
+  hipError_t e = ord ? mmx_launch_order(&sim->S, 0, sim->S.N, ord, sim->stream) : hipSuccess;
+  if (e == hipSuccess) e = launch_step(sim, action_dev, action_dim, 0, 0, sim->S.N, 1, sim->stream, ord);
   if (e == hipSuccess) e = mmx_launch_render(&sim->S, 0, sim->S.N, sim->stream);
   return hip_check(sim, e, "mmx_step");
 }
