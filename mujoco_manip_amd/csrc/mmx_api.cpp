@@ -548,10 +548,16 @@ static bool render_phased() {
   return on;
 }
 
+// lanes of a rollout: with cameras (phased render) one — every step ends in a join for the render
+// anyway, and one launch orders all envs longest-first (C5 +2.0 % over 4 lanes)
+static int rollout_lanes(const mmx_sim* sim) {
+  return sim->S.image_size > 0 && render_phased() ? 1 : sim->nlanes;
+}
+
 int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
   if (!sim || sim->S.action_mode != MMX_ACTION_ABS_POS) return MMX_EINVAL;
   DeviceGuard guard(sim);
-  const int N = sim->S.N, L = n_env_steps > 1 ? sim->nlanes : 1;
+  const int N = sim->S.N, L = n_env_steps > 1 ? rollout_lanes(sim) : 1;
   hipError_t e = hipSuccess;
   if (L > 1) {  // fork: every lane starts after the work already queued on the caller's stream
     e = hipEventRecord(sim->ev_fork, sim->stream);
@@ -561,9 +567,10 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
   // k-1 of range l.  Without cameras a launch runs up to `fuse` consecutive steps of its envs
   // (mmx_rollout_steps_per_launch); with cameras every step is rendered, one step per launch.
   const int nl = rollout_launches(sim, n_env_steps);
-  // with cameras: every lane's step, then ONE render launch over all envs (the render's 80 KB
+  // with cameras: the step of all envs, then ONE render launch over all envs (the render's 80 KB
   // workgroups cannot share a CU with the step kernel's, so a render per lane beside the other lanes'
-  // steps ran as a trickle: C5 +2.8 % phased); MMX_RENDER_PHASED=0 restores per-lane
+  // steps ran as a trickle: C5 +2.8 % phased); MMX_RENDER_PHASED=0 restores lanes
+  // with a render each
   const bool phased = render_phased();
   for (int r = 0; r < nl && e == hipSuccess; r++) {
     const int ns = n_env_steps / nl + (r < n_env_steps % nl ? 1 : 0);
@@ -575,11 +582,11 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
       if (e == hipSuccess)
         e = timed(sim, st, sim->t_step,
                   [&] { return launch_step(sim, sim->expert_action, 4, 1, b0, b1 - b0, ns, st, ord); });
-      if (e == hipSuccess && sim->S.image_size > 0 && !(phased && L > 1))
+      if (e == hipSuccess && sim->S.image_size > 0 && !phased)
         e = timed(sim, st, sim->t_render, [&] { return mmx_launch_render(&sim->S, b0, b1 - b0, st); });
     }
-    if (e == hipSuccess && sim->S.image_size > 0 && phased && L > 1) {
-      for (int l = 1; l < L && e == hipSuccess; l++) {  // join the lanes' steps
+    if (e == hipSuccess && sim->S.image_size > 0 && phased) {
+      for (int l = 1; l < L && e == hipSuccess; l++) {  // join the lanes' steps (L = 1 unless n = 1)
         e = hipEventRecord(sim->ev_join[l], sim->lane[l]);
         if (e == hipSuccess) e = hipStreamWaitEvent(sim->stream, sim->ev_join[l], 0);
       }
@@ -598,7 +605,7 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
   return hip_check(sim, e, "mmx_rollout_expert");
 }
 
-int mmx_rollout_lanes(const mmx_sim* sim) { return sim ? sim->nlanes : 0; }
+int mmx_rollout_lanes(const mmx_sim* sim) { return sim ? rollout_lanes(sim) : 0; }
 int mmx_rollout_render_launches(const mmx_sim* sim) {
   if (!sim || sim->S.image_size <= 0) return 0;
   return (render_phased() || sim->nlanes <= 1) ? 1 : sim->nlanes;

@@ -398,7 +398,8 @@ def test_determinism_and_shard_independence():
 
 
 def test_rollout_lanes_bit_identical(monkeypatch):
-    """Concurrent env ranges on separate streams (mmx_rollout_lanes) change nothing but timing."""
+    """Concurrent env ranges on separate streams (mmx_rollout_lanes) change nothing but timing
+    (rollouts without cameras: with cameras a rollout runs on one lane)."""
     import oracle_py as O
     from mujoco_manip_amd.vec_env import PickPlaceVecEnv
 
@@ -407,7 +408,7 @@ def test_rollout_lanes_bit_identical(monkeypatch):
     for lanes in ("1", "3"):  # 3 lanes over 10 envs: ragged ranges 3/3/4
         monkeypatch.setenv("MMX_STREAMS", lanes)
         env = PickPlaceVecEnv(10, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
-                              autoreset=True)
+                              autoreset=True, image_size=0)
         assert env.sim.rollout_lanes == int(lanes)
         env.reset(seed=seeds)
         env.rollout_expert(40)

@@ -14,8 +14,9 @@ def main():
     ap.add_argument("--round", default="r03")
     ap.add_argument("--prof", default=os.path.join(REPO, "gpurun_out", "rpmc"))
     ap.add_argument("--last", type=int, default=32)
-    ap.add_argument("--wg-per-dispatch", type=int, default=2048 * 2)  # envs x cameras (128^2: both bands in one workgroup)
-    ap.add_argument("--px-per-dispatch", type=int, default=2048 * 2 * 128 * 128)
+    ap.add_argument("--wg-per-dispatch", type=int, default=8192 * 2)  # envs x cameras (128^2: both bands in one workgroup)
+    ap.add_argument("--px-per-dispatch", type=int, default=8192 * 2 * 128 * 128)
+    ap.add_argument("--lanes", type=int, default=1)  # the C5 rollout's lanes (bench.py matches on it)
     a = ap.parse_args()
     per = {}
     for f in glob.glob(os.path.join(a.prof, "**", "*counter_collection.csv"), recursive=True):
@@ -23,8 +24,8 @@ def main():
         for r in csv.DictReader(open(f, newline="")):
             if "mmx_render_kernel" not in r.get("Kernel_Name", ""):
                 continue
-            # the bench's per-step launches only (2048 envs x 2 cameras x 512 lanes); its isolated
-            # render timing (mmx_forward over all 8192 envs) launches 4x larger grids
+            # launches of the configured shape only (r05: one render of all 8192 envs x 2 cameras per
+            # step, the same grid as the bench's isolated render timing through mmx_forward)
             if int(r.get("Grid_Size") or 0) != a.wg_per_dispatch * 512:
                 continue
             d = (pas, int(r.get("Dispatch_Id") or r.get("Correlation_Id")))
@@ -35,14 +36,14 @@ def main():
         ds = sorted(d for d in per if d[0] == pas)[-a.last:]
         for k in per[ds[0]]:
             out[k] = sum(per[d][k] for d in ds) / len(ds)
-    res = {"kernel": "mmx_render_kernel", "source": "tools/render_pmc.sh (C5, 128^2, 2048 envs per dispatch)",
+    res = {"kernel": "mmx_render_kernel", "source": f"tools/render_pmc.sh (C5, 128^2, {a.wg_per_dispatch // 2} envs per dispatch)",
            "per_dispatch": out,
            "per_workgroup": {k: v / a.wg_per_dispatch for k, v in out.items()},
            "valu_issue_per_wave_cycle": out.get("SQ_ACTIVE_INST_VALU", 0) / max(out.get("SQ_WAVE_CYCLES", 1), 1),
            "valu_insts_per_px": out.get("SQ_INSTS_VALU", 0) * 64 / a.px_per_dispatch}
     # what bench.py's C5 line cites (its `render.valu`), tagged with the configuration measured
     waves_per_simd = 4  # 512-lane workgroups (8 waves), two per CU (LDS), 4 SIMDs
-    res["config"] = {"workload": "render", "envs_per_gpu": 8192, "env_steps_per_launch": 1, "lanes": 4}
+    res["config"] = {"workload": "render", "envs_per_gpu": 8192, "env_steps_per_launch": 1, "lanes": a.lanes}
     res["valu"] = {"bound": "valu-issue", "valu_insts_per_px": res["valu_insts_per_px"],
                    "active_inst_valu_per_wave_cycle": res["valu_issue_per_wave_cycle"],
                    "waves_per_simd": waves_per_simd, "frac": res["valu_issue_per_wave_cycle"] * waves_per_simd,
