@@ -21,7 +21,7 @@ extern "C" hipError_t mmx_launch_step(const MMXState* S, const float* action, in
                                       int base, int count, int nsteps, hipStream_t st, const int* order);
 extern "C" hipError_t mmx_launch_step_l192(const MMXState* S, const float* action, int adim, int expert_autoreset,
                                            int base, int count, int nsteps, hipStream_t st, const int* order);
-extern "C" hipError_t mmx_launch_order(const MMXState* S, int base, int count, int* order, hipStream_t st);
+extern "C" hipError_t mmx_launch_order(const MMXState* S, int base, int count, int* order, int threads, hipStream_t st);
 extern "C" hipError_t mmx_launch_expert(const MMXState* S, int n, float* action, hipStream_t st);
 extern "C" hipError_t mmx_launch_physics(const MMXState* S, int n, int with_ik, hipStream_t st);
 extern "C" hipError_t mmx_launch_forward(const MMXState* S, hipStream_t st);
@@ -465,7 +465,7 @@ int mmx_step(mmx_sim* sim, const float* action_dev, int32_t action_dim) {
   // longest first by FSM phase (the expert's plan keeps it current; with policy actions it stays idle
   // and the order is index order up to ties)
   int* ord = step_order() ? sim->d_order : nullptr;
-  hipError_t e = ord ? mmx_launch_order(&sim->S, 0, sim->S.N, ord, sim->stream) : hipSuccess;
+  hipError_t e = ord ? mmx_launch_order(&sim->S, 0, sim->S.N, ord, 1024, sim->stream) : hipSuccess;
   if (e == hipSuccess) e = launch_step(sim, action_dev, action_dim, 0, 0, sim->S.N, 1, sim->stream, ord);
   if (e == hipSuccess) e = mmx_launch_render(&sim->S, 0, sim->S.N, sim->stream);
   return hip_check(sim, e, "mmx_step");
@@ -578,7 +578,7 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
       const int b0 = (int)((long)N * l / L), b1 = (int)((long)N * (l + 1) / L);
       hipStream_t st = l ? sim->lane[l] : sim->stream;
       int* ord = step_order() ? sim->d_order + b0 : nullptr;  // the lane's slice of the order buffer
-      if (ord) e = mmx_launch_order(&sim->S, b0, b1 - b0, ord, st);
+      if (ord) e = mmx_launch_order(&sim->S, b0, b1 - b0, ord, L > 1 ? 64 : 1024, st);
       if (e == hipSuccess)
         e = timed(sim, st, sim->t_step,
                   [&] { return launch_step(sim, sim->expert_action, 4, 1, b0, b1 - b0, ns, st, ord); });

@@ -3375,8 +3375,9 @@ extern "C" __global__ void __launch_bounds__(QWG) mmx_queue_kernel(MMXState S, M
 // FSM phase (profiles/r05_fsm_profile.json, cycles per env step): lift / move to bin / lower to bin
 // ~2.35 M, close gripper / settle ~2.0 M, release / retreat ~1.63 M, the rest ~1.3-1.42 M.  A counting
 // sort over those four classes puts the long ones at the front of order[], so the launch's last
-// workgroups are short ones (C3 / C5 +1.5 %).  One workgroup; the order within a class is
-// whatever the atomics give (the envs are independent: results do not depend on it).
+// workgroups are short ones (C3 +2.0 %, C5 +3.8 %).  One workgroup of any size (a single
+// wave beside running step launches: it then fits a CU the step kernel fills); the order within a
+// class is whatever the atomics give (the envs are independent: results do not depend on it).
 DEV int step_cost_class(int fsm_state) {
   switch (fsm_state) {
     case 4: case 5: case 7: return 0;  // lift, move to bin, lower to bin (the object held)
@@ -3389,21 +3390,24 @@ extern "C" __global__ void __launch_bounds__(1024) mmx_order_kernel(MMXState S, 
   __shared__ int cnt[4], off[4];
   if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
   __syncthreads();
-  for (int k = threadIdx.x; k < count; k += 1024)
+  for (int k = threadIdx.x; k < count; k += blockDim.x)
     atomicAdd(&cnt[step_cost_class(S.epi[(size_t)(base + k) * EPI_N + EPI_FSM_STATE])], 1);
   __syncthreads();
   if (threadIdx.x == 0) off[0] = 0, off[1] = cnt[0], off[2] = cnt[0] + cnt[1], off[3] = cnt[0] + cnt[1] + cnt[2];
   __syncthreads();
-  for (int k = threadIdx.x; k < count; k += 1024) {
+  for (int k = threadIdx.x; k < count; k += blockDim.x) {
     const int i = base + k;
     order[atomicAdd(&off[step_cost_class(S.epi[(size_t)i * EPI_N + EPI_FSM_STATE])], 1)] = i;
   }
 }
 
 // =========================================================================== host launchers
-extern "C" hipError_t mmx_launch_order(const MMXState* S, int base, int count, int* order, hipStream_t st) {
+// threads: 1024 when the launch has the GPU to itself, 64 beside other streams' step launches (a
+// 1,024-lane workgroup waited ~0.35 ms for a CU to drain there: profiles/r05_c3_kernel_stats.csv)
+extern "C" hipError_t mmx_launch_order(const MMXState* S, int base, int count, int* order, int threads, hipStream_t st) {
   if (count <= 0) return hipSuccess;
-  hipLaunchKernelGGL(mmx_order_kernel, dim3(1), dim3(1024), 0, st, *S, base, count, order);
+  if (threads != 64 && threads != 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(mmx_order_kernel, dim3(1), dim3(threads), 0, st, *S, base, count, order);
   return hipGetLastError();
 }
 extern "C" hipError_t mmx_launch_queue(const MMXState* S, int* slot, int* next, int n_ep, const unsigned long long* rng,
