@@ -136,6 +136,15 @@ int64_t mmx_copy_ranges(int64_t n, const uint64_t* src, const uint64_t* dst, con
 int mmx_set_step_rows(mmx_sim* sim, int32_t rows);
 int mmx_step_rows(const mmx_sim* sim);
 
+/* Dispatch order of env-step launches (mmx_step, mmx_rollout_expert): 1 (default) = each launch's
+ * envs longest first by FSM phase (a one-workgroup counting sort before the launch: the envs holding
+ * an object, then closing / settling, then releasing, then the rest), 0 = env index order.  Env
+ * MMX_STEP_ORDER=0 sets 0 at create.  Only the hardware's workgroup schedule changes: results are
+ * bit-identical either way.  MMX_EINVAL for other values; mmx_step_order returns -1 for NULL.  (No
+ * reference counterpart: a scheduling choice of this implementation.) */
+int mmx_set_step_order(mmx_sim* sim, int32_t on);
+int mmx_step_order(const mmx_sim* sim);
+
 /* PickAndPlaceTask.plan(n_steps) (pick_and_place.py:167-277) for every env; writes the
  * abs_pos action [N][4] = (target_xyz, gripper_val) to action_dev_out (may be NULL). */
 int mmx_expert_plan(mmx_sim* sim, int32_t n_steps, float* action_dev_out);

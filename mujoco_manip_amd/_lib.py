@@ -58,7 +58,8 @@ EXPORTED = ("mmx_config_default", "mmx_create", "mmx_destroy", "mmx_last_error",
             "mmx_synchronize", "mmx_get_state", "mmx_set_state", "mmx_episode_seed", "mmx_rollout_lanes",
             "mmx_rollout_steps_per_launch", "mmx_rollout_launches", "mmx_expert_physics", "mmx_eval_reward", "mmx_kernel_timing",
             "mmx_kernel_times", "mmx_png_bound", "mmx_png_scratch", "mmx_png_encode", "mmx_png_pack", "mmx_image_stats",
-            "mmx_queue_init", "mmx_queue_advance", "mmx_set_step_rows", "mmx_step_rows", "mmx_copy_ranges", "mmx_rollout_render_launches")
+            "mmx_queue_init", "mmx_queue_advance", "mmx_set_step_rows", "mmx_step_rows", "mmx_copy_ranges", "mmx_rollout_render_launches",
+            "mmx_set_step_order", "mmx_step_order")
 
 _lib = None
 
@@ -96,6 +97,9 @@ def load(build_if_missing: bool = True):
     L.mmx_set_step_rows.argtypes = [vp, C.c_int32]
     L.mmx_step_rows.argtypes = [vp]
     L.mmx_step_rows.restype = C.c_int
+    L.mmx_set_step_order.argtypes = [vp, C.c_int32]
+    L.mmx_step_order.argtypes = [vp]
+    L.mmx_step_order.restype = C.c_int
     L.mmx_rollout_steps_per_launch.argtypes = [vp]
     L.mmx_rollout_steps_per_launch.restype = C.c_int
     L.mmx_rollout_launches.argtypes = [vp, C.c_int32]
@@ -123,7 +127,7 @@ def load(build_if_missing: bool = True):
     for name in ("mmx_create", "mmx_reset", "mmx_step", "mmx_expert_plan", "mmx_rollout_expert", "mmx_physics_step",
                  "mmx_forward", "mmx_get_buffers", "mmx_synchronize", "mmx_get_state", "mmx_set_state",
                  "mmx_expert_physics", "mmx_eval_reward", "mmx_kernel_timing", "mmx_kernel_times", "mmx_png_encode",
-                 "mmx_png_pack", "mmx_image_stats", "mmx_queue_init", "mmx_queue_advance", "mmx_set_step_rows"):
+                 "mmx_png_pack", "mmx_image_stats", "mmx_queue_init", "mmx_queue_advance", "mmx_set_step_rows", "mmx_set_step_order"):
         getattr(L, name).restype = C.c_int
     _lib = L
     return L
@@ -404,6 +408,16 @@ class Sim:
     @step_rows.setter
     def step_rows(self, rows: int):
         self._check(self.L.mmx_set_step_rows(self.ptr, int(rows)), "mmx_set_step_rows")
+
+    @property
+    def step_order(self) -> bool:
+        """Env-step launches dispatch their envs longest first by FSM phase (True, the default) or in
+        index order; results are bit-identical either way."""
+        return bool(self.L.mmx_step_order(self.ptr))
+
+    @step_order.setter
+    def step_order(self, on: bool):
+        self._check(self.L.mmx_set_step_order(self.ptr, 1 if on else 0), "mmx_set_step_order")
 
     @property
     def rollout_steps_per_launch(self) -> int:

@@ -65,6 +65,9 @@ struct mmx_sim {
   // (eight per CU, mmx_step_l192.hip: faster when the batch leaves CU slots empty; mmx_set_step_rows,
   // MMX_STEP_ROWS)
   int step_rows = 128;
+  // env steps launched longest first (mmx_order_kernel; mmx_set_step_order, MMX_STEP_ORDER=0 at
+  // create turns it off): the launch's order only, never its results
+  int step_order = 1;
   hipStream_t lane[kMaxLanes] = {};
   hipEvent_t ev_fork = nullptr, ev_join[kMaxLanes] = {};
   // per-launch kernel timing (mmx_kernel_timing): an event pair around every step / render launch
@@ -344,6 +347,8 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
     const int r = std::atoi(v);
     if (r == 128 || r == 192) sim->step_rows = r;
   }
+  sim->step_order = 1;
+  if (const char* v = std::getenv("MMX_STEP_ORDER")) sim->step_order = std::atoi(v) != 0;
   lanes = std::max(1, std::min(lanes, std::min(N, int(mmx_sim::kMaxLanes))));
   if (hipEventCreateWithFlags(&sim->ev_fork, hipEventDisableTiming) != hipSuccess) lanes = 1;
   for (int l = 1; l < lanes; l++)
@@ -439,15 +444,6 @@ static hipError_t launch_step(const mmx_sim* sim, const float* action, int adim,
   return sim->step_rows == 192 ? mmx_launch_step_l192(&sim->S, action, adim, expert, base, count, nsteps, st, order)
                                : mmx_launch_step(&sim->S, action, adim, expert, base, count, nsteps, st, order);
 }
-// the rollout launches each env range longest-first (mmx_order_kernel: C3 / C5 +1.5 %);
-// MMX_STEP_ORDER=0 launches it in index order
-static bool step_order() {
-  static const bool on = [] {
-    const char* v = std::getenv("MMX_STEP_ORDER");
-    return !(v && std::atoi(v) == 0);
-  }();
-  return on;
-}
 }  // namespace
 
 int mmx_set_step_rows(mmx_sim* sim, int32_t rows) {
@@ -456,6 +452,12 @@ int mmx_set_step_rows(mmx_sim* sim, int32_t rows) {
   return MMX_OK;
 }
 int mmx_step_rows(const mmx_sim* sim) { return sim ? sim->step_rows : 0; }
+int mmx_set_step_order(mmx_sim* sim, int32_t on) {
+  if (!sim || (on != 0 && on != 1)) return MMX_EINVAL;
+  sim->step_order = on;
+  return MMX_OK;
+}
+int mmx_step_order(const mmx_sim* sim) { return sim ? sim->step_order : -1; }
 
 int mmx_step(mmx_sim* sim, const float* action_dev, int32_t action_dim) {
   if (!sim || !action_dev) return MMX_EINVAL;
@@ -464,7 +466,7 @@ int mmx_step(mmx_sim* sim, const float* action_dev, int32_t action_dim) {
   if (action_dim < kDim[sim->S.action_mode]) return fail(sim, MMX_EINVAL, "action_dim too small for action_mode");
   // longest first by FSM phase (the expert's plan keeps it current; with policy actions it stays idle
   // and the order is index order up to ties)
-  int* ord = step_order() ? sim->d_order : nullptr;
+  int* ord = sim->step_order ? sim->d_order : nullptr;
   hipError_t e = ord ? mmx_launch_order(&sim->S, 0, sim->S.N, ord, 1024, sim->stream) : hipSuccess;
   if (e == hipSuccess) e = launch_step(sim, action_dev, action_dim, 0, 0, sim->S.N, 1, sim->stream, ord);
   if (e == hipSuccess) e = mmx_launch_render(&sim->S, 0, sim->S.N, sim->stream);
@@ -577,7 +579,7 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
     for (int l = 0; l < L && e == hipSuccess; l++) {
       const int b0 = (int)((long)N * l / L), b1 = (int)((long)N * (l + 1) / L);
       hipStream_t st = l ? sim->lane[l] : sim->stream;
-      int* ord = step_order() ? sim->d_order + b0 : nullptr;  // the lane's slice of the order buffer
+      int* ord = sim->step_order ? sim->d_order + b0 : nullptr;  // the lane's slice of the order buffer
       if (ord) e = mmx_launch_order(&sim->S, b0, b1 - b0, ord, L > 1 ? 64 : 1024, st);
       if (e == hipSuccess)
         e = timed(sim, st, sim->t_step,

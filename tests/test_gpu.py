@@ -105,6 +105,45 @@ def test_step_layout_api():
         b.close()
 
 
+def test_step_order_bit_identical(margin, monkeypatch):
+    """mmx_set_step_order: the longest-first dispatch order (default) changes only which workgroup the
+    hardware starts first, so 512 C3 envs (enough to spread over several FSM phases and the four
+    cost classes) end an expert rollout bit-identical to index order, through fused launches on two
+    rollout lanes (the single-wave sort) and through one mmx_step launch of all envs (the 1,024-lane
+    sort)."""
+    monkeypatch.setenv("MMX_STREAMS", "2")
+    import oracle_py as O
+    from mujoco_manip_amd import _lib
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    n = 512
+    seeds = [O.episode_seed(11, i) for i in range(n)]
+    outs = []
+    for on in (True, False):
+        env = PickPlaceVecEnv(n, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
+                              autoreset=True, image_size=0)
+        assert env.sim.step_order is True and env.sim.rollout_lanes == 2  # the default order
+        env.sim.step_order = on
+        assert env.sim.step_order is on
+        with pytest.raises(RuntimeError):
+            env.sim._check(env.sim.L.mmx_set_step_order(env.sim.ptr, 2), "mmx_set_step_order")
+        env.reset(seed=seeds)
+        env.rollout_expert(96)  # fused launches on the rollout lanes
+        act = torch.zeros(n, 4, device="cuda")
+        env.sim.expert_plan(1, act.data_ptr())
+        env.sim.step(act.data_ptr(), 4)  # one mmx_step launch of all envs
+        torch.cuda.synchronize()
+        q, v, _, _ = env.sim.get_state()
+        fsm = env.sim.view("episode_i", _lib_epi_n(), "<i4").cpu().numpy()
+        outs.append((np.concatenate([q, v], 1), fsm))
+        env.close()
+    phases = np.unique(outs[0][1][:, _lib.EPI["fsm_state"]])
+    margin("fsm_phases_in_batch", int(len(phases)))
+    assert len(phases) >= 3, phases  # the order had more than one class to sort
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    np.testing.assert_array_equal(outs[0][1], outs[1][1])
+
+
 def test_step_layouts_agree(margin):
     """The two env-step kernel layouts (128 LDS rows + HBM overflow at eleven envs per CU; 192 LDS rows
     at eight) run the same arithmetic: 1024 C3 envs in lockstep through their approach and grasp
