@@ -138,7 +138,8 @@ int mmx_step_rows(const mmx_sim* sim);
 
 /* Dispatch order of env-step launches (mmx_step, mmx_rollout_expert): 1 (default) = each launch's
  * envs longest first by FSM phase (a one-workgroup counting sort before the launch: the envs holding
- * an object, then closing / settling, then releasing, then the rest), 0 = env index order.  Env
+ * an object, then closing / settling, then releasing, then the rest; within a phase class more
+ * constraint rows in the last substep first), 0 = env index order.  Env
  * MMX_STEP_ORDER=0 sets 0 at create.  Only the hardware's workgroup schedule changes: results are
  * bit-identical either way.  MMX_EINVAL for other values; mmx_step_order returns -1 for NULL.  (No
  * reference counterpart: a scheduling choice of this implementation.) */
