@@ -462,14 +462,21 @@ def main():
         rbytes = r_envs * (2 * S * S * 4 + 14 * 12 * 4)
         r_achieved = rl * rbytes / (med["render_ms"] * 1e-3) / 1e9
         rpmc = pmc_evidence("render", N, lanes)
+        # the default camera rollout renders step k on its own stream beside the step launch of step
+        # k + 1 (mmx_rollout_render_overlap): kernel_ms is then the render launch's span on that
+        # stream, shared with the step kernel; `isolated` is the render's own cost
+        overlap = bool(env.sim.rollout_render_overlap)
         render = {"kernel": "mmx_render_kernel", "kernel_ms": med["render_ms"], "launches_per_step": rl,
+                  "concurrent_with_step": overlap,
                   "envs_per_launch": r_envs, "image_size": S, "bytes_per_launch": rbytes,
                   "bound": "valu", "hbm_achieved_GBs": r_achieved, "hbm_frac": r_achieved / HBM_PEAK_GBS,
-                  "share_of_kernel_time": med["render_ms"] / (med["render_ms"] + kern_ms),
+                  "share_of_kernel_time": None if overlap else med["render_ms"] / (med["render_ms"] + kern_ms),
                   "pixels_per_s": rl * r_envs * 2 * S * S / (med["render_ms"] * 1e-3),
                   "valu": None if rpmc is None else rpmc.get("valu"), "isolated": isolated,
                   "note": "HBM is not the render kernel's roof (it writes 4 B per pixel); VALU issue is "
-                          "(valu: SQ counters of tools/render_pmc.sh for this configuration)"}
+                          "(valu: SQ counters of tools/render_pmc.sh for this configuration)" +
+                          ("; concurrent with the next step's launch: kernel_ms / pixels_per_s / hbm are "
+                           "per span on the render stream, isolated.forward_ms is the render alone" if overlap else "")}
     if rank == 0:
         pmc = pmc_evidence(args.workload, N, lanes)
         traffic = None if pmc is None else pmc["hbm_bytes_per_env_step"] * envs_per_launch * steps_per_launch

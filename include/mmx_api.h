@@ -171,6 +171,12 @@ int mmx_rollout_lanes(const mmx_sim* sim);
  * env MMX_RENDER_PHASED=0); 0 without cameras.  Timing only: the images are the same. */
 int mmx_rollout_render_launches(const mmx_sim* sim);
 
+/* 1 when camera rollouts (mmx_rollout_expert, more than one env step) render step k on a stream of
+ * their own beside the env-step launch of step k + 1, the body poses double-buffered (the default
+ * with cameras; env MMX_RENDER_OVERLAP=0 at create: render, then the next step); 0 otherwise.
+ * Timing only: images and states are bit-identical either way. */
+int mmx_rollout_render_overlap(const mmx_sim* sim);
+
 /* Upper bound of the env steps one mmx_env_step_kernel launch runs per env in mmx_rollout_expert: 1
  * with cameras (every step is rendered), else 16 (env MMX_FUSE overrides).  A fused launch runs its
  * envs' steps back to back inside each workgroup; the trajectories are bit-identical to one

@@ -59,7 +59,7 @@ EXPORTED = ("mmx_config_default", "mmx_create", "mmx_destroy", "mmx_last_error",
             "mmx_rollout_steps_per_launch", "mmx_rollout_launches", "mmx_expert_physics", "mmx_eval_reward", "mmx_kernel_timing",
             "mmx_kernel_times", "mmx_png_bound", "mmx_png_scratch", "mmx_png_encode", "mmx_png_pack", "mmx_image_stats",
             "mmx_queue_init", "mmx_queue_advance", "mmx_set_step_rows", "mmx_step_rows", "mmx_copy_ranges", "mmx_rollout_render_launches",
-            "mmx_set_step_order", "mmx_step_order")
+            "mmx_set_step_order", "mmx_step_order", "mmx_rollout_render_overlap")
 
 _lib = None
 
@@ -98,6 +98,8 @@ def load(build_if_missing: bool = True):
     L.mmx_step_rows.argtypes = [vp]
     L.mmx_step_rows.restype = C.c_int
     L.mmx_set_step_order.argtypes = [vp, C.c_int32]
+    L.mmx_rollout_render_overlap.argtypes = [vp]
+    L.mmx_rollout_render_overlap.restype = C.c_int
     L.mmx_step_order.argtypes = [vp]
     L.mmx_step_order.restype = C.c_int
     L.mmx_rollout_steps_per_launch.argtypes = [vp]
@@ -408,6 +410,11 @@ class Sim:
     @step_rows.setter
     def step_rows(self, rows: int):
         self._check(self.L.mmx_set_step_rows(self.ptr, int(rows)), "mmx_set_step_rows")
+
+    @property
+    def rollout_render_overlap(self) -> bool:
+        """Camera rollouts render step k beside the env-step launch of step k + 1 (timing only)."""
+        return bool(self.L.mmx_rollout_render_overlap(self.ptr))
 
     @property
     def step_order(self) -> bool:

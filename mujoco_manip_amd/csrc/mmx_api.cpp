@@ -70,6 +70,13 @@ struct mmx_sim {
   int step_order = 1;
   hipStream_t lane[kMaxLanes] = {};
   hipEvent_t ev_fork = nullptr, ev_join[kMaxLanes] = {};
+  // camera rollouts render step k on their own stream beside step k + 1 (MMX_RENDER_OVERLAP=0 at
+  // create: serial): the body poses alternate between S.rpose and rpose_alt; ev_step = the step
+  // launch done, ev_rend[k & 1] = render k done
+  int render_overlap = 0;
+  float* rpose_alt = nullptr;
+  hipStream_t rstream = nullptr;
+  hipEvent_t ev_step = nullptr, ev_rend[2] = {};
   // per-launch kernel timing (mmx_kernel_timing): an event pair around every step / render launch
   // on the stream it runs on; pairs come from a pool reused after each read-out
   bool timing = false;
@@ -310,6 +317,7 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
   if (cfg->image_size > 0) {  // camera renderer (mmx_render.hip): poses + RGB + segment ids
     const size_t px = static_cast<size_t>(cfg->image_size) * cfg->image_size;
     S.rpose = dalloc<float>(sim, 14 * 12 * n);
+    sim->rpose_alt = dalloc<float>(sim, 14 * 12 * n);
     S.images = dalloc<unsigned char>(sim, 2 * px * 3 * n);
     S.seg = dalloc<unsigned char>(sim, 2 * px * n);
     const size_t sg = static_cast<size_t>((cfg->image_size + 15) & ~15);
@@ -359,6 +367,13 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
       break;
     }
   sim->nlanes = lanes;
+  sim->render_overlap = sim->rpose_alt != nullptr;
+  if (const char* v = std::getenv("MMX_RENDER_OVERLAP")) sim->render_overlap = sim->render_overlap && std::atoi(v) != 0;
+  if (sim->render_overlap && (hipStreamCreateWithFlags(&sim->rstream, hipStreamNonBlocking) != hipSuccess ||
+                              hipEventCreateWithFlags(&sim->ev_step, hipEventDisableTiming) != hipSuccess ||
+                              hipEventCreateWithFlags(&sim->ev_rend[0], hipEventDisableTiming) != hipSuccess ||
+                              hipEventCreateWithFlags(&sim->ev_rend[1], hipEventDisableTiming) != hipSuccess))
+    sim->render_overlap = 0;
   // the fixed overhead camera's background, once; the handle is published only when the sim is
   // complete (on a failure every allocation is released and *out stays null)
   int rc = S.bg_overhead ? hip_check(sim, mmx_launch_render_bg(&S, sim->stream), "mmx_create background") : 0;
@@ -382,6 +397,9 @@ void mmx_destroy(mmx_sim* sim) {
     (void)hipStreamDestroy(sim->lane[l]);
   }
   if (sim->ev_fork) (void)hipEventDestroy(sim->ev_fork);
+  for (hipEvent_t ev : {sim->ev_step, sim->ev_rend[0], sim->ev_rend[1]})
+    if (ev) (void)hipEventDestroy(ev);
+  if (sim->rstream) (void)hipStreamDestroy(sim->rstream);
   for (hipEvent_t ev : sim->ev_pool) (void)hipEventDestroy(ev);
   delete sim;
 }
@@ -440,9 +458,10 @@ int mmx_reset(mmx_sim* sim, const uint64_t* seeds, const uint8_t* seed_given, co
 
 namespace {
 static hipError_t launch_step(const mmx_sim* sim, const float* action, int adim, int expert, int base, int count, int nsteps,
-                              hipStream_t st, const int* order = nullptr) {
-  return sim->step_rows == 192 ? mmx_launch_step_l192(&sim->S, action, adim, expert, base, count, nsteps, st, order)
-                               : mmx_launch_step(&sim->S, action, adim, expert, base, count, nsteps, st, order);
+                              hipStream_t st, const int* order = nullptr, const MMXState* S = nullptr) {
+  if (!S) S = &sim->S;
+  return sim->step_rows == 192 ? mmx_launch_step_l192(S, action, adim, expert, base, count, nsteps, st, order)
+                               : mmx_launch_step(S, action, adim, expert, base, count, nsteps, st, order);
 }
 }  // namespace
 
@@ -561,6 +580,31 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
   DeviceGuard guard(sim);
   const int N = sim->S.N, L = n_env_steps > 1 ? rollout_lanes(sim) : 1;
   hipError_t e = hipSuccess;
+  if (sim->render_overlap && sim->S.image_size > 0 && render_phased() && n_env_steps > 1) {
+    // the render of step k on its own stream beside the step k + 1 on the caller's stream (a render
+    // workgroup's 80 KB of LDS fits a CU the step launch's tail has half emptied: C5 +6.6 %, DESIGN
+    // §8 f1); step k writes the pose buffer render k - 2 read, so it waits for that render only
+    hipStream_t rs = sim->rstream;
+    float* rp[2] = {sim->S.rpose, sim->rpose_alt};
+    for (int k = 0; k < n_env_steps && e == hipSuccess; k++) {
+      MMXState Sk = sim->S;
+      Sk.rpose = rp[k & 1];
+      if (k >= 2) e = hipStreamWaitEvent(sim->stream, sim->ev_rend[k & 1], 0);
+      int* ord = sim->step_order ? sim->d_order : nullptr;
+      if (e == hipSuccess && ord) e = mmx_launch_order(&Sk, 0, N, ord, 1024, sim->stream);
+      if (e == hipSuccess)
+        e = timed(sim, sim->stream, sim->t_step,
+                  [&] { return launch_step(sim, sim->expert_action, 4, 1, 0, N, 1, sim->stream, ord, &Sk); });
+      if (e == hipSuccess) e = hipEventRecord(sim->ev_step, sim->stream);
+      if (e == hipSuccess) e = hipStreamWaitEvent(rs, sim->ev_step, 0);
+      if (e == hipSuccess) e = timed(sim, rs, sim->t_render, [&] { return mmx_launch_render(&Sk, 0, N, rs); });
+      if (e == hipSuccess) e = hipEventRecord(sim->ev_rend[k & 1], rs);
+    }
+    // the caller's stream sees the last render; S.rpose names the newest poses
+    if (e == hipSuccess) e = hipStreamWaitEvent(sim->stream, sim->ev_rend[(n_env_steps - 1) & 1], 0);
+    if (e == hipSuccess && ((n_env_steps - 1) & 1)) std::swap(sim->S.rpose, sim->rpose_alt);
+    return hip_check(sim, e, "mmx_rollout_expert");
+  }
   if (L > 1) {  // fork: every lane starts after the work already queued on the caller's stream
     e = hipEventRecord(sim->ev_fork, sim->stream);
     for (int l = 1; l < L && e == hipSuccess; l++) e = hipStreamWaitEvent(sim->lane[l], sim->ev_fork, 0);
@@ -608,6 +652,7 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
 }
 
 int mmx_rollout_lanes(const mmx_sim* sim) { return sim ? rollout_lanes(sim) : 0; }
+int mmx_rollout_render_overlap(const mmx_sim* sim) { return sim ? sim->render_overlap : 0; }
 int mmx_rollout_render_launches(const mmx_sim* sim) {
   if (!sim || sim->S.image_size <= 0) return 0;
   return (render_phased() || sim->nlanes <= 1) ? 1 : sim->nlanes;

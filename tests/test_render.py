@@ -256,6 +256,37 @@ def test_c5_full_batch_properties():
 
 
 @pytest.mark.gpu
+def test_render_overlap_bit_identical(monkeypatch):
+    """MMX_RENDER_OVERLAP=1: the render of step k runs on its own stream beside step k + 1 with the
+    body poses double-buffered; images, segment ids and states after an odd number of camera steps
+    (the pose buffers swap roles) equal the serial rollout's bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs an MI355X")
+    from mujoco_manip_amd import _lib
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    N, S = 2048, 64
+    outs = []
+    for ov in ("0", "1"):
+        monkeypatch.setenv("MMX_RENDER_OVERLAP", ov)
+        env = PickPlaceVecEnv(N, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
+                              image_size=S, autoreset=True)
+        env.reset(seed=[_lib.episode_seed(5, i) for i in range(N)])
+        env.rollout_expert(7)
+        torch.cuda.synchronize()
+        rgb, _ = env.sim.image_views()
+        q, v, _, _ = env.sim.get_state()
+        outs.append((rgb.cpu().numpy().copy(), env.segmentation.cpu().numpy().copy(), q.copy(), v.copy()))
+        env.rollout_expert(2)  # a second call starts from the swapped buffers
+        torch.cuda.synchronize()
+        rgb, _ = env.sim.image_views()
+        outs[-1] = outs[-1] + (rgb.cpu().numpy().copy(),)
+        env.close()
+    for a, b in zip(outs[0], outs[1]):
+        np.testing.assert_array_equal(a, b)
+
+
+@pytest.mark.gpu
 def test_render_after_divergence_without_autoreset():
     """with autoreset off (the dataset loop's setting) a diverged env's NaN / Inf poses
     reach the renderer.  The step must flag the env (env_error NaN bit), the render must complete
