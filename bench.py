@@ -455,8 +455,7 @@ def main():
         # mmx_render_kernel: per env of a launch, 2 cameras x S^2 x (RGB + segment id) bytes written
         # and the 14 body poses read; one launch per rollout lane and env step, lanes side by side
         S = args.image_size
-        # render launches per step: one over all envs after every lane's step (the default), or one
-        # per lane (MMX_RENDER_PHASED=0)
+        # render launches per step: one over all envs after the step launch
         rl = max(1, env.sim.rollout_render_launches)
         r_envs = N / rl
         rbytes = r_envs * (2 * S * S * 4 + 14 * 12 * 4)

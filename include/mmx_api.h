@@ -14,7 +14,8 @@
  *  - sim-owned buffers returned by mmx_get_buffers stay valid until mmx_destroy;
  *  - all launches are asynchronous on the sim's stream (cfg.stream, or the null stream);
  *  - one sim per host thread at a time (not re-entrant); per-env faults go to the
- *    env_error buffer, never to return codes;
+ *    env_error buffer, never to return codes, except the reference's one raising case, spawn
+ *    sampling exhaustion (MMX_ESAMPLING);
  *  - every entry point makes the sim's device (cfg.device) current for its HIP calls and
  *    restores the caller's current device before returning.
  */
@@ -30,6 +31,10 @@ extern "C" {
 #define MMX_EINVAL (-1)   /* bad argument (ValueError in the reference) */
 #define MMX_EDEVICE (-2)  /* HIP runtime error */
 #define MMX_ENOMEM (-3)   /* device allocation failed */
+#define MMX_ESAMPLING (-4) /* object spawn sampling exhausted its 1000 attempts (RuntimeError in the
+                              reference, randomization.py:84-87); reported by the synchronous
+                              mmx_reset, and for autoresets inside steps / rollouts / the episode queue
+                              by the next mmx_synchronize; the env's env_error carries bit 8 */
 
 /* action modes, gym_env.py:30-36 */
 enum { MMX_ACTION_ABS_POS = 0, MMX_ACTION_EE_POS_QUAT_G = 1, MMX_ACTION_EE_POS_ROT6D_G = 2,
@@ -111,7 +116,10 @@ const char* mmx_last_error(const mmx_sim* sim);
 /* PickPlaceGymEnv.reset (gym_env.py:477-534) for the envs selected by env_mask (host,
  * N bytes, NULL = all).  seeds: host, N entries, or NULL to continue each env's stream
  * (gym semantics: reset(seed=None)).  seed_given: host, N bytes, NULL = all seeds valid.
- * task_override: host, N entries of (obj << 4 | bin), -1 = none (options["task"]). */
+ * task_override: host, N entries of (obj << 4 | bin), -1 = none (options["task"]).
+ * Synchronous.  Returns MMX_ESAMPLING when an env's spawn sampling (randomize_objects) found no
+ * separated placement in 1000 attempts: as where the reference raises, that env's cubes stay at the
+ * keyframe and its task is not redrawn (its random stream stays the reference's); the others reset. */
 int mmx_reset(mmx_sim* sim, const uint64_t* seeds, const uint8_t* seed_given, const int32_t* task_override,
               const uint8_t* env_mask);
 
@@ -166,9 +174,8 @@ int mmx_rollout_launches(const mmx_sim* sim, int32_t n_env_steps);
  * range per 1024 envs, at most 4).  Single-step calls always run as one launch on cfg.stream. */
 int mmx_rollout_lanes(const mmx_sim* sim);
 
-/* Render launches per rollout step with cameras: 1 (every lane's env-step launch first, then one
- * render launch over all envs; the default) or mmx_rollout_lanes (a render per lane after its step,
- * env MMX_RENDER_PHASED=0); 0 without cameras.  Timing only: the images are the same. */
+/* Render launches per rollout step: 1 with cameras (the env-step launch of all envs, then one render
+ * launch over all envs), 0 without. */
 int mmx_rollout_render_launches(const mmx_sim* sim);
 
 /* 1 when camera rollouts (mmx_rollout_expert, more than one env step) render step k on a stream of
@@ -237,6 +244,8 @@ int mmx_eval_reward(mmx_sim* sim, const float* obj_dev, const float* ee_dev, con
                     const int32_t* pairs_dev, int32_t max_pairs);
 
 int mmx_get_buffers(mmx_sim* sim, mmx_buffers* out);
+/* Waits for the sim's stream; MMX_ESAMPLING when an autoreset since the last check (mmx_reset or
+ * mmx_synchronize) exhausted its spawn sampling (that env's env_error has bit 8). */
 int mmx_synchronize(mmx_sim* sim);
 
 /* Host copies of the core state (host arrays of [N][field] fp32). NULL skips a field. */

@@ -18,6 +18,9 @@ from . import _build
 NQ, NV, NU, NOBS = 30, 27, 8, 85
 MAXCON, CON_F = 64, 13
 PNG_MAX_WIDTH = 10922  # include/mmx_api.h MMX_PNG_MAX_WIDTH
+MMX_ESAMPLING = -4  # include/mmx_api.h: spawn sampling exhausted (randomization.py:84-87 raises RuntimeError)
+# env_error bits (mujoco_manip_amd/csrc/mmx_state.h)
+ERR_CON_OVERFLOW, ERR_EFC_OVERFLOW, ERR_NAN, ERR_SAMPLING = 1, 2, 4, 8
 EPI_N, EPF_N, KIN_N, STAT_N = 18, 28, 63, 19
 EPI_FIELDS = ("obj", "bin", "step_count", "flags", "fsm_state", "fsm_task_index", "fsm_settle", "fsm_gripper_open",
               "fsm_has_target", "env_error", "ncon", "nefc", "episodes", "rng_has32", "successes", "placed", "error_resets",
@@ -203,6 +206,8 @@ class Sim:
         self._check(self.L.mmx_get_buffers(self.ptr, C.byref(self.buffers)), "mmx_get_buffers")
 
     def _check(self, rc, what):
+        if rc == MMX_ESAMPLING:  # the reference's own exception and message (randomization.py:84-87)
+            raise RuntimeError(self.L.mmx_last_error(self.ptr).decode())
         if rc != 0:
             raise RuntimeError(f"{what} failed ({rc}): {self.L.mmx_last_error(self.ptr).decode()}")
 

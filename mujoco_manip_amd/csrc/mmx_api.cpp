@@ -184,6 +184,17 @@ int hip_check(mmx_sim* sim, hipError_t e, const char* what) {
   if (e == hipSuccess) return MMX_OK;
   return fail(sim, MMX_EDEVICE, std::string(what) + ": " + hipGetErrorString(e));
 }
+// After a stream synchronisation: the sim's fault word (ERR_SAMPLING of a reset since the last check,
+// set by the reset kernel or a step's autoreset) is read, cleared and returned as MMX_ESAMPLING with
+// the message randomization.py:84-87 raises.
+int check_fault(mmx_sim* sim, const char* what) {
+  int f = 0;
+  if (hipMemcpy(&f, sim->S.fault, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+    return fail(sim, MMX_EDEVICE, std::string(what) + ": fault readback");
+  if (!(f & ERR_SAMPLING)) return MMX_OK;
+  if (hipMemset(sim->S.fault, 0, sizeof(int)) != hipSuccess) return fail(sim, MMX_EDEVICE, std::string(what) + ": fault clear");
+  return fail(sim, MMX_ESAMPLING, "Failed to sample 3 positions with min_separation=0.08 in 1000 attempts");
+}
 
 template <typename T>
 T* dalloc(mmx_sim* sim, size_t count) {
@@ -310,6 +321,7 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
   S.con = dalloc<float>(sim, static_cast<size_t>(MMX_MAXCON) * CON_F * n);
   S.stats = dalloc<float>(sim, STAT_N * n);
   S.efc_ovf = dalloc<float>(sim, static_cast<size_t>(MMX_OVF_F) * n);
+  S.fault = dalloc<int>(sim, 1);
   sim->expert_action = dalloc<float>(sim, 4 * n);
   sim->d_mask = dalloc<unsigned char>(sim, n);
   sim->d_task = dalloc<int>(sim, n);
@@ -328,7 +340,7 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
       mmx_destroy(sim);
       return MMX_ENOMEM;
     }
-  if (!S.qpos || !S.con || !S.efc_ovf || !sim->d_task || !sim->d_order) {
+  if (!S.qpos || !S.con || !S.efc_ovf || !S.fault || !sim->d_task || !sim->d_order) {
     mmx_destroy(sim);
     return MMX_ENOMEM;
   }
@@ -453,7 +465,8 @@ int mmx_reset(mmx_sim* sim, const uint64_t* seeds, const uint8_t* seed_given, co
   if (rc) return rc;
   rc = hip_check(sim, mmx_launch_render(&S, 0, S.N, sim->stream), "mmx_reset render");
   if (rc) return rc;
-  return hip_check(sim, hipStreamSynchronize(sim->stream), "mmx_reset sync");
+  rc = hip_check(sim, hipStreamSynchronize(sim->stream), "mmx_reset sync");
+  return rc ? rc : check_fault(sim, "mmx_reset");
 }
 
 namespace {
@@ -561,26 +574,16 @@ int mmx_rollout_launches(const mmx_sim* sim, int32_t n_env_steps) {
   return sim ? rollout_launches(sim, n_env_steps) : 0;
 }
 
-static bool render_phased() {
-  static const bool on = [] {
-    const char* v = std::getenv("MMX_RENDER_PHASED");
-    return !(v && std::atoi(v) == 0);
-  }();
-  return on;
-}
-
-// lanes of a rollout: with cameras (phased render) one — every step ends in a join for the render
-// anyway, and one launch orders all envs longest-first (C5 +2.0 % over 4 lanes)
-static int rollout_lanes(const mmx_sim* sim) {
-  return sim->S.image_size > 0 && render_phased() ? 1 : sim->nlanes;
-}
+// lanes of a rollout: with cameras one (every step ends in the render over all envs, and one launch
+// orders all envs longest-first: C5 +2.0 % over 4 lanes)
+static int rollout_lanes(const mmx_sim* sim) { return sim->S.image_size > 0 ? 1 : sim->nlanes; }
 
 int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
   if (!sim || sim->S.action_mode != MMX_ACTION_ABS_POS) return MMX_EINVAL;
   DeviceGuard guard(sim);
   const int N = sim->S.N, L = n_env_steps > 1 ? rollout_lanes(sim) : 1;
   hipError_t e = hipSuccess;
-  if (sim->render_overlap && sim->S.image_size > 0 && render_phased() && n_env_steps > 1) {
+  if (sim->render_overlap && sim->S.image_size > 0 && n_env_steps > 1) {
     // the render of step k on its own stream beside the step k + 1 on the caller's stream (a render
     // workgroup's 80 KB of LDS fits a CU the step launch's tail has half emptied: C5 +6.6 %, DESIGN
     // §8 f1); step k writes the pose buffer render k - 2 read, so it waits for that render only
@@ -613,11 +616,9 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
   // k-1 of range l.  Without cameras a launch runs up to `fuse` consecutive steps of its envs
   // (mmx_rollout_steps_per_launch); with cameras every step is rendered, one step per launch.
   const int nl = rollout_launches(sim, n_env_steps);
-  // with cameras: the step of all envs, then ONE render launch over all envs (the render's 80 KB
-  // workgroups cannot share a CU with the step kernel's, so a render per lane beside the other lanes'
-  // steps ran as a trickle: C5 +2.8 % phased); MMX_RENDER_PHASED=0 restores lanes
-  // with a render each
-  const bool phased = render_phased();
+  // with cameras (L = 1): the step of all envs, then ONE render launch over all envs (the render's
+  // 80 KB workgroups cannot share a CU with the step kernel's: a render per lane beside the other
+  // lanes' steps ran as a trickle, C5 -2.8 %)
   for (int r = 0; r < nl && e == hipSuccess; r++) {
     const int ns = n_env_steps / nl + (r < n_env_steps % nl ? 1 : 0);
     for (int l = 0; l < L && e == hipSuccess; l++) {
@@ -628,19 +629,9 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
       if (e == hipSuccess)
         e = timed(sim, st, sim->t_step,
                   [&] { return launch_step(sim, sim->expert_action, 4, 1, b0, b1 - b0, ns, st, ord); });
-      if (e == hipSuccess && sim->S.image_size > 0 && !phased)
-        e = timed(sim, st, sim->t_render, [&] { return mmx_launch_render(&sim->S, b0, b1 - b0, st); });
     }
-    if (e == hipSuccess && sim->S.image_size > 0 && phased) {
-      for (int l = 1; l < L && e == hipSuccess; l++) {  // join the lanes' steps (L = 1 unless n = 1)
-        e = hipEventRecord(sim->ev_join[l], sim->lane[l]);
-        if (e == hipSuccess) e = hipStreamWaitEvent(sim->stream, sim->ev_join[l], 0);
-      }
-      if (e == hipSuccess)
-        e = timed(sim, sim->stream, sim->t_render, [&] { return mmx_launch_render(&sim->S, 0, N, sim->stream); });
-      if (e == hipSuccess) e = hipEventRecord(sim->ev_fork, sim->stream);  // fork again
-      for (int l = 1; l < L && e == hipSuccess; l++) e = hipStreamWaitEvent(sim->lane[l], sim->ev_fork, 0);
-    }
+    if (e == hipSuccess && sim->S.image_size > 0)
+      e = timed(sim, sim->stream, sim->t_render, [&] { return mmx_launch_render(&sim->S, 0, N, sim->stream); });
   }
   if (L > 1)  // join: the caller's stream sees the whole rollout, as with a single launch chain
     for (int l = 1; l < L; l++) {
@@ -654,8 +645,7 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
 int mmx_rollout_lanes(const mmx_sim* sim) { return sim ? rollout_lanes(sim) : 0; }
 int mmx_rollout_render_overlap(const mmx_sim* sim) { return sim ? sim->render_overlap : 0; }
 int mmx_rollout_render_launches(const mmx_sim* sim) {
-  if (!sim || sim->S.image_size <= 0) return 0;
-  return (render_phased() || sim->nlanes <= 1) ? 1 : sim->nlanes;
+  return sim && sim->S.image_size > 0 ? 1 : 0;
 }
 
 // the row-above match uses deflate distance 3 W + 1, which deflate caps at 32768: W <= 10922
@@ -772,7 +762,8 @@ int mmx_get_buffers(mmx_sim* sim, mmx_buffers* b) {
 int mmx_synchronize(mmx_sim* sim) {
   if (!sim) return MMX_EINVAL;
   DeviceGuard guard(sim);
-  return hip_check(sim, hipStreamSynchronize(sim->stream), "mmx_synchronize");
+  const int rc = hip_check(sim, hipStreamSynchronize(sim->stream), "mmx_synchronize");
+  return rc ? rc : check_fault(sim, "mmx_synchronize");
 }
 
 int mmx_get_state(mmx_sim* sim, float* qpos, float* qvel, float* ctrl, float* ws) {

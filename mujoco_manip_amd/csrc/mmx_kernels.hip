@@ -861,7 +861,7 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
   CLK_DECL;
   if (LANE == 0) {
     E.ncon = 0;
-    E.flags &= ~(SHF_ROBOT_OBST | SHF_CON_OVF);
+    E.flags &= ~SHF_ROBOT_OBST;  // (SHF_CON_OVF is sticky from the record load to the fold: any substep's overflow counts)
   }
   float* scr = scr_of(E);
   float* gx = scr + COL_GX;
@@ -1701,7 +1701,17 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
       groups(std::true_type{}, r0, split);
       if (split < r1) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the overflow rows' stores (ovf_fence)
+        // group k of the type (from r0) goes to accumulator k & 1 in either loop, so the sums do not
+        // depend on where the LDS rows end (the 128- and 192-row layouts are bit-identical)
+        const bool odd = ((split - r0) >> 2) & 1;  // uniform
+        auto swap_acc = [&]() {
+          const f32x4 t = acc0;
+          acc0 = acc1;
+          acc1 = t;
+        };
+        if (odd) swap_acc();
         groups(std::false_type{}, split, r1);
+        if (odd) swap_acc();
       }
       PROBE(6, stats, STAT_T_AUX0);
       // stage: lane l holds G[4 (l >> 4) + q][l & 15]
@@ -2708,9 +2718,10 @@ DEV void reset_lane0(const MMXState& S, int i, EnvSh& E, int task_override) {
   Pcg r = Pcg{S.rng[4 * (size_t)i], S.rng[4 * (size_t)i + 1], S.rng[4 * (size_t)i + 2], S.rng[4 * (size_t)i + 3]};
   int has32 = EPI(EPI_RNG_HAS32);
   unsigned buf32 = S.rng32[i];
+  bool ok = true;  // the spawn sampling succeeded (or did not run)
   if (S.randomize) {  // randomization.py:70-98 (fp64 draws, numpy-identical stream)
     double xs[3] = {0, 0, 0}, ys[3] = {0, 0, 0};
-    bool ok = false;
+    ok = false;
     for (int att = 0; att < 1000 && !ok; att++) {
       for (int k = 0; k < 3; k++) xs[k] = (double)S.spawn_x0 + ((double)S.spawn_x1 - (double)S.spawn_x0) * pcg_double(r);
       for (int k = 0; k < 3; k++) ys[k] = (double)S.spawn_y0 + ((double)S.spawn_y1 - (double)S.spawn_y0) * pcg_double(r);
@@ -2721,8 +2732,15 @@ DEV void reset_lane0(const MMXState& S, int i, EnvSh& E, int task_override) {
           if (dx * dx + dy * dy < 0.08 * 0.08) ok = false;
         }
     }
-    if (!ok) EPI(EPI_ERROR) |= ERR_SAMPLING;
-    for (int k = 0; k < 3; k++) {
+    // exhausted (randomization.py:84-87 raises RuntimeError before touching qpos or drawing the task):
+    // the cubes stay at the keyframe, the task draw is skipped (the stream stays the reference's), the
+    // env's error bit and the sim's fault word are set; mmx_reset / mmx_synchronize turn the fault into
+    // MMX_ESAMPLING and the facades into the reference's RuntimeError
+    if (!ok) {
+      EPI(EPI_ERROR) |= ERR_SAMPLING;
+      atomicOr(S.fault, (int)ERR_SAMPLING);
+    }
+    for (int k = 0; k < 3 && ok; k++) {
       const int qa = 9 + 7 * k;
       E.qpos[qa] = (float)xs[k]; E.qpos[qa + 1] = (float)ys[k]; E.qpos[qa + 2] = 0.26f;
       E.qpos[qa + 3] = 1.f; E.qpos[qa + 4] = 0.f; E.qpos[qa + 5] = 0.f; E.qpos[qa + 6] = 0.f;
@@ -2745,6 +2763,9 @@ DEV void reset_lane0(const MMXState& S, int i, EnvSh& E, int task_override) {
   } else if (S.fixed_obj >= 0) {
     ob = S.fixed_obj;
     bn = S.fixed_bin;
+  } else if (!ok) {  // (the reference raised before its task draw)
+    ob = EPI(EPI_OBJ);
+    bn = EPI(EPI_BIN);
   } else {
     const int idx = pcg_integers(r, has32, buf32, S.ntask);
     ob = S.task_obj[idx];

@@ -112,6 +112,7 @@ struct MMXState {
   float* con;    // [N][MAXCON][CON_F] contacts of the last substep
   float* stats;  // [N][STAT_N]
   float* efc_ovf;  // [N][MMX_OVF_F] constraint rows past the LDS ones (scratch, rarely touched)
+  int* fault;      // [1] sim-level sticky error bits: ERR_SAMPLING of any reset since the host last checked
   // camera images (image_size > 0 only, else null)
   float* rpose;            // [N][14][12] body poses (R row-major, p) of the last position stage
   unsigned char* images;   // [N][2][S][S][3] overhead, wrist RGB

@@ -9,3 +9,5 @@
 #define MMX_STEP_ONLY 1
 #define MMX_STEP_SUFFIX _l192
 #include "mmx_kernels.hip"
+// mmx_api.cpp allocates S.efc_ovf with the 128-row build's per-env stride, which must cover this one's
+static_assert(MMX_OVF_F <= (MMX_MAXEFC - 128) * 18 + 27 * 27 + 3, "overflow block stride exceeds the allocation");

@@ -100,6 +100,12 @@ class PickPlaceVecEnv:
         self.sim.reset(seeds=seeds, task_override=task)
         return self._obs_dict(), {}
 
+    def synchronize(self):
+        """Wait for the env's queued launches.  Raises the reference's RuntimeError (randomization.py:84-87)
+        when an autoreset since the last reset / synchronize exhausted its spawn sampling (that env's
+        env_error carries bit 8 and its cubes stay at the keyframe, as where the reference raises)."""
+        self.sim.synchronize()
+
     def step(self, actions: torch.Tensor):
         """PickPlaceGymEnv.step (gym_env.py:536-581), batched: actions [N, action_dim] fp32 on the GPU."""
         a = torch.as_tensor(actions, dtype=torch.float32, device=self.device)

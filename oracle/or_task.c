@@ -515,13 +515,15 @@ void or_get_obs(or_env* e, float* o) { /* gym_env.py:283-339 (numeric part) */
   o[83] = e->tgt_bin_kp[0]; o[84] = e->tgt_bin_kp[1];
 }
 
-void or_reset(or_env* e, int seed_given, uint64_t seed, int tobj, int tbin, float* obs) { /* gym_env.py:477-534 */
+/* returns 0, or -1 when the spawn sampling is exhausted: randomization.py:84-87 raises RuntimeError
+ * there, leaving the env at the keyframe with step_count 0 (gym_env.py:492-501), no task drawn */
+int or_reset(or_env* e, int seed_given, uint64_t seed, int tobj, int tbin, float* obs) { /* gym_env.py:477-534 */
   if (seed_given) or_pcg64_seed(&e->rng, seed);
   or_reset_keyframe(e);
   e->step_count = 0;
   if (e->randomize) { /* env.py:148-162 */
     double xy[6];
-    if (or_sample_positions(&e->rng, e->spawn_x, e->spawn_y, 0.08, xy) < 0) fprintf(stderr, "oracle: sampling failed\n");
+    if (or_sample_positions(&e->rng, e->spawn_x, e->spawn_y, 0.08, xy) < 0) return -1;
     for (int k = 0; k < 3; k++) {
       int qa = 9 + 7 * k;
       e->qpos[qa] = xy[2 * k]; e->qpos[qa + 1] = xy[2 * k + 1]; e->qpos[qa + 2] = 0.26;
@@ -549,6 +551,7 @@ void or_reset(or_env* e, int seed_given, uint64_t seed, int tobj, int tbin, floa
   project(e, OM_CAM_OVERHEAD, e->xpos[OBJ_BODY[e->obj]], e->tgt_obj_kp);
   project(e, OM_CAM_OVERHEAD, e->xpos[BIN_BODY[e->bin]], e->tgt_bin_kp);
   if (obs) or_get_obs(e, obs);
+  return 0;
 }
 
 static int robot_collision(const or_env* e) { /* gym_env.py:341-350 */

@@ -41,7 +41,7 @@ void or_set_task_pool(or_env* e, int n, const int* obj_idx, const int* bin_idx);
 void or_set_fixed_task(or_env* e, int obj, int bin); /* -1,-1 clears */
 
 /* gym API: seed_given=0 keeps the RNG stream (gym semantics).  task_obj/bin = -1: no override */
-void or_reset(or_env* e, int seed_given, uint64_t seed, int task_obj, int task_bin, float* obs85);
+int or_reset(or_env* e, int seed_given, uint64_t seed, int task_obj, int task_bin, float* obs85); /* -1: sampling exhausted */
 /* returns reward; writes terminated/truncated/success flags and reward_components[6] */
 double or_step(or_env* e, const float* action, float* obs85, int* terminated, int* truncated,
                int* success, float* reward_components);

@@ -42,6 +42,7 @@ def lib():
         L.or_set_task_pool.argtypes = [C.c_void_p, C.c_int, ip, ip]
         L.or_set_fixed_task.argtypes = [C.c_void_p, C.c_int, C.c_int]
         L.or_reset.argtypes = [C.c_void_p, C.c_int, C.c_uint64, C.c_int, C.c_int, fp]
+        L.or_reset.restype = C.c_int
         L.or_step.restype = C.c_double
         L.or_step.argtypes = [C.c_void_p, fp, fp, ip, ip, ip, fp]
         for name in ("or_reset_keyframe", "or_mj_step", "or_mj_forward", "or_fsm_actuate"):
@@ -184,7 +185,9 @@ class OracleEnv:
     def reset(self, seed=None, task=None):
         obs = np.zeros(85, np.float32)
         to, tb = task if task is not None else (-1, -1)
-        lib().or_reset(self.ptr, int(seed is not None), int(seed or 0), to, tb, _f(obs))
+        if lib().or_reset(self.ptr, int(seed is not None), int(seed or 0), to, tb, _f(obs)) < 0:
+            # randomization.py:84-87
+            raise RuntimeError("Failed to sample 3 positions with min_separation=0.08 in 1000 attempts")
         return obs
 
     def step(self, action):

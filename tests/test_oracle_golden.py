@@ -180,3 +180,45 @@ def test_oracle_observation_matches_reference_get_obs(golden):  # gym_env.py:283
             e.set_state(qpos=np.array(st["qpos"]), ctrl=np.array(st["ctrl"]))
             e.mj_forward()
             np.testing.assert_allclose(e.obs(), _flat_obs(st["obs"]), atol=1e-6, err_msg=f"t={st['t']}")
+
+
+SAMPLING_MSG = "Failed to sample 3 positions with min_separation=0.08 in 1000 attempts"
+
+
+def _reference_sampling(seed, xr, yr):
+    """randomization.py:70-98 verbatim in numpy (gymnasium's np_random = default_rng(seed)):
+    the positions, or None where the reference raises."""
+    rng = np.random.default_rng(seed)
+    for _ in range(1000):
+        xs, ys = rng.uniform(xr[0], xr[1], size=3), rng.uniform(yr[0], yr[1], size=3)
+        ok = all((xs[i] - xs[j]) ** 2 + (ys[i] - ys[j]) ** 2 >= 0.08 * 0.08 for i in range(3) for j in range(i + 1, 3))
+        if ok:
+            return np.stack([xs, ys], 1), rng
+    return None, rng
+
+
+@pytest.mark.parametrize("xr,yr", [((0.0, 0.01), (0.30, 0.31)), ((-0.05, 0.05), (0.30, 0.35))])
+def test_sampling_exhaustion_raises(xr, yr):  # randomization.py:78-87 ; gym_env.py:496-501
+    for seed in (0, 3, 42):
+        ref, rng = _reference_sampling(seed, xr, yr)
+        assert ref is None  # the reference raises for these ranges
+        e = O.OracleEnv(randomize_objects=True, spawn_x_range=xr, spawn_y_range=yr)
+        with pytest.raises(RuntimeError, match="^" + SAMPLING_MSG + "$"):
+            e.reset(seed=seed)
+        # the stream consumed exactly the reference's 6000 draws (no task draw after the raise)
+        r = O.PCG64(seed)
+        for _ in range(6000):
+            r.random()
+        assert r.random() == rng.random()
+        q = e.get_state()[0]
+        e0 = O.OracleEnv()
+        e0.reset_keyframe()
+        np.testing.assert_array_equal(q, e0.get_state()[0])  # cubes left at the keyframe
+
+
+def test_sampling_feasible_ranges_match_numpy():  # randomization.py:78-83 on narrow but feasible ranges
+    for seed in (1, 5, 9):
+        ref, _ = _reference_sampling(seed, (-0.2, 0.2), (0.30, 0.31))
+        xy, n = O.PCG64(seed).sample_positions((-0.2, 0.2), (0.30, 0.31))
+        assert ref is not None and n > 0
+        np.testing.assert_array_equal(xy, ref)
