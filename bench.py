@@ -261,13 +261,19 @@ def binding_roof(pmc: dict | None, workload: str) -> dict | None:
     cal_f = os.path.join(REPO, "profiles", "r05_valu_issue_calibration.json")
     ext_f = os.path.join(REPO, "profiles", f"r05_{workload}_sq_extended.json")
     try:
+        # the calibration's measured issue (SQ units, 8 independent FMA chains per wave) at 1-4 waves per
+        # SIMD, interpolated linearly to the kernel's resident waves per SIMD (2.75 at 11 envs per CU)
         cal = json.load(open(cal_f))
-        two = [r for r in cal["scalar_v_fma_f32"] if r["chains"] == 8 and r["waves_per_simd"] == 2][0]
-        ceil_w = 4.0 / two["cycles_per_fma_inst_per_wave"]  # VALU per quad-cycle one wave can issue
+        rows = sorted((r["waves_per_simd"], r["sq_active_inst_valu_per_wave_quad_cycle"], r["sq_valu_per_simd_quad_cycle"])
+                      for r in cal["scalar_v_fma_f32"] if r["chains"] == 8)
+        w = float(v.get("waves_per_simd") or 2)
+        ceil_w = float(np.interp(w, [r[0] for r in rows], [r[1] for r in rows]))  # per wave quad-cycle
+        ceil_s = float(np.interp(w, [r[0] for r in rows], [r[2] for r in rows]))  # per SIMD quad-cycle
         out["valu_issue_ceiling_per_wave"] = ceil_w
-        out["valu_issue_ceiling_per_simd"] = ceil_w * (v.get("waves_per_simd") or 2)
+        out["valu_issue_ceiling_per_simd"] = ceil_s
         out["valu_issue_frac_of_ceiling"] = v["active_inst_valu_per_wave_cycle"] / ceil_w
-        out["calibration"] = "profiles/r05_valu_issue_calibration.json"
+        out["valu_issue_simd_frac_of_ceiling"] = v["frac"] / ceil_s
+        out["calibration"] = "profiles/r05_valu_issue_calibration.json (measured at 1-4 waves per SIMD, interpolated)"
     except (OSError, ValueError, KeyError, IndexError, TypeError, ZeroDivisionError):
         pass
     try:
@@ -279,8 +285,8 @@ def binding_roof(pmc: dict | None, workload: str) -> dict | None:
         pass
     frac = out.get("valu_issue_frac_of_ceiling")
     out["bound"] = ("latency" if frac is not None and frac < 0.6 else "valu-issue")
-    out["note"] = ("a wave issues one instruction per quad-cycle at most and VALU at ~0.94 per quad-cycle "
-                   "(calibration); the step kernel's waves issue VALU at the fraction above of that and any "
+    out["note"] = ("the calibration kernel's waves issue VALU at ~0.94 per quad-cycle alone and ~0.8 at 2.75 waves per "
+                   "SIMD (2.2 per SIMD); the step kernel's waves issue VALU at the fraction above of that and any "
                    "instruction in ~56 % of their quad-cycles: latency / dependency-bound, so env steps/s follow "
                    "the resident envs per CU (profiles/r05_occupancy_probe.json) and the instructions on each "
                    "env's critical path, not the VALU rate")

@@ -134,26 +134,6 @@ int mmx_step(mmx_sim* sim, const float* action_dev, int32_t action_dim);
  * the pinned copy of the step, with no Python object per frame (ctypes releases the GIL for the call). */
 int64_t mmx_copy_ranges(int64_t n, const uint64_t* src, const uint64_t* dst, const int64_t* len);
 
-/* Constraint rows the env-step kernel (mmx_step, mmx_rollout_expert) keeps in LDS: 128 (eleven envs
- * per CU, the default: the fastest layout once the batch fills the GPU's workgroup slots, C3 / C5 /
- * dataset generation) or 192 (eight per CU: faster per env, so for batches that leave slots empty,
- * e.g. C2's 1024 envs).  Env MMX_STEP_ROWS overrides at create.  The rows past the LDS ones live in
- * the env's HBM overflow block; the two layouts agree to fp32 rounding (the parity tests run both),
- * so keep one layout per experiment.  MMX_EINVAL for any other value.  (No reference counterpart: a
- * layout choice of this implementation.) */
-int mmx_set_step_rows(mmx_sim* sim, int32_t rows);
-int mmx_step_rows(const mmx_sim* sim);
-
-/* Dispatch order of env-step launches (mmx_step, mmx_rollout_expert): 1 (default) = each launch's
- * envs longest first by FSM phase (a one-workgroup counting sort before the launch: the envs holding
- * an object, then closing / settling, then releasing, then the rest; within a phase class more
- * constraint rows in the last substep first), 0 = env index order.  Env
- * MMX_STEP_ORDER=0 sets 0 at create.  Only the hardware's workgroup schedule changes: results are
- * bit-identical either way.  MMX_EINVAL for other values; mmx_step_order returns -1 for NULL.  (No
- * reference counterpart: a scheduling choice of this implementation.) */
-int mmx_set_step_order(mmx_sim* sim, int32_t on);
-int mmx_step_order(const mmx_sim* sim);
-
 /* PickAndPlaceTask.plan(n_steps) (pick_and_place.py:167-277) for every env; writes the
  * abs_pos action [N][4] = (target_xyz, gripper_val) to action_dev_out (may be NULL). */
 int mmx_expert_plan(mmx_sim* sim, int32_t n_steps, float* action_dev_out);
@@ -162,42 +142,6 @@ int mmx_expert_plan(mmx_sim* sim, int32_t n_steps, float* action_dev_out);
  * step(abs_pos)); envs whose FSM is done auto-reset when cfg.autoreset is set.
  * Requires action_mode == MMX_ACTION_ABS_POS. */
 int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps);
-
-/* Launches per rollout lane that mmx_rollout_expert(sim, n_env_steps) makes: a launch runs
- * min(steps_per_launch, ceil(n / 8)) consecutive steps (1 with cameras) and the n steps are cut into
- * launches of near-equal length, so a short rollout still spreads over several launch rounds (the
- * drain at the end of a call then costs a fraction of a short launch).  0 for a null sim or n <= 0. */
-int mmx_rollout_launches(const mmx_sim* sim, int32_t n_env_steps);
-
-/* Number of independent env ranges a multi-step rollout runs concurrently (one internal stream
- * each, forked from and joined back to cfg.stream; env MMX_STREAMS overrides the default of one
- * range per 1024 envs, at most 4).  Single-step calls always run as one launch on cfg.stream. */
-int mmx_rollout_lanes(const mmx_sim* sim);
-
-/* Render launches per rollout step: 1 with cameras (the env-step launch of all envs, then one render
- * launch over all envs), 0 without. */
-int mmx_rollout_render_launches(const mmx_sim* sim);
-
-/* 1 when camera rollouts (mmx_rollout_expert, more than one env step) render step k on a stream of
- * their own beside the env-step launch of step k + 1, the body poses double-buffered (the default
- * with cameras; env MMX_RENDER_OVERLAP=0 at create: render, then the next step); 0 otherwise.
- * Timing only: images and states are bit-identical either way. */
-int mmx_rollout_render_overlap(const mmx_sim* sim);
-
-/* Upper bound of the env steps one mmx_env_step_kernel launch runs per env in mmx_rollout_expert: 1
- * with cameras (every step is rendered), else 16 (env MMX_FUSE overrides).  A fused launch runs its
- * envs' steps back to back inside each workgroup; the trajectories are bit-identical to one
- * launch per step.  0 for a null sim. */
-int mmx_rollout_steps_per_launch(const mmx_sim* sim);
-
-/* Per-launch kernel timing of mmx_rollout_expert (measurement): with enable = 1 every step-kernel
- * and render-kernel launch is bracketed by a HIP event pair on the stream it runs on (a new
- * collection starts); enable = 0 stops collecting.  mmx_kernel_times waits for the recorded events
- * and returns the summed launch durations (ms) and launch counts of each kernel; NULL skips a
- * field.  Not part of the reference interface. */
-int mmx_kernel_timing(mmx_sim* sim, int32_t enable);
-int mmx_kernel_times(mmx_sim* sim, float* step_ms, int32_t* step_launches, float* render_ms,
-                     int32_t* render_launches);
 
 /* Batched PNG encoder (dataset emission, generate_dataset.py:250-260: LeRobot embeds image
  * features as PNG files).  Encodes n RGB8 images (device, image i at rgb_dev + i * img_stride,
@@ -269,6 +213,9 @@ int mmx_queue_advance(mmx_sim* sim, int32_t* slot_ep_dev, int32_t* fin_ep_dev);
 /* Host helper: SeedSequence(root).spawn(n)[index].generate_state(1)[0]
  * (scripts/generate_dataset.py:263-268). */
 uint32_t mmx_episode_seed(uint64_t root_seed, int32_t index);
+
+/* Measurement and tuning entry points (launch shape, layout, dispatch order, per-launch timing) have
+ * no reference counterpart and are declared in mmx_tuning.h; a reference-side binding needs none. */
 
 #ifdef __cplusplus
 }

@@ -16,7 +16,8 @@ LIB = os.path.join(PKG, "libmmx.so")
 LIB_PROF = os.path.join(PKG, "libmmx_prof.so")
 SOURCES = ["mmx_kernels.hip", "mmx_step_l192.hip", "mmx_render.hip", "mmx_png.hip", "mmx_api.cpp"]
 HEADERS = ["mmx_kernels.hip", "mmx_model_gen.h", "mmx_render_gen.h", "mmx_state.h", "mmx_device.h", "mmx_geom.h", "mmx_clock.h",
-           os.path.join("..", "..", "include", "mmx_api.h")]
+           os.path.join("..", "..", "include", "mmx_api.h"),
+           os.path.join("..", "..", "include", "mmx_tuning.h")]
 ARCH = os.environ.get("MMX_OFFLOAD_ARCH", "gfx950")
 # device-code math: x / y as x * rcp(y) and sqrt without the denormal-scaling wrapper (v_rcp_f32 /
 # v_sqrt_f32, <= 1 ulp) instead of the correctly rounded fdiv / sqrt expansions (~10 VALU each).
@@ -50,6 +51,15 @@ SOURCE_FLAGS = {"mmx_kernels.hip": ["-Xarch_device", "-fassociative-math"],
                 "mmx_step_l192.hip": ["-Xarch_device", "-fassociative-math"]}
 
 
+# test-only builds of the step kernel (tests/test_overflow_kat.py): the same sources with a define that
+# forces a rare path; linked with the product objects of the other sources
+TEST_VARIANTS = {
+    # a 4-entry collision candidate list (product: 320): the sphere-test overflow path, flagged as
+    # ERR_CON_OVERFLOW in env_error
+    "libmmx_col4.so": ["MMX_COL_LIST=4", "MMX_CAND_CAP=4"],
+}
+
+
 def lib_path(profile: bool = False) -> str:
     return LIB_PROF if profile else LIB
 
@@ -78,18 +88,36 @@ def _compile(src: str, profile: bool, verbose: bool) -> str:
     return obj
 
 
+def _compile_test_variant(name: str, verbose: bool) -> str:
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    obj = os.path.join(CSRC, "mmx_kernels_" + os.path.splitext(name)[0] + ".o")
+    cmd = [hipcc] + FLAGS + SOURCE_FLAGS["mmx_kernels.hip"] + [f"-D{d}" for d in TEST_VARIANTS[name]] + [
+        f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-c", os.path.join(CSRC, "mmx_kernels.hip"), "-o", obj]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    return obj
+
+
 def build(force: bool = False, verbose: bool = False, profile: bool | None = False) -> str:
-    """Build one variant (profile=False/True) or both (profile=None); returns the product path."""
+    """Build one variant (profile=False/True) or both (profile=None, which also builds the test-only
+    TEST_VARIANTS); returns the product path."""
     variants = [False, True] if profile is None else [profile]
     variants = [v for v in variants if force or _stale(lib_path(v))]
-    if variants:
+    tests = [n for n in TEST_VARIANTS if profile is None and (force or _stale(os.path.join(PKG, n)))]
+    if variants or tests:
         jobs = [(src, v) for v in variants for src in SOURCES]
-        with ThreadPoolExecutor(max_workers=len(jobs)) as ex:
+        with ThreadPoolExecutor(max_workers=len(jobs) + len(tests)) as ex:
+            tobjs = [ex.submit(_compile_test_variant, n, verbose) for n in tests]
             objs = list(ex.map(lambda j: _compile(j[0], j[1], verbose), jobs))
+            tobjs = [f.result() for f in tobjs]
         hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
         for v in variants:
             mine = [o for o, (_, vv) in zip(objs, jobs) if vv == v]
             subprocess.check_call([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib_path(v)] + mine)
+        for n, kobj in zip(tests, tobjs):  # the product's objects of the other sources
+            rest = [os.path.join(CSRC, os.path.splitext(src)[0] + ".o") for src in SOURCES if src != "mmx_kernels.hip"]
+            subprocess.check_call([hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", os.path.join(PKG, n), kobj] + rest)
     return lib_path(bool(profile))
 
 

@@ -1,4 +1,4 @@
-// C-ABI implementation (include/mmx_api.h): device allocation, host-side seeding, launches.
+// C-ABI implementation (include/mmx_api.h, include/mmx_tuning.h): device allocation, host-side seeding, launches.
 //
 // Host-side seeding restates numpy's SeedSequence / PCG64 initialisation (the reference seeds
 // every episode through gymnasium: Generator(PCG64(SeedSequence(seed))), gym_env.py:491) so the
@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/mmx_api.h"
+#include "../../include/mmx_tuning.h"
 #include "mmx_state.h"
 
 extern "C" hipError_t mmx_launch_reset(const MMXState* S, const unsigned char* mask, const int* task, hipStream_t st);

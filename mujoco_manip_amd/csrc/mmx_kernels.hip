@@ -61,18 +61,11 @@ static constexpr float kHome[7] = {1.5708f, -0.2f, 0.0f, -2.1f, 0.0f, 1.8f, 0.78
 static constexpr int kBinBody[3] = {MMX_BODY_BIN_RED, MMX_BODY_BIN_GREEN, MMX_BODY_BIN_BLUE};
 
 #define NSLOT 14  // arm bodies 1..11 -> slots 0..10, cubes 16..18 -> slots 11..13
-#ifndef MMX_CAND_CAP
+#ifndef MMX_CAND_CAP  // (test builds lower it with MMX_COL_LIST: tests/test_overflow_kat.py)
 #define MMX_CAND_CAP 144      // persistent broadphase list entries (pair indices; a longer list is not kept: full prune)
 #endif
-#ifndef MMX_CAND_MARGIN
 #define MMX_CAND_MARGIN 0.08f  // m: the list's inflation of the sphere / plane test (A/B: 0.04 +0.2 %, 0.08 +0.8 %, 0.15 -0.6 %)
-#endif
 #define LD 28     // padded row stride for 27-wide rows
-// Newton line search: accept a Newton root of phi' on an unchanged active set without a confirming
-// evaluation (1, the product) or always confirm it (0, the parity A/B build: tools/ab_build.py)
-#ifndef MMX_LS_SHORTCUT
-#define MMX_LS_SHORTCUT 1
-#endif
 
 // ============================================================================ per-env LDS
 // LDS contact record: distance, position, normal and one int (bits): the 15-bit order key (pair x 8 +
@@ -623,13 +616,8 @@ DEV float row_bcast(float v, int k) {
   }
 }
 // broadcast of lane k's value (k < 16) to the lanes of DPP row 0 that hold the small system: one
-// row_newbcast (a VGPR result, no SGPR round trip and its hazard nops) or, the A/B form, v_readlane
-#ifndef MMX_CHOL_SMALL_DPP
-#define MMX_CHOL_SMALL_DPP 1
-#endif
-DEV float small_bcast(float v, int k) {
-  return MMX_CHOL_SMALL_DPP ? row_bcast(v, k) : __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), k));
-}
+// row_newbcast (a VGPR result, no SGPR round trip and its hazard nops; v_readlane measured slower)
+DEV float small_bcast(float v, int k) { return row_bcast(v, k); }
 
 // (A^{-1} v)_j in lane j for a small SPD A given by rows (lane j holds row j in arow[0..N), N <= 9:
 // the rows sit in DPP row 0; lanes of rows 1..3 compute values nobody reads).  Right-looking
@@ -1182,9 +1170,6 @@ DEV V3 contact_t1(V3 n) {  // mju_makeFrame's first tangent
 // term belongs to the normal); the solver forms them from these rows.  An arm block entry is the
 // motion subspace of dof d seen at the contact point, a cube block the free-body Jacobian.  Rows the
 // contact's condim does not use are zero rows with D = 0.  Returns the row's mu (-1: no edges).
-#ifndef MMX_CONPAR_SHFL
-#define MMX_CONPAR_SHFL 1  // 1: each contact's parameters computed once (its lane), read by its rows' lanes
-#endif
 DEV float contact_row(EnvSh& E, int row, int c, int rr, const ConPar& P) {
   const CRec cc = crec(E, c);
   const V3 p = V3{cc[CL_POS], cc[CL_POS + 1], cc[CL_POS + 2]};
@@ -1336,8 +1321,10 @@ DEV void make_constraints_wave(EnvSh& E) {
       if ((side == 0 ? lo_act : hi_act) && row < MMX_MAXEFC) rowmap_set(row++, -1);  // joint limits
   }
   PROBE(3, stats, STAT_T_AUX1);
-  ConPar Pc{1, 0.f, 0.f, 0.f, 0.f, 1.f};  // lane c: contact c's parameters (MMX_CONPAR_SHFL)
-  if (MMX_CONPAR_SHFL && LANE < ncon) Pc = contact_params(crec(E, LANE));
+  // each contact's parameters computed once, by its lane, and read by its rows' lanes over ds_bpermute
+  // (computing them per row measured -1.3 %)
+  ConPar Pc{1, 0.f, 0.f, 0.f, 0.f, 1.f};
+  if (LANE < ncon) Pc = contact_params(crec(E, LANE));
   if (LANE < ncon) {  // the contact's 4 basis rows in the row -> (contact, basis row) map
 #pragma unroll
     for (int rr = 0; rr < 4; rr++)
@@ -1355,17 +1342,13 @@ DEV void make_constraints_wave(EnvSh& E) {
     if (WG * q >= nefc) continue;  // uniform: no row in this slice
     const int m = r < nefc ? __float_as_int(dget(E, r)) : -1;
     const int c = m >= 0 ? (m & 255) : 0;
-    ConPar P;
-    if (MMX_CONPAR_SHFL) {  // contact c's parameters from lane c (every lane takes part in the exchange)
-      P.dim = __shfl(Pc.dim, c);
-      P.mu0 = __shfl(Pc.mu0, c);
-      P.mu1 = __shfl(Pc.mu1, c);
-      P.kid = __shfl(Pc.kid, c);
-      P.B = __shfl(Pc.B, c);
-      P.idiag = __shfl(Pc.idiag, c);
-    } else if (m >= 0) {
-      P = contact_params(crec(E, c));
-    }
+    ConPar P;  // contact c's parameters from lane c (every lane takes part in the exchange)
+    P.dim = __shfl(Pc.dim, c);
+    P.mu0 = __shfl(Pc.mu0, c);
+    P.mu1 = __shfl(Pc.mu1, c);
+    P.kid = __shfl(Pc.kid, c);
+    P.B = __shfl(Pc.B, c);
+    P.idiag = __shfl(Pc.idiag, c);
     if (m >= 0) mu[q] = contact_row(E, r, c, m >> 8, P);
   }
   row = arow;
@@ -1733,15 +1716,11 @@ DEV float hess_grad_mfma(EnvSh& E, int nefc, float* hrow, float mdx) {
 // (g = M (x - xs) + sum B' C r; B' C_old r_new = B' C_old r_old + a B' C_old B p).  E.D / E.NC /
 // slot 15 hold dC_kk, dC_nk and dC r_new (newton_wave's weight pass in delta mode); gm[q] bit 4m
 // marks group m of row slice q as changed (wave-uniform).  Only the changed groups' MFMA steps run,
-// and only the row types holding one are staged and gathered, LDS and (MMX_DELTA_OVF) HBM overflow rows
-// alike.  Adds into hrow; returns sum B' dC r in lane j < 27.
+// and only the row types holding one are staged and gathered, LDS and HBM overflow rows alike (r05:
+// with 128 LDS rows the grasp phases' rows spill; the full pass whenever rows spill, as in r02-r04,
+// measured slower).  Adds into hrow; returns sum B' dC r in lane j < 27.
 #define HESS_LQ (MMX_LDSEFC / WG)  // row slices held in LDS
-// incremental Hessian also over the HBM overflow rows (r05: with 128 LDS rows the grasp phases' rows
-// spill; 0 = the full pass whenever rows spill, as with 192 rows in r02-r04)
-#ifndef MMX_DELTA_OVF
-#define MMX_DELTA_OVF 1
-#endif
-#define HESS_NQ (MMX_DELTA_OVF ? RPL : HESS_LQ)  // row slices the delta pass covers
+#define HESS_NQ RPL                // row slices the delta pass covers
 DEV float hess_grad_delta(EnvSh& E, float* hrow, const unsigned long long* gm) {
   float* G = lrow_of(E);
   const int col = LANE & 15, rk = LANE >> 4;
@@ -2095,7 +2074,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid, int& exit) 
     // collects its edges' normal parts over the DPP quad.  Delta mode: the same with the change
     // of each edge's weight (+-D where its active state flipped, else 0), and a mask of the
     // groups holding a flipped edge.
-    const bool delta = it > 0 && (MMX_DELTA_OVF || nefc <= MMX_LDSEFC);  // uniform
+    const bool delta = it > 0;  // uniform
     unsigned long long gm[HESS_NQ];
 #pragma unroll
     for (int q = 0; q < HESS_NQ; q++) gm[q] = 0ull;
@@ -2199,7 +2178,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid, int& exit) 
     // up to 7e-4 m against the solver at MuJoCo's tolerance).
     float alpha = 1.f, lo = 0.f, hi = 3e38f;
     int bcur = act_at(1.f);
-    bool exact = false;  // (+1.0 % env steps/s in the A/B; MMX_LS_SHORTCUT=0: always confirm)
+    bool exact = false;  // (+1.0 % env steps/s in the A/B)
     for (int ls = 0; ls < 24 && !exact; ls++) {
       if (MMX_PROBE == 10 && LANE == 0) stats[STAT_T_AUX3] += 1.f;  // line-search steps
       float d1 = 0.f, d2 = 0.f;
@@ -2224,7 +2203,7 @@ DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid, int& exit) 
         break;
       }
       const int bn = act_at(na);
-      exact = MMX_LS_SHORTCUT && newton && __ballot(bn != bcur) == 0ull;
+      exact = newton && __ballot(bn != bcur) == 0ull;
       bcur = bn;
       alpha = na;
     }

@@ -8,9 +8,18 @@ import numpy as np
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_functions():
-    src = open(os.path.join(REPO, "include", "mmx_api.h")).read()
+def declared_functions(headers=("mmx_api.h", "mmx_tuning.h")):
+    src = "".join(open(os.path.join(REPO, "include", h)).read() for h in headers)
     return sorted(set(re.findall(r"^\s*(?:int|int64_t|void|const char\*|uint32_t)\s+(mmx_\w+)\s*\(", src, re.M)))
+
+
+def test_reference_boundary_header_has_no_tuning_entry_points():
+    """include/mmx_api.h holds the reference boundary only; the launch-shape / layout / timing calls a
+    reference-side binding never needs live in include/mmx_tuning.h."""
+    api, tuning = declared_functions(("mmx_api.h",)), declared_functions(("mmx_tuning.h",))
+    assert not set(api) & set(tuning)
+    assert {"mmx_set_step_rows", "mmx_kernel_timing", "mmx_rollout_lanes"} <= set(tuning)
+    assert {"mmx_create", "mmx_reset", "mmx_step", "mmx_rollout_expert"} <= set(api)
 
 
 def test_library_exports_every_declared_symbol():

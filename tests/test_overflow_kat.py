@@ -1,0 +1,65 @@
+"""Contact-overflow KAT: more sphere-test survivors than the collision candidate list
+holds must reach env_error as ERR_CON_OVERFLOW, whichever substep of the env step overflowed (the
+flag is sticky from the record load to the step's fold).  The product list holds 320 of the 780
+pairs, which no C3 state comes near, so the path is forced with the test-only build
+libmmx_col4.so (_build.TEST_VARIANTS: a 4-entry list), run in a child process because the binding
+loads one library per process.  The product library in this process shows no overflow over a C3
+rollout."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHILD = r"""
+import sys
+import numpy as np
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + "/oracle")
+import oracle_py as O
+from mujoco_manip_amd import _lib
+from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+env = PickPlaceVecEnv(64, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
+                      image_size=0)
+env.reset(seed=[O.episode_seed(42, i) for i in range(64)])
+hit = np.zeros(64, bool)
+for t in range(12):
+    env.step(env.expert_plan(16))
+    hit |= (env.env_error.cpu().numpy() & _lib.ERR_CON_OVERFLOW) != 0
+print("OVERFLOW_ENVS", int(hit.sum()), "NAN_ENVS", int(((env.env_error.cpu().numpy() & _lib.ERR_NAN) != 0).sum()))
+"""
+
+
+def test_candidate_list_overflow_reaches_env_error():
+    if not torch.cuda.is_available():
+        pytest.skip("needs an MI355X")
+    lib = os.path.join(REPO, "mujoco_manip_amd", "libmmx_col4.so")
+    assert os.path.exists(lib), "test build missing: run __graft_entry__.build()"
+    r = subprocess.run([sys.executable, "-c", CHILD, REPO], env=dict(os.environ, MMX_LIB_PATH=lib), capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("OVERFLOW_ENVS")][0].split()
+    print(" ".join(line))
+    assert int(line[1]) > 0  # envs whose sphere test kept more than 4 pairs (3 cubes on the table + the gripper)
+
+
+def test_product_c3_rollout_has_no_contact_overflow():
+    if not torch.cuda.is_available():
+        pytest.skip("needs an MI355X")
+    import oracle_py as O
+    from mujoco_manip_amd import _lib
+    from mujoco_manip_amd.vec_env import PickPlaceVecEnv
+
+    n = 1024
+    env = PickPlaceVecEnv(n, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
+                          image_size=0)
+    env.reset(seed=[O.episode_seed(42, i) for i in range(n)])
+    seen = np.zeros(n, np.int32)
+    for t in range(60):  # approach, grasps, transport: the contact piles
+        env.step(env.expert_plan(16))
+        seen |= env.env_error.cpu().numpy()
+    assert not (seen & (_lib.ERR_CON_OVERFLOW | _lib.ERR_EFC_OVERFLOW)).any()

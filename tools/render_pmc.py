@@ -1,4 +1,4 @@
-"""Condense tools/render_pmc.sh output: mean SQ counters per mmx_render_kernel dispatch (the last
+"""Condense the render_pmc recipe of tools/gpu.sh: mean SQ counters per mmx_render_kernel dispatch (the last
 `--last` dispatches) and per workgroup / per pixel -> profiles/<round>_render_pmc.json.  Diagnostic."""
 import argparse
 import csv
