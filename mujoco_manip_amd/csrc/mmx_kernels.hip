@@ -1018,6 +1018,15 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
     stats[STAT_T_AUX2] += (float)ncls[2];
     stats[STAT_T_AUX3] += (float)ncls[0];
   }
+  // probe set 13: per collision pass of a substep, the full 780-pair prunes (no
+  // valid persistent list), the list rebuilds that then kept no list (more than MMX_CAND_CAP pairs),
+  // and the box-box / GJK candidates after the OBB prune
+  if (MMX_PROBE == 13 && LANE == 0 && !only_ro) {
+    stats[STAT_T_AUX0] += use_list ? 0.f : 1.f;
+    stats[STAT_T_AUX1] += (rebuild && E.ncand < 0) ? 1.f : 0.f;
+    stats[STAT_T_AUX2] += (float)ncls[1];
+    stats[STAT_T_AUX3] += (float)ncls[2];
+  }
   PROBE(2, stats, STAT_T_AUX2);
   PROBE(5, stats, STAT_T_AUX3);
 }
