@@ -574,6 +574,37 @@ static int rollout_launches(const mmx_sim* sim, int n) {
 int mmx_rollout_launches(const mmx_sim* sim, int32_t n_env_steps) {
   return sim ? rollout_launches(sim, n_env_steps) : 0;
 }
+// Launch lengths of lane `lane` for an n-step rollout: near-equal launches of rollout_len steps, or
+// (experiments) the env override MMX_PLAN = "a,b,...[;c,d,...]" per lane (the last list repeats for
+// the lanes after it), used when its lengths sum to n.
+static std::vector<int> rollout_plan(const mmx_sim* sim, int n, int lane) {
+  std::vector<int> v;
+  if (const char* e = std::getenv("MMX_PLAN")) {
+    std::string all(e), mine;
+    size_t pos = 0;
+    for (int l = 0;; l++) {
+      const size_t sc = all.find(';', pos);
+      mine = all.substr(pos, sc == std::string::npos ? std::string::npos : sc - pos);
+      if (l == lane || sc == std::string::npos) break;
+      pos = sc + 1;
+    }
+    int sum = 0;
+    for (size_t a = 0; a < mine.size();) {
+      const int k = std::atoi(mine.c_str() + a);
+      if (k <= 0) break;
+      v.push_back(k);
+      sum += k;
+      const size_t c = mine.find(',', a);
+      if (c == std::string::npos) break;
+      a = c + 1;
+    }
+    if (sum == n) return v;
+    v.clear();
+  }
+  const int nl = rollout_launches(sim, n);
+  for (int r = 0; r < nl; r++) v.push_back(n / nl + (r < n % nl ? 1 : 0));
+  return v;
+}
 
 // lanes of a rollout: with cameras one (every step ends in the render over all envs, and one launch
 // orders all envs longest-first: C5 +2.0 % over 4 lanes)
@@ -616,13 +647,19 @@ int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
   // the step kernel plans with the FSM itself (expert=1); step k of range l only depends on step
   // k-1 of range l.  Without cameras a launch runs up to `fuse` consecutive steps of its envs
   // (mmx_rollout_steps_per_launch); with cameras every step is rendered, one step per launch.
-  const int nl = rollout_launches(sim, n_env_steps);
+  std::vector<int> plan[mmx_sim::kMaxLanes];
+  size_t nl = 0;
+  for (int l = 0; l < L; l++) {
+    plan[l] = rollout_plan(sim, n_env_steps, l);
+    nl = std::max(nl, plan[l].size());
+  }
   // with cameras (L = 1): the step of all envs, then ONE render launch over all envs (the render's
   // 80 KB workgroups cannot share a CU with the step kernel's: a render per lane beside the other
   // lanes' steps ran as a trickle, C5 -2.8 %)
-  for (int r = 0; r < nl && e == hipSuccess; r++) {
-    const int ns = n_env_steps / nl + (r < n_env_steps % nl ? 1 : 0);
+  for (size_t r = 0; r < nl && e == hipSuccess; r++) {
     for (int l = 0; l < L && e == hipSuccess; l++) {
+      if (r >= plan[l].size()) continue;
+      const int ns = plan[l][r];
       const int b0 = (int)((long)N * l / L), b1 = (int)((long)N * (l + 1) / L);
       hipStream_t st = l ? sim->lane[l] : sim->stream;
       int* ord = sim->step_order ? sim->d_order + b0 : nullptr;  // the lane's slice of the order buffer
