@@ -602,7 +602,23 @@ DEV bool epa_face(const SVx* V, EFace& f, int a, int b, int c) {
   f.d = dot(f.n, V[a].w);
   return true;
 }
-// V, F, edges: LDS scratch (EPA_MAXV SVx, EPA_MAXF EFace, 3 EPA_MAXF edge pairs)
+// wave-level ordering of the EPA's LDS arrays between its lane-parallel steps (one wave runs the pair)
+DEV void epa_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+DEV int epa_lane() { return (int)(threadIdx.x & 63); }
+DEV int epa_prefix(unsigned long long m) {  // set bits of m below this lane
+  return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+// V, F, edges: LDS scratch (EPA_MAXV SVx, EPA_MAXF EFace, 3 EPA_MAXF edge pairs).
+// The polytope's faces are handled one per lane (r06): the nearest face is a wave arg-min (ties to
+// the lowest index, as the serial scan), the faces the new point sees are one ballot, the others
+// are compacted in index order by ballot prefixes, and the horizon's new faces are formed one per
+// lane and appended in edge order; the horizon edge list itself is built from the visible faces in
+// index order with the serial add / cancel rule.  Every array ends each iteration exactly as the
+// serial loops left it (same faces, same order, same arithmetic per face).
 DEV bool epa(const Geom& A, const Geom& B, SVx* V, int nv, V3& nrm, float& depth, V3& pa, V3& pb, EFace* F,
              int (*edges)[2]) {
   int nf = 0;
@@ -636,52 +652,100 @@ DEV bool epa(const Geom& A, const Geom& B, SVx* V, int nv, V3& nrm, float& depth
     if (dot(F[nf].n, V[T[k][0]].w - cen) < 0.f) epa_face(V, F[nf], T[k][0], T[k][2], T[k][1]);
     nf++;
   }
+  static_assert(EPA_MAXF <= 128, "two faces per lane");
+  const int ln = epa_lane();
   int best = -1;
   for (int it = 0; it < 32; it++) {
-    best = -1;
-    float bd = 3e38f;
-    for (int k = 0; k < nf; k++)
-      if (F[k].d < bd) {
-        bd = F[k].d;
-        best = k;
-      }
+    epa_sync();
+    // nearest face: per lane its faces ln, ln + 64 (strict <: the lower index on ties), then the
+    // wave's arg-max of -d (ties: the lowest index)
+    float bd = -3e38f;
+    int bi = 0x7fffffff;
+    if (ln < nf && F[ln].d < 3e38f) {
+      bd = -F[ln].d;
+      bi = ln;
+    }
+    if (ln + 64 < nf && -F[ln + 64].d > bd) {
+      bd = -F[ln + 64].d;
+      bi = ln + 64;
+    }
+    wave_argmax(bd, bi);
+    best = bi < nf ? bi : -1;
     if (best < 0) return false;
-    const SVx P = mk_sv(A, B, F[best].n);
-    const float dist = dot(P.w, F[best].n);
-    if (dist - F[best].d < 1e-6f * (1.f + fabsf(dist)) || nv >= EPA_MAXV) break;
-    int ne = 0, m = 0;
-    for (int k = 0; k < nf; k++) {
-      const EFace f = F[k];
-      if (dot(f.n, P.w - V[f.v0].w) > 1e-9f) {
+    const V3 fn = F[best].n;
+    const float fd = F[best].d;
+    const SVx P = mk_sv(A, B, fn);
+    const float dist = dot(P.w, fn);
+    if (dist - fd < 1e-6f * (1.f + fabsf(dist)) || nv >= EPA_MAXV) break;
+    // which faces P sees (lane ln: faces ln and ln + 64), the others kept in index order
+    EFace f0, f1;
+    bool vis0 = false, vis1 = false;
+    if (ln < nf) {
+      f0 = F[ln];
+      vis0 = dot(f0.n, P.w - V[f0.v0].w) > 1e-9f;
+    }
+    if (ln + 64 < nf) {
+      f1 = F[ln + 64];
+      vis1 = dot(f1.n, P.w - V[f1.v0].w) > 1e-9f;
+    }
+    const unsigned long long mv0 = __ballot(vis0), mv1 = __ballot(vis1);
+    const unsigned long long mk0 = __ballot(ln < nf && !vis0), mk1 = __ballot(ln + 64 < nf && !vis1);
+    // horizon: the visible faces' edges in face order, an edge cancelling its reverse (serial rule)
+    int ne = 0;
+    for (int half = 0; half < 2; half++) {
+      unsigned long long m = half ? mv1 : mv0;
+      while (m) {
+        const int k = 64 * half + __builtin_ctzll(m);
+        m &= m - 1ull;
+        const EFace f = F[k];
         const int vv[3] = {f.v0, f.v1, f.v2};
         for (int e = 0; e < 3; e++) {
           const int a = vv[e], b = vv[(e + 1) % 3];
           int found = -1;
-          for (int q = 0; q < ne; q++)
-            if (edges[q][0] == b && edges[q][1] == a) {
-              found = q;
-              break;
-            }
+          for (int q0 = 0; q0 < ne && found < 0; q0 += 64) {  // the first (b, a) in the list
+            const int q = q0 + ln;
+            const unsigned long long hit = __ballot(q < ne && edges[q][0] == b && edges[q][1] == a);
+            if (hit) found = q0 + __builtin_ctzll(hit);
+          }
+          epa_sync();
           if (found >= 0) {
-            edges[found][0] = edges[ne - 1][0];
-            edges[found][1] = edges[ne - 1][1];
+            if (ln == 0) {
+              edges[found][0] = edges[ne - 1][0];
+              edges[found][1] = edges[ne - 1][1];
+            }
             ne--;
           } else if (ne < EPA_MAXF * 3) {
-            edges[ne][0] = a;
-            edges[ne][1] = b;
+            if (ln == 0) {
+              edges[ne][0] = a;
+              edges[ne][1] = b;
+            }
             ne++;
           }
+          epa_sync();
         }
-      } else {
-        F[m++] = f;
       }
     }
-    nf = m;
+    // kept faces compacted in index order (their records are in registers: no overlap hazard)
+    epa_sync();
+    const int nk0 = __popcll(mk0);
+    if (ln < nf && !vis0) F[epa_prefix(mk0)] = f0;
+    if (ln + 64 < nf && !vis1) F[nk0 + epa_prefix(mk1)] = f1;
+    nf = nk0 + __popcll(mk1);
     const int pi = nv++;
-    V[pi] = P;
-    for (int q = 0; q < ne && nf < EPA_MAXF; q++)
-      if (epa_face(V, F[nf], edges[q][0], edges[q][1], pi)) nf++;
+    if (ln == 0) V[pi] = P;
+    epa_sync();
+    // the horizon's faces with P, appended in edge order while they fit (degenerate ones skipped)
+    for (int q0 = 0; q0 < ne && nf < EPA_MAXF; q0 += 64) {
+      const int q = q0 + ln;
+      EFace g;
+      const bool ok = q < ne && epa_face(V, g, edges[q][0], edges[q][1], pi);
+      const unsigned long long mo = __ballot(ok);
+      const int pos = nf + epa_prefix(mo);
+      if (ok && pos < EPA_MAXF) F[pos] = g;
+      nf = min(EPA_MAXF, nf + __popcll(mo));
+    }
   }
+  epa_sync();
   if (best < 0) return false;
   const EFace& f = F[best];
   const V3 p = f.n * f.d;
