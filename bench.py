@@ -449,7 +449,10 @@ def main():
     # (rocprof's per-dispatch average agrees) and the chip-level rate is lanes x one dispatch's
     # bytes / kern_ms.  nefc is the mean rows per substep counted on device in the same window.
     envs_per_launch = N / lanes
-    steps_per_launch = args.steps / launches
+    # the lanes' launches differ in length (mmx_rollout_expert staggers them): the mean env steps per
+    # launch from the window's launch count (every launch covers N / lanes envs)
+    nlaunch = med["launch_counts"][0] or launches * lanes
+    steps_per_launch = args.steps * lanes / nlaunch
     bpe = algorithmic_bytes_per_env_step(solver["mean_nefc"])
     bytes_per_launch = bpe * envs_per_launch * steps_per_launch
     achieved = lanes * bytes_per_launch / (kern_ms * 1e-3) / 1e9

@@ -33,10 +33,10 @@ int mmx_step_rows(const mmx_sim* sim);
 int mmx_set_step_order(mmx_sim* sim, int32_t on);
 int mmx_step_order(const mmx_sim* sim);
 
-/* Launches per rollout lane that mmx_rollout_expert(sim, n_env_steps) makes: a launch runs
- * min(steps_per_launch, ceil(n / 8)) consecutive steps (1 with cameras) and the n steps are cut into
- * launches of near-equal length, so a short rollout still spreads over several launch rounds (the
- * drain at the end of a call then costs a fraction of a short launch).  0 for a null sim or n <= 0. */
+/* The most launches any rollout lane makes in mmx_rollout_expert(sim, n_env_steps): a launch runs
+ * len = min(steps_per_launch, ceil(n / 4)) consecutive steps (1 with cameras); lane l of L starts with
+ * a launch of l * len / L steps, then launches of len, then the remainder, so the lanes' launch
+ * boundaries (each launch ends with a drain) do not fall together.  0 for a null sim or n <= 0. */
 int mmx_rollout_launches(const mmx_sim* sim, int32_t n_env_steps);
 
 /* Number of independent env ranges a multi-step rollout runs concurrently (one internal stream

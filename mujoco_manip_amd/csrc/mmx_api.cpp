@@ -553,30 +553,26 @@ int mmx_kernel_times(mmx_sim* sim, float* step_ms, int32_t* step_launches, float
   return hip_check(sim, e, "mmx_kernel_times");
 }
 
-// Launches per rollout lane of an n-step expert rollout.  A launch runs `len` consecutive env steps
-// of its envs, len = min(fuse, ceil(n / kMinRounds)), and the n steps are cut into ceil(n / len)
-// launches of near-equal length.  Every launch of a lane ends with a drain (its slowest workgroups
-// finish while the chip empties); with the lanes' launches desynchronised the other lanes fill it,
-// except at the end of the call, where all lanes drain together.  That final drain costs a fraction
-// of one launch, so a call keeps at least kMinRounds launches per lane: C3 driver windows (20 steps)
-// 2.07M env steps/s at 10 + 10 steps, 2.30M at 3 steps per launch, 1.96M at 16 + 4; 512-step
-// windows are unchanged from 4 to 16 steps per launch (fuse caps the length there).
-static constexpr int kMinRounds = 8;
+// Launch plan of an n-step expert rollout without cameras.  A launch runs `len` consecutive env steps
+// of its lane's envs, len = min(fuse, ceil(n / 4)); lane l of L starts with a launch of l * len / L
+// steps (none for lane 0), then launches of len, then the remainder, so the lanes' launch boundaries
+// are spread over the launch period instead of falling together.  Every launch ends with a drain (its
+// slowest workgroups finish while its slots empty); the other lanes fill the slots it frees as long as
+// they are not draining at the same time.  Measured on the driver's 20-step windows
+// (tools/sweep_env.py, profiles/r06_sweep_driver_plans.json): equal 3-step launches, all lanes in step,
+// 2.72 M env steps/s; the staggered 5-step plan 2.87 M (+5.4 %); staggered 3-, 4-, 6-, 7-, 10-step
+// plans and 1-step final launches between them; 512-step windows +0.5 % (16-step launches offset by 4).
+// With cameras every step is rendered: one step per launch, one lane.
 static int rollout_len(const mmx_sim* sim, int n) {
-  if (sim->S.image_size > 0) return 1;  // with cameras every step is rendered
-  return std::max(1, std::min(sim->fuse, (n + kMinRounds - 1) / kMinRounds));
+  if (sim->S.image_size > 0) return 1;
+  return std::max(1, std::min(sim->fuse, (n + 3) / 4));
 }
-static int rollout_launches(const mmx_sim* sim, int n) {
-  if (n <= 0) return 0;
-  const int len = rollout_len(sim, n);
-  return (n + len - 1) / len;
-}
-int mmx_rollout_launches(const mmx_sim* sim, int32_t n_env_steps) {
-  return sim ? rollout_launches(sim, n_env_steps) : 0;
-}
-// Launch lengths of lane `lane` for an n-step rollout: near-equal launches of rollout_len steps, or
-// (experiments) the env override MMX_PLAN = "a,b,...[;c,d,...]" per lane (the last list repeats for
-// the lanes after it), used when its lengths sum to n.
+// lanes of a rollout: with cameras one (every step ends in the render over all envs, and one launch
+// orders all envs longest-first: C5 +2.0 % over 4 lanes, DESIGN §8 f1)
+static int rollout_lanes(const mmx_sim* sim) { return sim->S.image_size > 0 ? 1 : sim->nlanes; }
+// Launch lengths of lane `lane` for an n-step rollout (above); env MMX_PLAN = "a,b,...[;c,d,...]" per
+// lane (the last list repeats for the lanes after it) overrides it for experiments when its lengths sum
+// to n.
 static std::vector<int> rollout_plan(const mmx_sim* sim, int n, int lane) {
   std::vector<int> v;
   if (const char* e = std::getenv("MMX_PLAN")) {
@@ -601,15 +597,26 @@ static std::vector<int> rollout_plan(const mmx_sim* sim, int n, int lane) {
     if (sum == n) return v;
     v.clear();
   }
-  const int nl = rollout_launches(sim, n);
-  for (int r = 0; r < nl; r++) v.push_back(n / nl + (r < n % nl ? 1 : 0));
+  if (n <= 0) return v;
+  const int len = rollout_len(sim, n), L = rollout_lanes(sim);
+  int rem = n;
+  const int first = std::min(rem, lane * len / std::max(L, 1));
+  if (first > 0) {
+    v.push_back(first);
+    rem -= first;
+  }
+  for (; rem > 0; rem -= std::min(rem, len)) v.push_back(std::min(rem, len));
   return v;
 }
-
-// lanes of a rollout: with cameras one (every step ends in the render over all envs, and one launch
-// orders all envs longest-first: C5 +2.0 % over 4 lanes, DESIGN §8 f1)
-static int rollout_lanes(const mmx_sim* sim) { return sim->S.image_size > 0 ? 1 : sim->nlanes; }
-
+// the most launches any lane makes
+static int rollout_launches(const mmx_sim* sim, int n) {
+  size_t m = 0;
+  for (int l = 0; l < rollout_lanes(sim); l++) m = std::max(m, rollout_plan(sim, n, l).size());
+  return (int)m;
+}
+int mmx_rollout_launches(const mmx_sim* sim, int32_t n_env_steps) {
+  return sim ? rollout_launches(sim, n_env_steps) : 0;
+}
 int mmx_rollout_expert(mmx_sim* sim, int32_t n_env_steps) {
   if (!sim || sim->S.action_mode != MMX_ACTION_ABS_POS) return MMX_EINVAL;
   DeviceGuard guard(sim);

@@ -586,15 +586,18 @@ DEV bool gjk(const Geom& A, const Geom& B, SVx& s0, SVx& s1, SVx& s2, SVx& s3, i
 
 #define EPA_MAXV 38
 #define EPA_MAXF 72  // 2 EPA_MAXV - 4: the faces of a closed polytope on EPA_MAXV vertices
+// an EPA face: its three vertex indices packed in one word (8 bits each: EPA_MAXV < 256), unit
+// normal and distance from the origin (5 words; the polytope fits the collision scratch beside the
+// contacts)
 struct EFace {
-  int v0, v1, v2;
+  int vv;
   V3 n;
   float d;
+  DEV int v(int k) const { return (vv >> (8 * k)) & 255; }
 };
+static_assert(EPA_MAXV < 256, "EPA vertex indices are packed in bytes");
 DEV bool epa_face(const SVx* V, EFace& f, int a, int b, int c) {
-  f.v0 = a;
-  f.v1 = b;
-  f.v2 = c;
+  f.vv = a | (b << 8) | (c << 16);
   const V3 n = cross(V[b].w - V[a].w, V[c].w - V[a].w);
   const float ln = norm(n);
   if (ln < 1e-20f) return false;
@@ -612,7 +615,7 @@ DEV int epa_lane() { return (int)(threadIdx.x & 63); }
 DEV int epa_prefix(unsigned long long m) {  // set bits of m below this lane
   return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
 }
-// V, F, edges: LDS scratch (EPA_MAXV SVx, EPA_MAXF EFace, 3 EPA_MAXF edge pairs).
+// V, F, edges: LDS scratch (EPA_MAXV SVx, EPA_MAXF EFace, 3 EPA_MAXF edges packed a | b << 8).
 // The polytope's faces are handled one per lane (r06): the nearest face is a wave arg-min (ties to
 // the lowest index, as the serial scan), the faces the new point sees are one ballot, the others
 // are compacted in index order by ballot prefixes, and the horizon's new faces are formed one per
@@ -620,7 +623,7 @@ DEV int epa_prefix(unsigned long long m) {  // set bits of m below this lane
 // index order with the serial add / cancel rule.  Every array ends each iteration exactly as the
 // serial loops left it (same faces, same order, same arithmetic per face).
 DEV bool epa(const Geom& A, const Geom& B, SVx* V, int nv, V3& nrm, float& depth, V3& pa, V3& pb, EFace* F,
-             int (*edges)[2]) {
+             int* edges) {
   int nf = 0;
   if (nv == 1) {
     for (int k = 0; k < 6 && nv < 2; k++) {  // +x, -x, +y, -y, +z, -z
@@ -682,11 +685,11 @@ DEV bool epa(const Geom& A, const Geom& B, SVx* V, int nv, V3& nrm, float& depth
     bool vis0 = false, vis1 = false;
     if (ln < nf) {
       f0 = F[ln];
-      vis0 = dot(f0.n, P.w - V[f0.v0].w) > 1e-9f;
+      vis0 = dot(f0.n, P.w - V[f0.v(0)].w) > 1e-9f;
     }
     if (ln + 64 < nf) {
       f1 = F[ln + 64];
-      vis1 = dot(f1.n, P.w - V[f1.v0].w) > 1e-9f;
+      vis1 = dot(f1.n, P.w - V[f1.v(0)].w) > 1e-9f;
     }
     const unsigned long long mv0 = __ballot(vis0), mv1 = __ballot(vis1);
     const unsigned long long mk0 = __ballot(ln < nf && !vis0), mk1 = __ballot(ln + 64 < nf && !vis1);
@@ -698,27 +701,20 @@ DEV bool epa(const Geom& A, const Geom& B, SVx* V, int nv, V3& nrm, float& depth
         const int k = 64 * half + __builtin_ctzll(m);
         m &= m - 1ull;
         const EFace f = F[k];
-        const int vv[3] = {f.v0, f.v1, f.v2};
         for (int e = 0; e < 3; e++) {
-          const int a = vv[e], b = vv[(e + 1) % 3];
+          const int a = f.v(e), b = f.v((e + 1) % 3);
           int found = -1;
           for (int q0 = 0; q0 < ne && found < 0; q0 += 64) {  // the first (b, a) in the list
             const int q = q0 + ln;
-            const unsigned long long hit = __ballot(q < ne && edges[q][0] == b && edges[q][1] == a);
+            const unsigned long long hit = __ballot(q < ne && edges[q] == (b | (a << 8)));
             if (hit) found = q0 + __builtin_ctzll(hit);
           }
           epa_sync();
           if (found >= 0) {
-            if (ln == 0) {
-              edges[found][0] = edges[ne - 1][0];
-              edges[found][1] = edges[ne - 1][1];
-            }
+            if (ln == 0) edges[found] = edges[ne - 1];
             ne--;
           } else if (ne < EPA_MAXF * 3) {
-            if (ln == 0) {
-              edges[ne][0] = a;
-              edges[ne][1] = b;
-            }
+            if (ln == 0) edges[ne] = a | (b << 8);
             ne++;
           }
           epa_sync();
@@ -738,7 +734,7 @@ DEV bool epa(const Geom& A, const Geom& B, SVx* V, int nv, V3& nrm, float& depth
     for (int q0 = 0; q0 < ne && nf < EPA_MAXF; q0 += 64) {
       const int q = q0 + ln;
       EFace g;
-      const bool ok = q < ne && epa_face(V, g, edges[q][0], edges[q][1], pi);
+      const bool ok = q < ne && epa_face(V, g, edges[q] & 255, edges[q] >> 8, pi);
       const unsigned long long mo = __ballot(ok);
       const int pos = nf + epa_prefix(mo);
       if (ok && pos < EPA_MAXF) F[pos] = g;
@@ -749,20 +745,20 @@ DEV bool epa(const Geom& A, const Geom& B, SVx* V, int nv, V3& nrm, float& depth
   if (best < 0) return false;
   const EFace& f = F[best];
   const V3 p = f.n * f.d;
-  const V3 v0 = V[f.v1].w - V[f.v0].w, v1 = V[f.v2].w - V[f.v0].w, v2 = p - V[f.v0].w;
+  const V3 v0 = V[f.v(1)].w - V[f.v(0)].w, v1 = V[f.v(2)].w - V[f.v(0)].w, v2 = p - V[f.v(0)].w;
   const float d00 = dot(v0, v0), d01 = dot(v0, v1), d11 = dot(v1, v1), d20 = dot(v2, v0), d21 = dot(v2, v1);
   const float den = d00 * d11 - d01 * d01;
   const float lv = den > 1e-30f ? (d11 * d20 - d01 * d21) / den : 0.f;
   const float lw = den > 1e-30f ? (d00 * d21 - d01 * d20) / den : 0.f;
   const float lu = 1.f - lv - lw;
-  pa = V[f.v0].a * lu + V[f.v1].a * lv + V[f.v2].a * lw;
-  pb = V[f.v0].b * lu + V[f.v1].b * lv + V[f.v2].b * lw;
+  pa = V[f.v(0)].a * lu + V[f.v(1)].a * lv + V[f.v(2)].a * lw;
+  pb = V[f.v(0)].b * lu + V[f.v(1)].b * lv + V[f.v(2)].b * lw;
   nrm = f.n;
   depth = f.d;
   return true;
 }
 
-#define EPA_SCRATCH_FLOATS (9 * EPA_MAXV + 7 * EPA_MAXF + 6 * EPA_MAXF)
+#define EPA_SCRATCH_FLOATS (9 * EPA_MAXV + 5 * EPA_MAXF + 3 * EPA_MAXF)
 // scr: EPA_SCRATCH_FLOATS of LDS; emits at most one contact (lane 0)
 template <class Sink>
 DEV void convex_convex(Sink& cs, const Geom& A, const Geom& B, float* scr) {
@@ -771,7 +767,7 @@ DEV void convex_convex(Sink& cs, const Geom& A, const Geom& B, float* scr) {
   if (!gjk(A, B, s0, s1, s2, s3, n)) return;
   SVx* V = reinterpret_cast<SVx*>(scr);
   EFace* F = reinterpret_cast<EFace*>(scr + 9 * EPA_MAXV);
-  int(*edges)[2] = reinterpret_cast<int(*)[2]>(scr + 9 * EPA_MAXV + 7 * EPA_MAXF);
+  int* edges = reinterpret_cast<int*>(scr + 9 * EPA_MAXV + 5 * EPA_MAXF);
   V[0] = s0;
   if (n > 1) V[1] = s1;
   if (n > 2) V[2] = s2;

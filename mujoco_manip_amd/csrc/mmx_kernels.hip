@@ -61,9 +61,6 @@ static constexpr float kHome[7] = {1.5708f, -0.2f, 0.0f, -2.1f, 0.0f, 1.8f, 0.78
 static constexpr int kBinBody[3] = {MMX_BODY_BIN_RED, MMX_BODY_BIN_GREEN, MMX_BODY_BIN_BLUE};
 
 #define NSLOT 14  // arm bodies 1..11 -> slots 0..10, cubes 16..18 -> slots 11..13
-#ifndef MMX_CAND_CAP  // (test builds lower it with MMX_COL_LIST: tests/test_overflow_kat.py)
-#define MMX_CAND_CAP 144      // persistent broadphase list entries (pair indices; a longer list is not kept: full prune)
-#endif
 #define MMX_CAND_MARGIN 0.08f  // m: the list's inflation of the sphere / plane test (A/B: 0.04 +0.2 %, 0.08 +0.8 %, 0.15 -0.6 %)
 #define LD 28     // padded row stride for 27-wide rows
 
@@ -84,9 +81,21 @@ struct CRecW {
   int c;
   DEV float& operator[](int k) const { return b[k * MMX_MAXCON + c]; }
 };
-DEV int con_key(CRec c) { return __float_as_int(c[CL_KEY]); }
-DEV int con_g1(CRec c) { return (con_key(c) >> 16) & 63; }
-DEV int con_g2(CRec c) { return (con_key(c) >> 22) & 63; }
+// a contact record held in registers (the row build: lane c holds contact c)
+struct CReg {
+  float v[CL_F];
+  DEV float operator[](int k) const { return v[k]; }
+};
+template <class R>
+DEV int con_key(const R& c) { return __float_as_int(c[CL_KEY]); }
+template <class R>
+DEV int con_g1(const R& c) { return (con_key(c) >> 16) & 63; }
+template <class R>
+DEV int con_g2(const R& c) { return (con_key(c) >> 22) & 63; }
+// Hessian staging tile row stride: 17, so the dof lanes' reads of different tile rows (tile_gather)
+// fall on different banks (a 16-float stride put rows sd and sd + 2 on one bank: up to 5-way; with the
+// polygon stride below, LDS bank conflicts 0.31 -> 0.12 per LDS-active cycle, +0.2 % in the A/B)
+#define GST 17
 struct EnvSh {
   float qpos[30], qvel[28], ctrl[8];
   float target[4];
@@ -98,10 +107,6 @@ struct EnvSh {
   // x: the Newton solution; between solves it holds the warm start for the next one (MuJoCo's
   // qacc_warmstart: the record's qacc_ws is loaded into it and stored from it)
   float qfrc[LD], qacc_s[LD], x[LD], p[LD];
-  // contacts in LDS: 8 floats each (CL_*); the pair's friction and condim are table lookups of the
-  // two geoms (MuJoCo mixing: max), recomputed where needed, so the 13-field HBM record (CON_*,
-  // include/mmx_api.h) is filled only when the contacts are stored
-  float con[CL_F][MMX_MAXCON];  // field-major: E.con[k][c] = field k of contact c (crec)
   // constraint rows in block format: a row touches at most two dof blocks (arm = 9 dofs,
   // cube k = 6 dofs); J[i][0..n0) holds block b0's columns, J[i][n0..n0+n1) block b1's;
   // J doubles as the contact-sort scratch in collide_wave (rows are built after it).
@@ -118,14 +123,16 @@ struct EnvSh {
   // rows put lanes 4 apart on one bank (4-way): LDS bank conflicts 0.71 -> 0.31 cycles per
   // LDS-active cycle, +0.75 % env steps/s at unchanged VALU (A/B).
   alignas(16) float J[4][MMX_LDSEFC + 1][4];  // J[k >> 2][i][k & 3] = slot k of row i (past the width 0; 15 = aref)
-  unsigned char hdr[MMX_MAXEFC];  // b0 | b1 << 4 (block 15 = none); row 0 is the equality
+  unsigned char hdr[MMX_LDSEFC];  // b0 | b1 << 4 (block 15 = none); row 0 is the equality (rows past: ovf)
   // D: the row's 1 / R while the rows are built (doubling as the row -> contact map before) and in
   // the solver's setup; then per Newton iteration the diagonal entry of the group's edge-weight
   // matrix C (C_kk; a single row's active weight).  NC: C_nk, the row's coupling to its contact's
   // normal row (0 for single and normal rows).
   alignas(16) float D[MMX_LDSEFC];
   alignas(16) float NC[MMX_LDSEFC];
-  float* ovf;  // this env's overflow rows (S.efc_ovf + i * MMX_OVF_F)
+  // the Newton Hessian's 16 x 16 staging tile (row stride GST); the collision scratch before the rows
+  alignas(16) float G[16 * GST];
+  float* ovf;  // this env's overflow block (S.efc_ovf + i * MMX_OVF_F): rows past LDSEFC, headers, list
   int ncon, nefc, flags;
   int nsingle;  // rows [0, nsingle): equality + limit rows (+ zero padding); contact groups after
   int nefc_mj;  // MuJoCo's row count (pyramid edges + equality + limits), for the statistics
@@ -133,34 +140,37 @@ struct EnvSh {
   int tbase[11];  // rows are grouped by block-pair type: type t owns rows [tbase[t], tbase[t+1])
   int act_free;  // bit a: actuator a's force is inside its forcerange (its kv enters qDeriv)
   float stats[STAT_N];  // lane 0 accumulates; loaded / stored with the env record
-  // persistent broadphase list (collide_prune): the pairs within MMX_CAND_MARGIN of contact when it
-  // was built, in pair order; valid while the bodies' accumulated displacement bound stays under
-  // half the margin.  ncand < 0: no valid list (every record load invalidates it).
+  // persistent broadphase list (collide_prune; its entries in the overflow block, cand_of): the pairs
+  // within MMX_CAND_MARGIN of contact when it was built, in pair order; valid while the bodies'
+  // accumulated displacement bound stays under half the margin.  ncand < 0: no valid list (every
+  // record load invalidates it).
   float cdisp;     // bound on any geom's displacement since the build (x 2: a pair's relative one)
   float crad;      // max over moving geoms of |geom centre - body origin| + bounding radius
   float cva, cwa;  // this substep's max arm-body origin speed and angular speed (from the RNE)
   int ncand;
-  unsigned short cand[MMX_CAND_CAP];
 };
 // The workgroup's env lives in one file-scope LDS object: the non-inlined substep function below
 // reaches it by symbol (LDS address space), not through a generic pointer.
 static __shared__ EnvSh g_E;
-// eleven workgroups (envs) per CU share its 160 KiB of LDS, allocated in 1,280-byte blocks (measured:
-// tools/calib/lds_occ.hip, profiles/r05_lds_residency.json): the occupancy the kernel is tuned for (r05;
-// with 192 LDS rows, MMX_LDSEFC=192, eight)
-static_assert(MMX_LDSEFC != 128 || (sizeof(EnvSh) + 1279) / 1280 * 1280 * 11 <= 160 * 1024,
-              "EnvSh no longer fits 11 envs per CU");
+// twelve workgroups (envs) per CU share its 160 KiB of LDS, allocated in 1,280-byte blocks (measured:
+// tools/calib/lds_occ.hip, profiles/r05_lds_residency.json): the occupancy the kernel is tuned for (r06;
+// r05: eleven; with 192 LDS rows, MMX_LDSEFC=192, eight).  Twelve waves are three per SIMD, the
+// 168-VGPR budget of amdgpu_waves_per_eu(3).
+static_assert(MMX_LDSEFC != 128 || (sizeof(EnvSh) + 1279) / 1280 * 1280 * 12 <= 160 * 1024,
+              "EnvSh no longer fits 12 envs per CU");
 static_assert((sizeof(EnvSh) + 1279) / 1280 * 1280 * 8 <= 160 * 1024, "EnvSh no longer fits 8 envs per CU");
 
-// The scratch region: E.J, E.hdr, E.D and E.NC (contiguous in EnvSh) hold the phases' scratch outside
-// the constraint build + Newton solve (rows are rebuilt every substep): the collision layout below,
-// the position stage's chain scan, the IK system, the RNE / composite-inertia / actuator scratch of the
-// dynamics (at COL_WORK) and the observation of the step end.  The Newton Hessian staging tile and
-// Cholesky transpose live in E.con instead (contacts are dead once the rows exist; the last substep
-// stores them to HBM first).
-// r05: 128 LDS rows (MMX_LDSEFC), this scratch layout, 8-float contacts, the warm start kept in E.x,
-// the cubes' mass entries as constants and a 144-pair broadphase list bring the env to 14,064 B of
-// LDS, eleven per CU (was 20,432 B with 192 rows: eight); rows past 128 go to the HBM overflow block.
+// The scratch region: E.J, E.hdr, E.D, E.NC and E.G (contiguous in EnvSh) hold the phases' scratch
+// outside the constraint build + Newton solve (rows are rebuilt every substep): the collision layout
+// below (geom records, candidates, the contacts, the narrowphase work space), the position stage's chain
+// scan, the IK system, the RNE / composite-inertia / actuator scratch of the dynamics (at COL_WORK) and
+// the observation of the step end.  The contacts live here from the narrowphase to the row build, whose
+// lanes take them into registers (lane c: contact c) before the first row is written; the Newton
+// Hessian staging tile is E.G.
+// r06: the contacts out of their own LDS array (into this region, then registers), the rows' mu passed
+// to the solver in registers, the overflow rows' headers and the broadphase list in the HBM overflow
+// block: 12,640 B of LDS, twelve envs per CU (r05: 14,080 B with its own contact array, eleven; r04:
+// 20,432 B with 192 rows, eight); rows past 128 go to the HBM overflow block.
 #define GXS 17        // geom record: world pose (x 3, R 9), rbound, type, box half extents (3)
 #define GX_RB 12
 #define GX_TYPE 13
@@ -171,18 +181,21 @@ static_assert((sizeof(EnvSh) + 1279) / 1280 * 1280 * 8 <= 160 * 1024, "EnvSh no 
 #define MMX_COL_LIST 320  // more survivors of the sphere test than this: the rest are dropped, SHF_CON_OVF
 #endif
 #define COL_LIST MMX_COL_LIST
-#define COL_WORK (COL_CAND + COL_LIST)  // narrowphase work space: box-box polygons, the EPA polytope
+#define COL_CON (COL_CAND + COL_LIST)   // the contacts, field-major [CL_F][MMX_MAXCON] (crec)
+#define COL_WORK (COL_CON + CL_F * MMX_MAXCON)  // narrowphase work space: box-box polygons, the EPA polytope
 #define COL_POLY 49                     // (GJK pass), then the contact sort (49: the quads' polygons
                                         // start on different banks; 48 put quads 2 apart on one)
 #define COL_PLANES 16                   // box-box lane quads per pass: one polygon each
 #define COL_EPA COL_WORK
 static_assert(offsetof(EnvSh, hdr) == offsetof(EnvSh, J) + sizeof(EnvSh::J) &&
                   offsetof(EnvSh, D) == offsetof(EnvSh, hdr) + sizeof(EnvSh::hdr) &&
-                  offsetof(EnvSh, NC) == offsetof(EnvSh, D) + sizeof(EnvSh::D),
+                  offsetof(EnvSh, NC) == offsetof(EnvSh, D) + sizeof(EnvSh::D) &&
+                  offsetof(EnvSh, G) == offsetof(EnvSh, NC) + sizeof(EnvSh::NC),
               "the scratch region must be contiguous");
-#define SCR_FLOATS ((int)((offsetof(EnvSh, NC) + sizeof(EnvSh::NC) - offsetof(EnvSh, J)) / 4))
+#define SCR_FLOATS ((int)((offsetof(EnvSh, G) + sizeof(EnvSh::G) - offsetof(EnvSh, J)) / 4))
 static_assert(COL_EPA + EPA_SCRATCH_FLOATS <= SCR_FLOATS, "EPA scratch exceeds the scratch region");
 static_assert(COL_WORK + MMX_MAXCON * CL_F <= SCR_FLOATS, "contact sort exceeds the scratch region");
+static_assert(COL_CON % 4 == 0 && COL_WORK % 4 == 0, "16-byte aligned collision scratch blocks");
 static_assert(COL_WORK + COL_PLANES * COL_POLY <= SCR_FLOATS, "box-box polygons exceed the scratch region");
 static_assert(MMX_CAND_CAP <= COL_LIST && MMX_NPAIR < 4096, "collision scratch layout");
 
@@ -198,15 +211,15 @@ DEV float* scr_of(EnvSh& E) { return reinterpret_cast<float*>(&E.J); }
 DEV const float* scr_of(const EnvSh& E) { return reinterpret_cast<const float*>(&E.J); }
 DEV float* obs_of(EnvSh& E) { return scr_of(E) + SCR_OBS; }
 DEV const float* obs_of(const EnvSh& E) { return scr_of(E) + SCR_OBS; }
-DEV CRec crec(const EnvSh& E, int c) { return CRec{&E.con[0][0], c}; }
-DEV float* lrow_of(EnvSh& E) { return &E.con[0][0]; }  // Hessian staging tiles (E.con is dead once the rows exist)
-// the general (cube-cube coupled) Cholesky's 27 x 27 transpose: rare, so in the env's HBM scratch
-// block after the overflow rows (MMX_OVF_F), not in LDS
-DEV float* arrow_of(EnvSh& E) { return E.ovf + 18 * MMX_OVFEFC; }
-
-// the rows' mu between the row build and the solver setup (E.con is dead once the rows exist)
-DEV float* mu_stage(EnvSh& E) { return &E.con[0][0]; }
-static_assert(MMX_MAXEFC <= MMX_MAXCON * CL_F, "row mu staging exceeds E.con");
+// the contacts (from the narrowphase to the row build, which takes them into registers)
+DEV float* con_of(EnvSh& E) { return scr_of(E) + COL_CON; }
+DEV CRec crec(const EnvSh& E, int c) { return CRec{scr_of(E) + COL_CON, c}; }
+DEV float* lrow_of(EnvSh& E) { return E.G; }  // the Hessian staging tile
+// the general (cube-cube coupled) Cholesky's 27 x 27 transpose: rare, so in the env's HBM overflow
+// block after the overflow rows, not in LDS
+DEV float* arrow_of(EnvSh& E) { return E.ovf + MMX_OVF_ARROW_AT(MMX_LDSEFC); }
+// the persistent broadphase list (16-bit pair indices) in the overflow block
+DEV unsigned short* cand_of(const EnvSh& E) { return reinterpret_cast<unsigned short*>(E.ovf + MMX_OVF_CAND_AT(MMX_LDSEFC)); }
 // Constraint row i: J in E.J[.][i] (chunk-major) and D in E.D[i] for i < MMX_LDSEFC, else in the env's HBM
 // overflow block (J rows [OVFEFC][16], then D [OVFEFC]).  For a lane-owned row i = LANE + 64 q the
 // test folds at compile time (LANE's known bits), so the unrolled loops carry no branch.
@@ -231,6 +244,13 @@ DEV void dset(EnvSh& E, int i, float v) {
   else *ovf_d(E, i) = v;
 }
 DEV float ncget(const EnvSh& E, int i) { return i < MMX_LDSEFC ? E.NC[i] : *ovf_nc(E, i); }
+// row headers: LDS for the LDS rows, the overflow block's byte array for the rest
+DEV unsigned char* ovf_hdr(const EnvSh& E) { return reinterpret_cast<unsigned char*>(E.ovf + MMX_OVF_HDR_AT(MMX_LDSEFC)); }
+DEV int hdr_get(const EnvSh& E, int i) { return i < MMX_LDSEFC ? E.hdr[i] : ovf_hdr(E)[i - MMX_LDSEFC]; }
+DEV void hdr_set(EnvSh& E, int i, int h) {
+  if (i < MMX_LDSEFC) E.hdr[i] = (unsigned char)h;
+  else ovf_hdr(E)[i - MMX_LDSEFC] = (unsigned char)h;
+}
 DEV void ncset(EnvSh& E, int i, float v) {
   if (i < MMX_LDSEFC) E.NC[i] = v;
   else *ovf_nc(E, i) = v;
@@ -240,8 +260,8 @@ DEV void ncset(EnvSh& E, int i, float v) {
 DEV void ovf_fence(int nefc) {
   if (nefc > MMX_LDSEFC) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 }
-// the last substep's contacts (diagnostic copy, mmx_buffers.contacts), stored once the rows are
-// built: the solver then reuses E.con as scratch
+// the last substep's contacts (diagnostic copy, mmx_buffers.contacts), stored before the row build
+// overwrites the scratch region that holds them
 DEV void store_contacts(float* dst, const EnvSh& E) {
   const int n = E.ncon;
   for (int c = LANE; c < MMX_MAXCON; c += WG) {  // the 13-field record (CON_*) of LDS contact c
@@ -793,7 +813,7 @@ struct WaveSink {
   DEV void put(int slot, int g1, int g2, float dist, V3 pos, V3 nrm) {
     if (slot >= MMX_MAXCON) return;
     nrm = normalize(nrm);
-    const CRecW c{&E->con[0][0], slot};
+    const CRecW c{scr_of(*E) + COL_CON, slot};
     c[CL_DIST] = dist;
     c[CL_POS] = pos.x; c[CL_POS + 1] = pos.y; c[CL_POS + 2] = pos.z;
     c[CL_N] = nrm.x; c[CL_N + 1] = nrm.y; c[CL_N + 2] = nrm.z;
@@ -911,14 +931,16 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
     return dot(d, d) <= rb * rb;
   };
   int nc = 0;
-  if (use_list) {  // uniform: the list's pairs only (<= MMX_CAND_CAP, pair order)
+  if (use_list) {  // uniform: the list's pairs only (<= MMX_CAND_CAP, pair order; in the overflow block)
     const int n = E.ncand;
     constexpr int NLP = (MMX_CAND_CAP + WG - 1) / WG;
     int lp[NLP], lk[NLP];  // every pass's pair-table gather in flight at once
+    const unsigned short* cl = cand_of(E);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");  // the rebuild's stores (below)
 #pragma unroll
     for (int q = 0; q < NLP; q++) {
       const int k = q * WG + LANE;
-      lp[q] = k < n ? (int)E.cand[k] : 0;
+      lp[q] = k < n ? (int)cl[k] : 0;
       lk[q] = WG * q < n ? MMX_pair_packed[lp[q]] : 0;
     }
 #pragma unroll
@@ -958,13 +980,16 @@ DEV void collide_prune(EnvSh& E, bool only_ro) {
     if (rebuild) {  // the inflated set -> the persistent list (pair order)
       const unsigned long long mi = ki[q];
       const int pos = __builtin_amdgcn_mbcnt_hi((unsigned)(mi >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mi, 0u));
-      if (((mi >> LANE) & 1ull) && ni + pos < MMX_CAND_CAP) E.cand[ni + pos] = (unsigned short)(q * WG + LANE);
+      if (((mi >> LANE) & 1ull) && ni + pos < MMX_CAND_CAP) cand_of(E)[ni + pos] = (unsigned short)(q * WG + LANE);
       ni += __popcll(mi);
     }
   }
-  if (rebuild && LANE == 0) {
-    E.ncand = ni <= MMX_CAND_CAP ? ni : -1;
-    E.cdisp = 0.f;
+  if (rebuild) {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // the list's stores complete before its next read
+    if (LANE == 0) {
+      E.ncand = ni <= MMX_CAND_CAP ? ni : -1;
+      E.cdisp = 0.f;
+    }
   }
   if (nc > COL_LIST) {  // uniform: more sphere-test survivors than the list holds (flagged; none in C3)
     if (LANE == 0) E.flags |= SHF_CON_OVF;
@@ -1093,10 +1118,10 @@ DEV void collide_sort(EnvSh& E) {
     const int key = kb & 0xFFFF;
     for (int j = 0; j < n; j++) rank += (con_key(crec(E, j)) & 0xFFFF) < key;
 #pragma unroll
-    for (int f = 0; f < CL_F; f++) tmp[f * MMX_MAXCON + rank] = E.con[f][LANE];
+    for (int f = 0; f < CL_F; f++) tmp[f * MMX_MAXCON + rank] = con_of(E)[f * MMX_MAXCON + LANE];
   }
   SYNC();
-  for (int k = LANE; k < MMX_MAXCON * CL_F; k += WG) (&E.con[0][0])[k] = tmp[k];
+  for (int k = LANE; k < MMX_MAXCON * CL_F; k += WG) con_of(E)[k] = tmp[k];
   if (LANE == 0) E.ncon = n;
   SYNC();
   PROBE(5, stats, STAT_T_AUX3);
@@ -1134,7 +1159,7 @@ DEV void store_row(EnvSh& E, int row, const float* jv, int hdr, float vel, float
     for (int q = 0; q < 3; q++) Jr[q] = make_float4(jv[4 * q], jv[4 * q + 1], jv[4 * q + 2], jv[4 * q + 3]);
     Jr[3] = make_float4(jv[12], jv[13], jv[14], aref);
   }
-  E.hdr[row] = (unsigned char)hdr;
+  hdr_set(E, row, hdr);
   dset(E, row, 1.f / fmaxf(imp_ratio * diag, 1e-15f));
 }
 
@@ -1146,7 +1171,8 @@ struct ConPar {
   int dim;
   float mu0, mu1, kid, B, idiag;
 };
-DEV ConPar contact_params(CRec cc) {
+template <class R>
+DEV ConPar contact_params(const R& cc) {
   const int g1 = con_g1(cc), g2 = con_g2(cc);
   ConPar P;
   P.dim = max(MMX_geom_condim[g1], MMX_geom_condim[g2]);
@@ -1179,8 +1205,7 @@ DEV V3 contact_t1(V3 n) {  // mju_makeFrame's first tangent
 // term belongs to the normal); the solver forms them from these rows.  An arm block entry is the
 // motion subspace of dof d seen at the contact point, a cube block the free-body Jacobian.  Rows the
 // contact's condim does not use are zero rows with D = 0.  Returns the row's mu (-1: no edges).
-DEV float contact_row(EnvSh& E, int row, int c, int rr, const ConPar& P) {
-  const CRec cc = crec(E, c);
+DEV float contact_row(EnvSh& E, int row, const CReg& cc, int rr, const ConPar& P) {
   const V3 p = V3{cc[CL_POS], cc[CL_POS + 1], cc[CL_POS + 2]};
   const V3 n = V3{cc[CL_N], cc[CL_N + 1], cc[CL_N + 2]};
   const int b1 = MMX_geom_body[con_g1(cc)], b2 = MMX_geom_body[con_g2(cc)];
@@ -1258,13 +1283,18 @@ DEV float contact_row(EnvSh& E, int row, int c, int rr, const ConPar& P) {
 // written by their lanes; contact rows are spread over all lanes through a row -> (contact, basis
 // row) map.  Rows are grouped by block-pair type in aligned groups of 4 (type 0 starts with the
 // equality / limit rows, padded with zero rows to a multiple of 4); the rows' mu (the solver's
-// edge coefficients) are staged in E.con once every contact row is built.
-DEV void make_constraints_wave(EnvSh& E) {
+// edge coefficients) go to the solver in registers (mu_out, the lane's rows LANE + 64 q).
+DEV void make_constraints_wave(EnvSh& E, float* mu_out) {
   float* stats = E.stats;
   CLK_DECL;
   const float def_ref[2] = {0.02f, 1.0f};
   const float def_imp[5] = {0.9f, 0.95f, 0.001f, 0.5f, 2.0f};
   const int ncon = E.ncon;
+  // the lane's own contact into registers (lane c: contact c): the rows overwrite the scratch region
+  // that holds the contacts, and each row's lane reads its contact's fields from lane c (ds_bpermute)
+  CReg own;
+#pragma unroll
+  for (int k = 0; k < CL_F; k++) own.v[k] = LANE < ncon ? crec(E, LANE)[k] : 0.f;
   // row -> (contact, basis row) map, -1 for the equality / limit / padding rows; it lives in the
   // rows' D (dset / dget), so the equality / limit rows (whose store_row writes D) are stored after
   // the contact rows
@@ -1278,7 +1308,7 @@ DEV void make_constraints_wave(EnvSh& E) {
     nlim = (int)lo_act + (int)hi_act;
   }
   if (LANE < ncon) {
-    const int g1 = con_g1(crec(E, LANE)), g2 = con_g2(crec(E, LANE));
+    const int g1 = con_g1(own), g2 = con_g2(own);
     const int dim = max(MMX_geom_condim[g1], MMX_geom_condim[g2]);
     nedge = dim == 1 ? 1 : 2 * (dim - 1);
     const int k1 = body_block(MMX_geom_body[g1]), k2 = body_block(MMX_geom_body[g2]);
@@ -1333,7 +1363,7 @@ DEV void make_constraints_wave(EnvSh& E) {
   // each contact's parameters computed once, by its lane, and read by its rows' lanes over ds_bpermute
   // (computing them per row measured -1.3 %)
   ConPar Pc{1, 0.f, 0.f, 0.f, 0.f, 1.f};
-  if (LANE < ncon) Pc = contact_params(crec(E, LANE));
+  if (LANE < ncon) Pc = contact_params(own);
   if (LANE < ncon) {  // the contact's 4 basis rows in the row -> (contact, basis row) map
 #pragma unroll
     for (int rr = 0; rr < 4; rr++)
@@ -1358,7 +1388,11 @@ DEV void make_constraints_wave(EnvSh& E) {
     P.kid = __shfl(Pc.kid, c);
     P.B = __shfl(Pc.B, c);
     P.idiag = __shfl(Pc.idiag, c);
-    if (m >= 0) mu[q] = contact_row(E, r, c, m >> 8, P);
+    CReg cc;  // contact c's position, normal and geoms from lane c
+    cc.v[CL_DIST] = 0.f;
+#pragma unroll
+    for (int k = CL_POS; k < CL_F; k++) cc.v[k] = __shfl(own.v[k], c);
+    if (m >= 0) mu[q] = contact_row(E, r, cc, m >> 8, P);
   }
   row = arow;
   float jv[16];
@@ -1395,11 +1429,9 @@ DEV void make_constraints_wave(EnvSh& E) {
     dset(E, nsingle_raw + LANE, 0.f);
   }
   ovf_fence(nefc);
-  SYNC();  // every contact row is built: E.con is dead, the rows' mu go there for the solver setup
+  SYNC();  // every row is built; the rows' mu go to the solver in registers
 #pragma unroll
-  for (int q = 0; q < RPB; q++)
-    if (LANE + WG * q < nefc) mu_stage(E)[LANE + WG * q] = mu[q];
-  SYNC();
+  for (int q = 0; q < RPB; q++) mu_out[q] = mu[q];
   PROBE(3, stats, STAT_T_AUX2);
 }
 
@@ -1428,7 +1460,7 @@ __host__ __device__ constexpr int newton_lane(int d) { return d < 9 ? d : 16 * (
 
 // J_i . x for a block-format row (slots past the row's width hold zeros)
 DEV float row_dot16(const EnvSh& E, int i, const float* x) {
-  const int h = E.hdr[i], b0 = h & 15, b1 = (h >> 4) & 15;
+  const int h = hdr_get(E, i), b0 = h & 15, b1 = (h >> 4) & 15;
   const int n0 = blk_size(b0), o0 = blk_d0(b0), o1 = (b1 == BLK_NONE ? 0 : blk_d0(b1)) - n0;
   float jv[16];
 #pragma unroll
@@ -1567,10 +1599,6 @@ DEV void cost2_wave(const EnvSh& E, const float* xa, const float* xb, const floa
 // dof lanes into their Hessian row (static columns) and gradient.  Returns, in lane j < 27,
 // row j of H = M + J'WJ in hrow[0..27) and g_j = (M (x - xs) + J'W r)_j.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-// staging tile row stride: 17, so the dof lanes' reads of different tile rows (tile_gather) fall on
-// different banks (a 16-float stride put rows sd and sd + 2 on one bank: up to 5-way; with the
-// polygon stride below, LDS bank conflicts 0.31 -> 0.12 per LDS-active cycle, +0.2 % in the A/B)
-#define GST 17
 // groups (MFMA steps) per trip, their loads issued together (3 or 4: -1.3 / -0.7 % in the r03 A/B)
 #define MMX_HESS_U 2
 // gather one row type's staged 16 x 16 tile into the dof lanes' Hessian rows: dof lane d reads row
@@ -2034,18 +2062,18 @@ DEV float chol_solve(EnvSh& E, const float* hrow, float v, int cpl) {
 
 // exit: 0 converged (gradient below tol), 1 no progress (step below 1e-9 with the gradient above
 // tol: an fp32 stall), 2 iteration cap reached above tol
-DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid, int& exit) {
+DEV int newton_wave(EnvSh& E, int max_iter, float tol, float& resid, int& exit, const float* mu_in) {
   float* stats = E.stats;
   CLK_DECL;
   const int nefc = E.nefc, nsingle = E.nsingle;
-  // per owned row: D (1/R; the contact's common pyramid R), mu (staged in E.con by the row build,
-  // read before the Hessian staging tile reuses E.con) and the edge coefficients
+  // per owned row: D (1/R; the contact's common pyramid R), mu (from the row build, in registers) and
+  // the edge coefficients
   float dd[RPL], mu[RPL];
 #pragma unroll
   for (int q = 0; q < RPL; q++) {
     const int i = LANE + WG * q;
     dd[q] = i < nefc ? dget(E, i) : 0.f;
-    mu[q] = i < nefc ? mu_stage(E)[i] : 0.f;
+    mu[q] = i < nefc ? mu_in[q] : 0.f;
   }
   // start from the cheaper of the warm start and qacc_smooth (as MuJoCo does)
   float c_ws, c_s, ra[RPL], rs[RPL], mws, ms;
@@ -2508,11 +2536,12 @@ DEV void mj_step_wave(int max_iter, float tol, EnvSh& E, float* con_dst) {
   collide_wave(E, false);
   CLK(stats, STAT_T_COL);
   if (con_dst) store_contacts(con_dst, E);  // before the row build reuses contact fields
-  make_constraints_wave(E);
+  float mu[RPL];  // the lane's rows' mu (LANE + 64 q), from the row build to the solver
+  make_constraints_wave(E, mu);
   CLK(stats, STAT_T_CON);
   float resid = 0.f;
   int exit = 0;
-  const int it = newton_wave(E, max_iter, tol, resid, exit);
+  const int it = newton_wave(E, max_iter, tol, resid, exit, mu);
   CLK(stats, STAT_T_SOLVE);
   integrate_wave(E);
   CLK(stats, STAT_T_INT);

@@ -17,15 +17,26 @@
 // constraint rows (basis rows: 4 per contact + equality / limits padded to 4; <= 64 x 4 + 20)
 #define MMX_MAXEFC 320
 // constraint rows [0, MMX_LDSEFC) live in the workgroup's LDS, rows [MMX_LDSEFC, MMX_MAXEFC) in the
-// env's HBM overflow block (efc_ovf); 128 rows keep the env's LDS at 14,064 B (11 envs per CU: the
-// LDS is allocated in 1,280-byte blocks, tools/calib/lds_occ.hip; r01-r04: 192 rows, 20 KB, 8 per CU)
+// env's HBM overflow block (efc_ovf); 128 rows keep the env's LDS within 12,800 B (twelve envs per CU:
+// the LDS is allocated in 1,280-byte blocks, tools/calib/lds_occ.hip; r05: 14,080 B, 11 per CU; r01-r04:
+// 192 rows, 20 KB, 8 per CU)
 #ifndef MMX_LDSEFC
 #define MMX_LDSEFC 128
 #endif
 #define MMX_OVFEFC (MMX_MAXEFC - MMX_LDSEFC)
-// floats per env: J rows [OVFEFC][16], then D, NC [OVFEFC], then the general Cholesky's 27 x 27
-// transpose (+3: 16-byte aligned blocks)
-#define MMX_OVF_F (MMX_OVFEFC * 18 + 27 * 27 + 3)
+// persistent broadphase list entries (pair indices, in the env's overflow block; a longer list is not
+// kept: the full prune runs)
+#ifndef MMX_CAND_CAP  // (test builds lower it with MMX_COL_LIST: tests/test_overflow_kat.py)
+#define MMX_CAND_CAP 256
+#endif
+// the env's HBM overflow block, in floats: J rows [OVFEFC][16], then D, NC [OVFEFC], then the general
+// Cholesky's 27 x 27 transpose (+3: 16-byte aligned blocks), then the overflow rows' headers (bytes)
+// and the broadphase list (16-bit pair indices)
+#define MMX_OVF_ARROW_AT(efc) (18 * (MMX_MAXEFC - (efc)))
+#define MMX_OVF_HDR_AT(efc) (MMX_OVF_ARROW_AT(efc) + 27 * 27 + 3)
+#define MMX_OVF_CAND_AT(efc) (MMX_OVF_HDR_AT(efc) + (MMX_MAXEFC - (efc) + 3) / 4)
+#define MMX_OVF_F_AT(efc) ((MMX_OVF_CAND_AT(efc) + (MMX_CAND_CAP + 1) / 2 + 3) / 4 * 4)  // (16-byte env blocks)
+#define MMX_OVF_F MMX_OVF_F_AT(MMX_LDSEFC)
 #define MMX_NSUBSTEP 16
 
 // stale kinematics cache read by the IK (controller.py:99-108 reads data.xpos / mj_jac

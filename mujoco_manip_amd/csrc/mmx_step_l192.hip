@@ -10,4 +10,4 @@
 #define MMX_STEP_SUFFIX _l192
 #include "mmx_kernels.hip"
 // mmx_api.cpp allocates S.efc_ovf with the 128-row build's per-env stride, which must cover this one's
-static_assert(MMX_OVF_F <= (MMX_MAXEFC - 128) * 18 + 27 * 27 + 3, "overflow block stride exceeds the allocation");
+static_assert(MMX_OVF_F <= MMX_OVF_F_AT(128), "overflow block stride exceeds the allocation");
