@@ -468,33 +468,73 @@ DEV void wave_argmax(float& v, int& i) {
   v = bv;
   i = bi;
 }
-DEV V3 support_wave(const Geom& G, V3 dir) {
+// A mesh geom's hull vertices held in registers for one GJK / EPA pair (r06): lane l holds vertices
+// l, l + 64, l + 128 in the mesh frame, loaded once per pair, so a support query is three FMAs per
+// vertex, the wave arg-max and three v_readlane of the winner's coordinates from its lane (was: the
+// vertex loads from the constant tables in every query and a dependent load of the winner after it).
+#define HULL_PER_LANE 3
+struct Hull {
+  float x[HULL_PER_LANE], y[HULL_PER_LANE], z[HULL_PER_LANE];
+  int nvert;  // 0: not a mesh (support() of the primitive)
+};
+DEV void hull_load(const Geom& G, Hull& H) {
+  H.nvert = 0;
+#pragma unroll
+  for (int k = 0; k < HULL_PER_LANE; k++) H.x[k] = H.y[k] = H.z[k] = 0.f;
+  if (G.type != GT_MESH) return;
+  const int m = MMX_geom_mesh[G.g];
+  const int a = MMX_mesh_vertadr[m];
+  H.nvert = MMX_mesh_vertnum[m];
+#pragma unroll
+  for (int k = 0; k < HULL_PER_LANE; k++) {
+    const int v = (int)(threadIdx.x & 63) + 64 * k;
+    if (v < H.nvert) {
+      H.x[k] = MMX_mesh_vert[3 * (a + v)];
+      H.y[k] = MMX_mesh_vert[3 * (a + v) + 1];
+      H.z[k] = MMX_mesh_vert[3 * (a + v) + 2];
+    }
+  }
+}
+DEV V3 support_wave(const Geom& G, const Hull& H, V3 dir) {
   if (G.type != GT_MESH) return support(G, dir);
   const V3 dl = mulT(G.R, dir);
-  const int m = MMX_geom_mesh[G.g];
-  const int a = MMX_mesh_vertadr[m], nvert = MMX_mesh_vertnum[m];
-  float best = -3.0e38f;
+  float best = -3.0e38f, bx = 0.f, by = 0.f, bz = 0.f;
   int bi = 0x7fffffff;
-  for (int v = (int)(threadIdx.x & 63); v < nvert; v += 64) {
-    const int q = 3 * (a + v);
-    const float s = MMX_mesh_vert[q] * dl.x + MMX_mesh_vert[q + 1] * dl.y + MMX_mesh_vert[q + 2] * dl.z;
-    if (s > best) {
-      best = s;
-      bi = v;
+#pragma unroll
+  for (int k = 0; k < HULL_PER_LANE; k++) {  // the lane's vertices in index order (strict >: the lower on ties)
+    const int v = (int)(threadIdx.x & 63) + 64 * k;
+    if (v < H.nvert) {
+      const float s = H.x[k] * dl.x + H.y[k] * dl.y + H.z[k] * dl.z;
+      if (s > best) {
+        best = s;
+        bi = v;
+        bx = H.x[k];
+        by = H.y[k];
+        bz = H.z[k];
+      }
     }
   }
   wave_argmax(best, bi);
-  const int q = 3 * (a + bi);
-  return G.x + mul(G.R, V3{MMX_mesh_vert[q], MMX_mesh_vert[q + 1], MMX_mesh_vert[q + 2]});
+  const int wl = bi & 63;  // the winner's lane holds its coordinates as its own best
+  const V3 p = V3{__int_as_float(__builtin_amdgcn_readlane(__float_as_int(bx), wl)),
+                  __int_as_float(__builtin_amdgcn_readlane(__float_as_int(by), wl)),
+                  __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bz), wl))};
+  return G.x + mul(G.R, p);
 }
 
 struct SVx {
   V3 w, a, b;
 };
-DEV SVx mk_sv(const Geom& A, const Geom& B, V3 dir) {
+// the pair's geoms with their cached hulls
+struct GPair {
+  const Geom& A;
+  const Geom& B;
+  Hull HA, HB;
+};
+DEV SVx mk_sv(const GPair& P, V3 dir) {
   SVx s;
-  s.a = support_wave(A, dir);
-  s.b = support_wave(B, -dir);
+  s.a = support_wave(P.A, P.HA, dir);
+  s.b = support_wave(P.B, P.HB, -dir);
   s.w = s.a - s.b;
   return s;
 }
@@ -562,15 +602,15 @@ DEV bool gjk_tet(const SVx& s0, SVx& s1, SVx& s2, SVx& s3, int& n, V3& dir) {
   n = 4;
   return true;
 }
-DEV bool gjk(const Geom& A, const Geom& B, SVx& s0, SVx& s1, SVx& s2, SVx& s3, int& n) {
-  V3 dir = A.x - B.x;
+DEV bool gjk(const GPair& GP, SVx& s0, SVx& s1, SVx& s2, SVx& s3, int& n) {
+  V3 dir = GP.A.x - GP.B.x;
   if (norm(dir) < 1e-9f) dir = V3{1.f, 0.f, 0.f};
-  s0 = mk_sv(A, B, dir);
+  s0 = mk_sv(GP, dir);
   n = 1;
   dir = -s0.w;
   for (int it = 0; it < 48; it++) {
     if (norm(dir) < 1e-12f) return true;
-    const SVx P = mk_sv(A, B, dir);
+    const SVx P = mk_sv(GP, dir);
     if (dot(P.w, dir) < 0.f) return false;
     s3 = s2;  // push P; entries beyond n are dead
     s2 = s1;
@@ -622,13 +662,12 @@ DEV int epa_prefix(unsigned long long m) {  // set bits of m below this lane
 // lane and appended in edge order; the horizon edge list itself is built from the visible faces in
 // index order with the serial add / cancel rule.  Every array ends each iteration exactly as the
 // serial loops left it (same faces, same order, same arithmetic per face).
-DEV bool epa(const Geom& A, const Geom& B, SVx* V, int nv, V3& nrm, float& depth, V3& pa, V3& pb, EFace* F,
-             int* edges) {
+DEV bool epa(const GPair& GP, SVx* V, int nv, V3& nrm, float& depth, V3& pa, V3& pb, EFace* F, int* edges) {
   int nf = 0;
   if (nv == 1) {
     for (int k = 0; k < 6 && nv < 2; k++) {  // +x, -x, +y, -y, +z, -z
       const float sg = (k & 1) ? -1.f : 1.f;
-      V[nv] = mk_sv(A, B, V3{k < 2 ? sg : 0.f, (k >> 1) == 1 ? sg : 0.f, k >= 4 ? sg : 0.f});
+      V[nv] = mk_sv(GP, V3{k < 2 ? sg : 0.f, (k >> 1) == 1 ? sg : 0.f, k >= 4 ? sg : 0.f});
       if (norm(V[nv].w - V[0].w) > 1e-7f) nv++;
     }
   }
@@ -638,14 +677,14 @@ DEV bool epa(const Geom& A, const Geom& B, SVx* V, int nv, V3& nrm, float& depth
                       ? V3{1.f, 0.f, 0.f}
                       : (fabsf(ab.y) <= fabsf(ab.z) ? V3{0.f, 1.f, 0.f} : V3{0.f, 0.f, 1.f});
     const V3 t = normalize(cross(ab, ax));
-    V[2] = mk_sv(A, B, t);
-    if (norm(cross(V[2].w - V[0].w, ab)) < 1e-10f) V[2] = mk_sv(A, B, -t);
+    V[2] = mk_sv(GP, t);
+    if (norm(cross(V[2].w - V[0].w, ab)) < 1e-10f) V[2] = mk_sv(GP, -t);
     nv = 3;
   }
   if (nv == 3) {
     const V3 n = normalize(cross(V[1].w - V[0].w, V[2].w - V[0].w));
-    V[3] = mk_sv(A, B, n);
-    if (fabsf(dot(V[3].w - V[0].w, n)) < 1e-9f) V[3] = mk_sv(A, B, -n);
+    V[3] = mk_sv(GP, n);
+    if (fabsf(dot(V[3].w - V[0].w, n)) < 1e-9f) V[3] = mk_sv(GP, -n);
     nv = 4;
   }
   const int T[4][3] = {{0, 1, 2}, {0, 3, 1}, {0, 2, 3}, {1, 3, 2}};
@@ -677,7 +716,7 @@ DEV bool epa(const Geom& A, const Geom& B, SVx* V, int nv, V3& nrm, float& depth
     if (best < 0) return false;
     const V3 fn = F[best].n;
     const float fd = F[best].d;
-    const SVx P = mk_sv(A, B, fn);
+    const SVx P = mk_sv(GP, fn);
     const float dist = dot(P.w, fn);
     if (dist - fd < 1e-6f * (1.f + fabsf(dist)) || nv >= EPA_MAXV) break;
     // which faces P sees (lane ln: faces ln and ln + 64), the others kept in index order
@@ -762,9 +801,12 @@ DEV bool epa(const Geom& A, const Geom& B, SVx* V, int nv, V3& nrm, float& depth
 // scr: EPA_SCRATCH_FLOATS of LDS; emits at most one contact (lane 0)
 template <class Sink>
 DEV void convex_convex(Sink& cs, const Geom& A, const Geom& B, float* scr) {
+  GPair GP{A, B};
+  hull_load(A, GP.HA);
+  hull_load(B, GP.HB);
   SVx s0, s1, s2, s3;
   int n = 0;
-  if (!gjk(A, B, s0, s1, s2, s3, n)) return;
+  if (!gjk(GP, s0, s1, s2, s3, n)) return;
   SVx* V = reinterpret_cast<SVx*>(scr);
   EFace* F = reinterpret_cast<EFace*>(scr + 9 * EPA_MAXV);
   int* edges = reinterpret_cast<int*>(scr + 9 * EPA_MAXV + 5 * EPA_MAXF);
@@ -774,7 +816,7 @@ DEV void convex_convex(Sink& cs, const Geom& A, const Geom& B, float* scr) {
   if (n > 3) V[3] = s3;
   V3 nrm, pa, pb;
   float depth;
-  if (!epa(A, B, V, n, nrm, depth, pa, pb, F, edges)) return;
+  if (!epa(GP, V, n, nrm, depth, pa, pb, F, edges)) return;
   if (depth < 0.f) return;
   // Minkowski A-B face normal n: translating B by +depth n separates -> normal A->B is n
   if ((threadIdx.x & 63) == 0) cs.add(A.g, B.g, -depth, (pa + pb) * 0.5f, nrm);

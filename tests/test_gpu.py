@@ -457,11 +457,23 @@ def test_rollout_lanes_bit_identical(monkeypatch):
     np.testing.assert_array_equal(outs[0], outs[1])
 
 
+def _plan_launches(n, fuse, lanes):
+    """mmx_rollout_expert's plan (mmx_api.cpp rollout_plan): len = min(fuse, ceil(n / 4)); lane l starts
+    with l * len / lanes steps, then launches of len, then the remainder; the most launches of a lane."""
+    ln = max(1, min(fuse, -(-n // 4)))
+    out = 0
+    for l in range(lanes):
+        first = min(n, l * ln // lanes)
+        out = max(out, (1 if first else 0) + -(-(n - first) // ln))
+    return out
+
+
 def test_fused_rollout_bit_identical(monkeypatch):
     """Several env steps per launch (mmx_rollout_steps_per_launch, mmx_rollout_launches) change
     nothing but timing: state, episode records, observations, rewards, flags and solver stats match
     one launch per step bit for bit, incl. autoresets inside a fused launch and launches of unequal
-    length (43 steps at a cap of 7 or 32: 8 launches of min(cap, ceil(43 / 8)) = 6 -> 6,6,6,5,5,5,5,5)."""
+    length (43 steps at a cap of 7 on one lane: 7 x 6 + 1; at a cap of 32 on three staggered lanes:
+    11,11,11,10 / 3,11,11,11,7 / 7,11,11,11,3)."""
     import oracle_py as O
     from mujoco_manip_amd import _lib
     from mujoco_manip_amd.vec_env import PickPlaceVecEnv
@@ -474,8 +486,8 @@ def test_fused_rollout_bit_identical(monkeypatch):
         env = PickPlaceVecEnv(12, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
                               autoreset=True, image_size=0, max_episode_steps=25)
         assert env.sim.rollout_steps_per_launch == int(fuse)
-        assert env.sim.rollout_launches(43) == (43 if fuse == "1" else 8)
-        assert env.sim.rollout_launches(512) == -(-512 // min(int(fuse), 64))
+        assert env.sim.rollout_launches(43) == _plan_launches(43, int(fuse), int(lanes))
+        assert env.sim.rollout_launches(512) == _plan_launches(512, int(fuse), int(lanes))
         env.reset(seed=seeds)
         env.rollout_expert(43)
         torch.cuda.synchronize()
