@@ -55,7 +55,7 @@ int mmx_rollout_render_launches(const mmx_sim* sim);
 int mmx_rollout_render_overlap(const mmx_sim* sim);
 
 /* Upper bound of the env steps one mmx_env_step_kernel launch runs per env in mmx_rollout_expert: 1
- * with cameras (every step is rendered), else 16 (env MMX_FUSE overrides).  A fused launch runs its
+ * with cameras (every step is rendered), else 32 (env MMX_FUSE overrides).  A fused launch runs its
  * envs' steps back to back inside each workgroup; the trajectories are bit-identical to one
  * launch per step.  0 for a null sim. */
 int mmx_rollout_steps_per_launch(const mmx_sim* sim);

@@ -60,8 +60,10 @@ struct mmx_sim {
   // so one range's last-wave tail overlaps the next step of the others.
   static constexpr int kMaxLanes = 8;
   int nlanes = 1;
-  // env steps per mmx_env_step_kernel launch in expert rollouts without cameras (MMX_FUSE overrides)
-  int fuse = 16;
+  // cap on the env steps per mmx_env_step_kernel launch in expert rollouts without cameras (MMX_FUSE
+  // overrides): with the staggered lanes 32 beat 16 by 0.5 % and 8 lost 2.7 % on 512-step C3 windows
+  // (profiles/r06_sweep_launch_shape.json)
+  int fuse = 32;
   // constraint rows the env-step kernel keeps in LDS: 128 (eleven envs per CU, the default) or 192
   // (eight per CU, mmx_step_l192.hip: faster when the batch leaves CU slots empty; mmx_set_step_rows,
   // MMX_STEP_ROWS)
