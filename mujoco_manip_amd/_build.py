@@ -57,6 +57,9 @@ TEST_VARIANTS = {
     # a 4-entry collision candidate list (product: 320): the sphere-test overflow path, flagged as
     # ERR_CON_OVERFLOW in env_error
     "libmmx_col4.so": ["MMX_COL_LIST=4", "MMX_CAND_CAP=4"],
+    # a 1-entry persistent broadphase list: every collision pass runs the full 780-pair prune (the
+    # list-vs-full-prune bit-identity test)
+    "libmmx_nolist.so": ["MMX_CAND_CAP=1"],
 }
 
 
