@@ -468,50 +468,28 @@ DEV void wave_argmax(float& v, int& i) {
   v = bv;
   i = bi;
 }
-// A mesh geom's hull vertices held in registers for one GJK / EPA pair (r06): lane l holds vertices
-// l, l + 64, l + 128 in the mesh frame, loaded once per pair, so a support query is three FMAs per
-// vertex, the wave arg-max and three v_readlane of the winner's coordinates from its lane (was: the
-// vertex loads from the constant tables in every query and a dependent load of the winner after it).
-#define HULL_PER_LANE 3
-struct Hull {
-  float x[HULL_PER_LANE], y[HULL_PER_LANE], z[HULL_PER_LANE];
-  int nvert;  // 0: not a mesh (support() of the primitive)
-};
-DEV void hull_load(const Geom& G, Hull& H) {
-  H.nvert = 0;
-#pragma unroll
-  for (int k = 0; k < HULL_PER_LANE; k++) H.x[k] = H.y[k] = H.z[k] = 0.f;
-  if (G.type != GT_MESH) return;
-  const int m = MMX_geom_mesh[G.g];
-  const int a = MMX_mesh_vertadr[m];
-  H.nvert = MMX_mesh_vertnum[m];
-#pragma unroll
-  for (int k = 0; k < HULL_PER_LANE; k++) {
-    const int v = (int)(threadIdx.x & 63) + 64 * k;
-    if (v < H.nvert) {
-      H.x[k] = MMX_mesh_vert[3 * (a + v)];
-      H.y[k] = MMX_mesh_vert[3 * (a + v) + 1];
-      H.z[k] = MMX_mesh_vert[3 * (a + v) + 2];
-    }
-  }
-}
-DEV V3 support_wave(const Geom& G, const Hull& H, V3 dir) {
+// Mesh support query over the wave: the hull's vertices strided by lane (each lane keeps the best of
+// its own and that vertex's coordinates), the wave arg-max (ties: the lowest index, as the serial
+// scan), then the winner's coordinates by v_readlane from its lane (r06: no dependent reload of the
+// winning vertex from the constant tables).  Caching the hull in registers for the whole GJK / EPA
+// pair measured no faster (the extra live registers cost spill slots, CHANGELOG r06).
+DEV V3 support_wave(const Geom& G, V3 dir) {
   if (G.type != GT_MESH) return support(G, dir);
   const V3 dl = mulT(G.R, dir);
+  const int m = MMX_geom_mesh[G.g];
+  const int a = MMX_mesh_vertadr[m], nvert = MMX_mesh_vertnum[m];
   float best = -3.0e38f, bx = 0.f, by = 0.f, bz = 0.f;
   int bi = 0x7fffffff;
-#pragma unroll
-  for (int k = 0; k < HULL_PER_LANE; k++) {  // the lane's vertices in index order (strict >: the lower on ties)
-    const int v = (int)(threadIdx.x & 63) + 64 * k;
-    if (v < H.nvert) {
-      const float s = H.x[k] * dl.x + H.y[k] * dl.y + H.z[k] * dl.z;
-      if (s > best) {
-        best = s;
-        bi = v;
-        bx = H.x[k];
-        by = H.y[k];
-        bz = H.z[k];
-      }
+  for (int v = (int)(threadIdx.x & 63); v < nvert; v += 64) {
+    const int q = 3 * (a + v);
+    const float x = MMX_mesh_vert[q], y = MMX_mesh_vert[q + 1], z = MMX_mesh_vert[q + 2];
+    const float s = x * dl.x + y * dl.y + z * dl.z;
+    if (s > best) {
+      best = s;
+      bi = v;
+      bx = x;
+      by = y;
+      bz = z;
     }
   }
   wave_argmax(best, bi);
@@ -525,16 +503,15 @@ DEV V3 support_wave(const Geom& G, const Hull& H, V3 dir) {
 struct SVx {
   V3 w, a, b;
 };
-// the pair's geoms with their cached hulls
+// the pair's geoms
 struct GPair {
   const Geom& A;
   const Geom& B;
-  Hull HA, HB;
 };
 DEV SVx mk_sv(const GPair& P, V3 dir) {
   SVx s;
-  s.a = support_wave(P.A, P.HA, dir);
-  s.b = support_wave(P.B, P.HB, -dir);
+  s.a = support_wave(P.A, dir);
+  s.b = support_wave(P.B, -dir);
   s.w = s.a - s.b;
   return s;
 }
@@ -801,9 +778,7 @@ DEV bool epa(const GPair& GP, SVx* V, int nv, V3& nrm, float& depth, V3& pa, V3&
 // scr: EPA_SCRATCH_FLOATS of LDS; emits at most one contact (lane 0)
 template <class Sink>
 DEV void convex_convex(Sink& cs, const Geom& A, const Geom& B, float* scr) {
-  GPair GP{A, B};
-  hull_load(A, GP.HA);
-  hull_load(B, GP.HB);
+  const GPair GP{A, B};
   SVx s0, s1, s2, s3;
   int n = 0;
   if (!gjk(GP, s0, s1, s2, s3, n)) return;

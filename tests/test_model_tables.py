@@ -264,14 +264,3 @@ def test_kernel_and_oracle_headers_agree():
     np.testing.assert_allclose(orac["act_bias"][1], np.ravel([a["bias"] for a in MODEL["actuators"]]))
     np.testing.assert_allclose(orac["key_qpos"][1], MODEL["key_qpos"])
 
-
-def test_mesh_hulls_fit_the_register_cache():
-    """The GJK / EPA support queries hold a hull's vertices in registers, HULL_PER_LANE per lane of the
-    64-lane wave (mmx_geom.h): every compiled hull must fit."""
-    import re
-
-    src = open(os.path.join(REPO, "mujoco_manip_amd", "csrc", "mmx_model_gen.h")).read()
-    nv = [int(x) for x in re.search(r"MMX_mesh_vertnum\[\d+\] = \{([^}]*)\}", src).group(1).split(",")]
-    per_lane = int(re.search(r"#define HULL_PER_LANE (\d+)",
-                             open(os.path.join(REPO, "mujoco_manip_amd", "csrc", "mmx_geom.h")).read()).group(1))
-    assert max(nv) <= 64 * per_lane, (max(nv), per_lane)
