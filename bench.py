@@ -314,9 +314,9 @@ def main():
     # (obj_red, bin_red), keyframe start, no randomisation), c5 (c3 settings + 2 x 128^2 RGB
     # cameras per env step, 8192 envs per GPU as in the 65536-env / 8-GPU config)
     ap.add_argument("--workload", default="c3", choices=("c2", "c3", "c5"))
-    # env-step kernel layout (mmx_set_step_rows): 0 = the library's default (128 LDS rows / eleven envs
-    # per CU); C2's 1024 envs fill only 4 of a CU's slots, where the 192-row layout's faster envs win
-    # (+4 %), so the c2 workload uses it
+    # env-step kernel layout (mmx_set_step_rows, bit-identical results): 0 = the library's default (128
+    # LDS rows, twelve envs per CU); C2's 1024 envs are four per CU, where the 192-row layout at one wave
+    # per SIMD is faster per env, so the c2 workload uses it
     ap.add_argument("--step-rows", type=int, default=0, choices=(0, 128, 192))
     args = ap.parse_args()
     if args.workload == "c5":

@@ -15,12 +15,12 @@
 extern "C" {
 #endif
 
-/* Constraint rows the env-step kernel (mmx_step, mmx_rollout_expert) keeps in LDS: 128 (eleven envs
+/* Constraint rows the env-step kernel (mmx_step, mmx_rollout_expert) keeps in LDS: 128 (twelve envs
  * per CU, the default: the fastest layout once the batch fills the GPU's workgroup slots, C3 / C5 /
- * dataset generation) or 192 (eight per CU: faster per env, so for batches that leave slots empty,
- * e.g. C2's 1024 envs).  Env MMX_STEP_ROWS overrides at create.  The rows past the LDS ones live in
- * the env's HBM overflow block; the two layouts are bit-identical (a performance choice only).
- * MMX_EINVAL for any other value. */
+ * dataset generation) or 192 (four per CU, one wave per SIMD with its whole register file: faster per
+ * env, for batches of at most four envs per CU, e.g. C2's 1024).  Env MMX_STEP_ROWS overrides at
+ * create.  The rows past the LDS ones live in the env's HBM overflow block; the two layouts are
+ * bit-identical (a performance choice only).  MMX_EINVAL for any other value. */
 int mmx_set_step_rows(mmx_sim* sim, int32_t rows);
 int mmx_step_rows(const mmx_sim* sim);
 

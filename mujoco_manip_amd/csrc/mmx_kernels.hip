@@ -3184,10 +3184,12 @@ extern "C" int mmx_fsm_profile_fields() { return FSMP_N; }
 #endif  // MMX_STEP_ONLY
 #endif
 
-// waves per SIMD the step kernel's register allocation is made for (2: <= 256 VGPRs; the A/B build
-// MMX_STEP_WAVES=3 caps it at 168)
+// waves per SIMD the step kernel's register allocation is made for: 3 for the 128-row layout (168
+// VGPRs: twelve envs per CU); 1 for the 192-row layout, the one for batches that leave CU slots empty
+// (C2's 1024 envs are four per CU: one wave per SIMD, whose spare registers hold what 2 waves per SIMD
+// saved to scratch; C2 +1.1 %, profiles/r06_ab_c2_l192_waves.json)
 #ifndef MMX_STEP_WAVES
-#define MMX_STEP_WAVES (MMX_LDSEFC == 128 ? 3 : 2)
+#define MMX_STEP_WAVES (MMX_LDSEFC == 128 ? 3 : 1)
 #endif
 #ifndef MMX_STEP_SUFFIX
 #define MMX_STEP_SUFFIX

@@ -1,7 +1,8 @@
 #!/bin/bash
 # The one GPU-box runner (replaces the per-experiment gpu_*.sh scripts of r01-r05).  Usage, from the
 # repo root on the GPU box (gpurun -- 'bash tools/gpu.sh RECIPE [RECIPE ...]'); recipes run in order and
-# the first failure ends the call.  Outputs under gpurun_out/ (copied to profiles/ by hand).
+# the first failure ends the call.  Outputs under gpurun_out/ (copied to profiles/ by hand; the condensed
+# PMC files also under gpurun_out/profiles_out/).
 #   tests            GPU suite (pytest -m gpu, every failure listed) + smoke()
 #   quick            GPU suite (-x) + a 200-step C3 bench line
 #   bench:WL         bench line of workload WL (c3 with the CPU baseline; c2, c5; driver = the driver's
@@ -59,7 +60,8 @@ profile() {  # profile WL: trace + separate PMC passes (no trace domain combined
    timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_CYCLES_SALU \
      SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU --output-format csv -d $out/sqx_b -o run -- \
      python3 $ROOT/bench.py $args > $out/bench_sqx_b.log 2>&1) || { tail -5 $out/*.log; return 1; }
-  python3 tools/pmc_traffic.py --round $R --workload $wl --prof $out --timed-steps $steps
+  python3 tools/pmc_traffic.py --round $R --workload $wl --prof $out --timed-steps $steps || return 1
+  mkdir -p gpurun_out/profiles_out && cp profiles/${R}_${wl}_* profiles/pmc_${wl}.json gpurun_out/profiles_out/  # (only gpurun_out/ comes back)
 }
 
 trace_driver() {
@@ -82,7 +84,8 @@ render_pmc() {
    timeout -s KILL 200 rocprofv3 --kernel-include-regex mmx_render_kernel --pmc SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_INSTS_LDS \
      SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM --output-format csv \
      -d $ROOT/gpurun_out/rpmc/b -o run -- python3 $ROOT/bench.py $args > $ROOT/gpurun_out/rpmc/b.log 2>&1) || return 1
-  python3 tools/render_pmc.py --round $R --prof $ROOT/gpurun_out/rpmc
+  python3 tools/render_pmc.py --round $R --prof $ROOT/gpurun_out/rpmc || return 1
+  mkdir -p gpurun_out/profiles_out && cp profiles/${R}_render_pmc.json profiles/pmc_render.json gpurun_out/profiles_out/
 }
 
 fsm() {

@@ -109,10 +109,9 @@ def main():
     if os.path.isdir(lanes_dir):
         ln = timed_mean(per_dispatch(lanes_dir, ["SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU"]), n_timed)
         lane_util = ln["SQ_THREAD_CYCLES_VALU"] / max(64.0 * ln["SQ_ACTIVE_INST_VALU"], 1.0)
-    # resident one-wave workgroups (envs) per SIMD: at most 11 per CU since r05 (14,080 B of LDS per
-    # env in 1,280-byte allocation blocks, tools/calib/lds_occ.hip; 168 VGPRs), 8 per CU before
-    # (MMX_LDSEFC=192); fewer when the configuration has fewer envs than the 256 CUs hold (C2: 1024)
-    per_cu = float(os.environ.get("MMX_ENVS_PER_CU", "11"))
+    # resident one-wave workgroups (envs) per SIMD: at most 12 per CU since r06 (12,640 B of LDS per
+    # env in 1,280-byte blocks; r05: 11)
+    per_cu = float(os.environ.get("MMX_ENVS_PER_CU", "12"))
     waves_per_simd = min(per_cu * 256.0, float(line["config"]["envs_per_gpu"])) / 1024.0
     per_wave = sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_WAVE_CYCLES"]
     hbm = 2.0 * fetch * 1024.0 + write * 1024.0
