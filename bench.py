@@ -259,7 +259,11 @@ def binding_roof(pmc: dict | None, workload: str) -> dict | None:
            "hbm_frac_note": "HBM frac <= ~0.2 by design while the efc working set stays in LDS (DESIGN §4)",
            "units": "SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (quad-cycles): instructions per quad-cycle"}
     cal_f = os.path.join(REPO, "profiles", "r05_valu_issue_calibration.json")
-    ext_f = os.path.join(REPO, "profiles", f"r05_{workload}_sq_extended.json")
+    # the newest round's extended SQ pass of this workload (tools/gpu.sh profile:<workload>)
+    import glob
+
+    ext = sorted(glob.glob(os.path.join(REPO, "profiles", f"r0*_{workload}_sq_extended.json")))
+    ext_f = ext[-1] if ext else os.path.join(REPO, "profiles", f"r06_{workload}_sq_extended.json")
     try:
         # the calibration's measured issue (SQ units, 8 independent FMA chains per wave) at 1-4 waves per
         # SIMD, interpolated linearly to the kernel's resident waves per SIMD (2.75 at 11 envs per CU)

@@ -25,7 +25,7 @@ ARCH = os.environ.get("MMX_OFFLOAD_ARCH", "gfx950")
 # +3.7 % env steps/s (C3), parity tolerances unchanged.  Host code keeps IEEE semantics.
 # r04: no NaN / Inf / signed-zero semantics either (-ffinite-math-only -fno-signed-zeros): selects
 # and min / max lose their NaN guards, -2.3 % VALU instructions per env step and +1.1 % env steps/s
-# in the interleaved A/B (profiles/r04_ab_finite_math.json), GPU suite unchanged.  The divergence
+# in the interleaved A/B (profiles/archive/r04_ab_finite_math.json), GPU suite unchanged.  The divergence
 # detector (NaN / Inf / |v| >= 1e10 -> counted reset) is an integer bit test, exact under any of these.
 DEVICE_MATH = ["-Xarch_device", "-freciprocal-math", "-Xarch_device", "-fapprox-func",
                "-Xarch_device", "-ffinite-math-only", "-Xarch_device", "-fno-signed-zeros"]
@@ -45,7 +45,7 @@ DEVICE_NOSLP = ["-Xarch_device", "-fno-slp-vectorize"]
 FLAGS = DEVICE_MATH + DEVICE_SCHED + DEVICE_NOSLP + os.environ.get("MMX_EXTRA_FLAGS", "").split()
 # per-source flags.  The env-step kernel (r04 end): floating-point reassociation in device code
 # (-fassociative-math; explicit fmaf / DPP / readlane reductions keep their written order), -2 %
-# VALU instructions per env step, C3 +0.9 % in the interleaved A/B (profiles/r04_ab_assoc.json),
+# VALU instructions per env step, C3 +0.9 % in the interleaved A/B (profiles/archive/r04_ab_assoc.json),
 # GPU suite unchanged.  Not the renderer, whose shared-edge functions rely on one evaluation order.
 SOURCE_FLAGS = {"mmx_kernels.hip": ["-Xarch_device", "-fassociative-math"],
                 "mmx_step_l192.hip": ["-Xarch_device", "-fassociative-math"]}

@@ -3412,7 +3412,7 @@ extern "C" __global__ void __launch_bounds__(QWG) mmx_queue_kernel(MMXState S, M
 }
 
 // Dispatch order of an env range for the step kernel, longest first.  An env step's cycles follow its
-// FSM phase (profiles/r05_fsm_profile.json, cycles per env step): lift / move to bin / lower to bin
+// FSM phase (profiles/archive/r05_fsm_profile.json, cycles per env step): lift / move to bin / lower to bin
 // ~2.35 M, close gripper / settle ~2.0 M, release / retreat ~1.63 M, the rest ~1.3-1.42 M.  A counting
 // sort over those four classes (refined by rows, below) puts the long ones at the front of order[],
 // so the launch's last workgroups are short ones (C3 +2.0 %, C5 +3.8 %).  One workgroup of any size (a single
@@ -3451,7 +3451,7 @@ extern "C" __global__ void __launch_bounds__(1024) mmx_order_kernel(MMXState S, 
 
 // =========================================================================== host launchers
 // threads: 1024 when the launch has the GPU to itself, 64 beside other streams' step launches (a
-// 1,024-lane workgroup waited ~0.35 ms for a CU to drain there: profiles/r05_c3_kernel_stats.csv)
+// 1,024-lane workgroup waited ~0.35 ms for a CU to drain there: profiles/archive/r05_c3_kernel_stats.csv)
 extern "C" hipError_t mmx_launch_order(const MMXState* S, int base, int count, int* order, int threads, hipStream_t st) {
   if (count <= 0) return hipSuccess;
   if (threads != 64 && threads != 1024) return hipErrorInvalidValue;

@@ -48,7 +48,7 @@ NV = 27
 ARM_BODIES = ["link1", "link2", "link3", "link4", "link5", "link6", "link7", "hand", "left_finger", "right_finger"]
 CUBE_FAR = [(1.0, -1.0, 1.0), (1.2, -1.0, 1.0), (1.4, -1.0, 1.0)]  # far from everything: no contact
 DEF_SOLREF, DEF_SOLIMP = (0.02, 1.0), (0.9, 0.95, 0.001, 0.5, 2.0)
-KERNEL_TOL_QVEL = 1e-5  # fp32 kernel vs the fp64 answer after one substep (r05 measured <= 7.2e-7: profiles/r05_parity_margins_smooth.json)
+KERNEL_TOL_QVEL = 1e-5  # fp32 kernel vs the fp64 answer after one substep (r05 measured <= 7.2e-7: profiles/archive/r05_parity_margins_smooth.json)
 ORACLE_TOL_QVEL = 1e-8
 
 
