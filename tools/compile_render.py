@@ -167,7 +167,7 @@ def geom_to_body(v, pos, quat):
     return v @ R.T + np.asarray(pos, float)
 
 
-def build():
+def build(robot_tris=None, hand_weight=1.0):
     model = CM.compile_model()
     bodies = model["bodies"]
     bnames = [b["name"] for b in bodies]
@@ -227,6 +227,8 @@ def build():
         meshfile[m.get("name", os.path.splitext(fname)[0])] = os.path.join(CM.REF_DATA, "franka_emika_panda",
                                                                            "assets", fname)
 
+    robot = []  # (body id, material, verts, faces) of every visual part
+
     def walk(be):
         name = be.get("name")
         if name in ROBOT:
@@ -235,18 +237,25 @@ def build():
                     continue
                 assert ge.get("pos") is None and ge.get("quat") is None
                 v, t = load_obj_tris(meshfile[ge.get("mesh")])
-                mat = material(ge.get("material"), SEG["robot"])
-                if name.startswith("link"):  # arm links: convex pieces of each visual part
-                    for pv, pf in convex_pieces(v, LINK_PIECE_SIZE, LINK_PIECE_VERTS):
-                        parts.append((bnames.index(name), pv, pf, mat))
-                else:  # hand and fingers (the wrist camera's close-up): clustered meshes
-                    cv, cf = cluster_mesh(v, t, HAND_CELL if name == "hand" else FINGER_CELL)
-                    parts.append((bnames.index(name), cv, cf.tolist(), mat))
+                robot.append((bnames.index(name), material(ge.get("material"), SEG["robot"]), v, t))
         for c in be.findall("body"):
             walk(c)
 
     for be in panda.find("worldbody").findall("body"):
         walk(be)
+    if robot_tris:  # every visual part decimated under one triangle budget (tools/qem.py)
+        import qem
+        w = [hand_weight if bnames[b] in ("hand", "left_finger", "right_finger") else 1.0 for b, _, _, _ in robot]
+        for (b, m, _, _), (dv, dt) in zip(robot, qem.decimate_many([(v, t) for _, _, v, t in robot], robot_tris, w)):
+            parts.append((b, dv, dt.tolist(), m))
+    else:
+        for b, m, v, t in robot:
+            if bnames[b].startswith("link"):  # arm links: convex pieces of each visual part
+                for pv, pf in convex_pieces(v, LINK_PIECE_SIZE, LINK_PIECE_VERTS):
+                    parts.append((b, pv, pf, m))
+            else:  # hand and fingers (the wrist camera's close-up): clustered meshes
+                cv, cf = cluster_mesh(v, t, HAND_CELL if bnames[b] == "hand" else FINGER_CELL)
+                parts.append((b, cv, cf.tolist(), m))
 
     # flatten, vertices grouped by body
     verts, vbody, tris, tmat = [], [], [], []
