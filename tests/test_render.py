@@ -150,8 +150,10 @@ def _iou(a, b):
 
 
 # robot-mask IoU against the full 134,888-triangle visual meshes (tests/golden/make_robot_masks.py):
-# one convex hull per body (the r02 model) reached 0.89 (overhead) / 0.75 (wrist) on these states
-IOU_MIN = {"overhead": 0.90, "wrist": 0.94}
+# one convex hull per body (the r02 model) reached 0.89 (overhead) / 0.75 (wrist) on these states,
+# the r03-r05 convex pieces 0.92 / 0.97, the quadric-error model (tools/compile_render.py) 0.973 / 0.977
+IOU_MIN = {"overhead": 0.97, "wrist": 0.97}
+IOU_GPU_SLACK = 0.02  # the HIP rasteriser's edge rules against make_robot_masks.raster_depth: gate 0.95
 
 
 def test_render_model_robot_silhouettes_match_full_meshes():
@@ -196,7 +198,7 @@ def test_render_model_robot_silhouettes_match_full_meshes():
 @pytest.mark.gpu
 def test_gpu_robot_silhouettes_match_full_meshes():
     """The HIP renderer's robot segment (id 9) at 128 x 128 for the fixture's states against the
-    full visual meshes: mean IoU per camera above IOU_MIN less 0.02 (edge rules differ)."""
+    full visual meshes: mean IoU per camera above IOU_MIN less IOU_GPU_SLACK (edge rules differ)."""
     from mujoco_manip_amd import _lib
 
     if not torch.cuda.is_available():
@@ -215,7 +217,7 @@ def test_gpu_robot_silhouettes_match_full_meshes():
     for ci, cam in enumerate(("overhead", "wrist")):
         ious = [_iou(seg[k, ci] == 9, d["masks"][k, ci].astype(bool)) for k in range(n)]
         print(cam, [round(x, 3) for x in ious])
-        assert np.mean(ious) >= IOU_MIN[cam] - 0.02, (cam, ious)
+        assert np.mean(ious) >= IOU_MIN[cam] - IOU_GPU_SLACK, (cam, ious)
 
 
 @pytest.mark.gpu

@@ -13,10 +13,9 @@ Geometry (all vertices in their BODY frame, so the device only needs body poses)
   * every box geom of the table, bins and cubes (:43-125) as 12 triangles, the table legs
     (cylinders) as 16-gon prisms, each with its own material rgba;
   * the Panda's visual meshes (panda.xml:123-246, 134,888 triangles, far beyond what a batched
-    per-env rasterizer should carry) reduced per visual part, each part in its own material:
-    arm links as convex pieces (k-means clusters of ~6 cm, each the hull of <= 12 points), the
-    hand and fingers (the wrist camera's close-up) as vertex-clustered meshes (12 mm / 4 mm
-    cells, the file's winding kept).
+    per-env rasterizer should carry): all 57 visual parts decimated together under one budget of
+    ROBOT_TRIS triangles by quadric-error edge collapse (tools/qem.py), each part in its own
+    material, the hand and fingers' errors weighted by HAND_WEIGHT (the wrist camera's close-up).
 Segment ids (the mask-level parity channel): 0 sky, 1 floor, 2 table, 3/4/5 bins red/green/blue,
 6/7/8 cubes red/green/blue, 9 robot.
 """
@@ -34,11 +33,20 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import compile_model as CM  # noqa: E402
 
 MAX_HULL_VERTS = 96
-# robot geometry (robot-mask IoU against the full 134,888-triangle visual meshes,
-# tests/golden/robot_masks.npz, 8 states, 128 x 128): one hull per body gave 0.89 (overhead) /
-# 0.75 (wrist); convex pieces of ~7 cm per link part (<= 10 points) + clustered hand (20 mm) /
-# fingers (6 mm) give 0.92 / 0.97 with 2,033 robot triangles (was 1,956), inside the renderer's
-# LDS budget for two workgroups per CU (finer: 6 cm / 12 / 4 mm gave 0.94 / 0.98 with 2,967)
+# robot geometry (mean robot-mask IoU against the full 134,888-triangle
+# visual meshes, tests/golden/robot_masks.npz, 8 states, 128 x 128, overhead / wrist):
+#   one hull per body (r02)                                              0.89 / 0.75
+#   convex pieces per link part + clustered hand / fingers, 2,033 tris   0.92 / 0.97  (r03-r05)
+#   quadric-error collapse, one budget (tools/qem.py): 1,400 tris        0.951 / 0.969
+#                                                     1,600              0.962 / 0.975
+#                                                     1,800              0.973 / 0.977  <- kept
+#                                                     2,000              0.976 / 0.975
+#   hand / finger error weight at 1,800 tris: 30 -> 0.974 / 0.970, 100 -> 0.973 / 0.977 (kept);
+#   at 2,000: 1 -> 0.979 / 0.792 (the fingers collapse), 300 -> 0.967 / 0.977
+ROBOT_TRIS = 1800
+HAND_WEIGHT = 100.0
+# the r03-r05 reduction (robot_tris=0): convex pieces of ~7 cm per link part (<= 10 points), hand
+# clustered at 20 mm, fingers at 6 mm
 LINK_PIECE_SIZE = 0.07
 LINK_PIECE_VERTS = 10
 HAND_CELL = 0.02
@@ -167,7 +175,7 @@ def geom_to_body(v, pos, quat):
     return v @ R.T + np.asarray(pos, float)
 
 
-def build(robot_tris=None, hand_weight=1.0):
+def build(robot_tris=ROBOT_TRIS, hand_weight=HAND_WEIGHT):
     model = CM.compile_model()
     bodies = model["bodies"]
     bnames = [b["name"] for b in bodies]
