@@ -3164,10 +3164,11 @@ __device__ __attribute__((noinline)) void step_finish(const MMXState& S, int i) 
 #ifdef MMX_PHASE_CLOCK
 // Diagnostic build only: per FSM state of the env step (the state the step's action was planned
 // in), the sums over env steps of the shader cycles of each phase (STAT_T_IK .. STAT_T_END), of
-// the whole step, of the solver iterations / MuJoCo rows / contacts, and the env-step count
-// (tools/gpu_probe.py fsm_profile).  Lane 0 of each env adds with global atomics.
+// the whole step, of the solver iterations / MuJoCo rows / contacts, the whole step's constant-rate
+// wall clock (100 MHz ticks: the slot time an env step holds, and with FSMP_STEP the shader clock) and
+// the env-step count (tools/gpu_probe.py fsm_profile).  Lane 0 of each env adds with global atomics.
 enum { FSMP_PHASES = STAT_T_AUX3 - STAT_T_IK + 1, FSMP_STEP = FSMP_PHASES, FSMP_ITER, FSMP_NEFC, FSMP_NCON,
-       FSMP_COUNT, FSMP_N };
+       FSMP_RT, FSMP_COUNT, FSMP_N };
 #ifdef MMX_STEP_ONLY
 static __device__ double g_fsm_prof[11 * FSMP_N];  // (this build's copy is not read out)
 #else
@@ -3208,6 +3209,9 @@ MMX_STEP_SYM(mmx_env_step_kernel)(MMXState S, const float* action, int adim, int
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
       XSYNC();
     }
+#ifdef MMX_PHASE_CLOCK
+    const unsigned long long rt_step = wall_clock64();  // (the record load and the plan included)
+#endif
     step_begin(S, i, action, adim, expert);
     XSYNC();
 #ifdef MMX_PHASE_CLOCK
@@ -3239,6 +3243,7 @@ MMX_STEP_SYM(mmx_env_step_kernel)(MMXState S, const float* action, int adim, int
       double* g = g_fsm_prof + FSMP_N * min(max(fsm, 0), 10);
       atomicAdd(g + STAT_T_END - STAT_T_IK, (double)(g_E.stats[STAT_T_END] - snap[STAT_T_END - STAT_T_IK]));
       atomicAdd(g + FSMP_STEP, (double)(clk_now() - t_step));
+      atomicAdd(g + FSMP_RT, (double)(wall_clock64() - rt_step));
       atomicAdd(g + FSMP_COUNT, 1.0);
     }
 #endif

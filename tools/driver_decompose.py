@@ -38,6 +38,7 @@ def main(N=4096, warm=5, steps=20, windows=5, long_steps=512):
     buf = (C.c_double * (11 * nf))()
     L.mmx_fsm_profile.argtypes = [C.POINTER(C.c_double), C.c_int]
     P = 12  # phase fields before FSMP_STEP (tools/gpu_probe.py)
+    SLOTS = torch.cuda.get_device_properties(0).multi_processor_count * 12  # twelve envs per CU (128-row build)
     env = PickPlaceVecEnv(N, tasks="all", action_mode="abs_pos", reward_type="staged", randomize_objects=True,
                           autoreset=True, image_size=0)
     env.reset(seed=[_lib.episode_seed(42, i) for i in range(N)])
@@ -53,10 +54,14 @@ def main(N=4096, warm=5, steps=20, windows=5, long_steps=512):
         T = time.perf_counter() - t0
         L.mmx_fsm_profile(buf, 1)
         a = np.array(buf[:]).reshape(11, nf)
-        cnt, cyc = a[:, nf - 1], a[:, P]
+        cnt, cyc, rt = a[:, nf - 1], a[:, P], a[:, nf - 2]
         assert abs(cnt.sum() - N * n) < 0.5, (cnt.sum(), N * n)
         return {"env_steps": int(cnt.sum()), "seconds": T, "rate": cnt.sum() / T, "busy_cycles": float(cyc.sum()),
                 "cycles_per_env_step": float(cyc.sum() / cnt.sum()), "fill_cycles_per_s": float(cyc.sum() / T),
+                # absolute: the fraction of the window's slot-time (resident workgroup slots x wall time)
+                # spent inside env steps, from the constant 100 MHz clock; and the shader clock
+                "slot_occupancy": float(rt.sum() * 1e-8 / (T * SLOTS)),
+                "shader_clock_ghz": float(cyc.sum() / max(rt.sum(), 1.0) * 0.1),
                 "phase_env_steps": {FSM[s]: int(cnt[s]) for s in range(11) if cnt[s]},
                 "phase_cycles_per_env_step": {FSM[s]: float(cyc[s] / cnt[s]) for s in range(11) if cnt[s]}}
 
@@ -75,7 +80,9 @@ def main(N=4096, warm=5, steps=20, windows=5, long_steps=512):
     out["summary"] = {"median_window_rate": med["rate"], "stationary_rate": S["rate"],
                       "median_overhead_factor": med["overhead_factor"], "median_phase_mix_factor": med["phase_mix_factor"],
                       "mean_overhead_factor": float(np.mean([w["overhead_factor"] for w in ws])),
-                      "mean_phase_mix_factor": float(np.mean([w["phase_mix_factor"] for w in ws]))}
+                      "mean_phase_mix_factor": float(np.mean([w["phase_mix_factor"] for w in ws])),
+                      "stationary_slot_occupancy": S["slot_occupancy"],
+                      "mean_window_slot_occupancy": float(np.mean([w["slot_occupancy"] for w in ws]))}
     os.makedirs(os.path.join(REPO, "gpurun_out"), exist_ok=True)
     with open(os.path.join(REPO, "gpurun_out", "driver_decompose.json"), "w") as f:
         json.dump(out, f, indent=1)

@@ -168,7 +168,9 @@ def fsm_profile(N=4096, steps=160, warm=0):
                              "nefc_per_substep": a[s, P + 2] / (16 * n),
                              "ncon_per_substep": a[s, P + 3] / (16 * n)}
     allc = (a[:, P]).sum() / tot
-    out["all"] = {"env_steps": int(tot), "cycles_per_env_step": allc}
+    # shader clock over the env steps: s_memtime cycles / s_memrealtime seconds (100 MHz ticks)
+    out["all"] = {"env_steps": int(tot), "cycles_per_env_step": allc,
+                  "shader_clock_ghz": float(a[:, P].sum() / max(a[:, nf - 2].sum(), 1.0) * 0.1)}
     return out
 
 
