@@ -252,10 +252,10 @@ def binding_roof(pmc: dict | None, workload: str) -> dict | None:
     out = {"valu_insts_per_env_step": v.get("valu_insts_per_env_step"),
            "valu_issue_per_wave": v.get("active_inst_valu_per_wave_cycle"),
            "waves_per_simd": v.get("waves_per_simd"),
-           "valu_issue_per_simd": v.get("frac"),
+           "valu_issue_per_simd": v.get("valu_issue_per_simd"),
            "active_lane_fraction": v.get("active_lane_fraction"),
-           "lane_weighted_valu_issue_per_simd": (v["frac"] * v["active_lane_fraction"]
-                                                 if v.get("frac") and v.get("active_lane_fraction") else None),
+           "lane_weighted_valu_issue_per_simd": (v["valu_issue_per_simd"] * v["active_lane_fraction"]
+                                                 if v.get("valu_issue_per_simd") and v.get("active_lane_fraction") else None),
            "hbm_frac_note": "HBM frac <= ~0.2 by design while the efc working set stays in LDS (DESIGN §4)",
            "units": "SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (quad-cycles): instructions per quad-cycle"}
     cal_f = os.path.join(REPO, "profiles", "r05_valu_issue_calibration.json")
@@ -276,7 +276,7 @@ def binding_roof(pmc: dict | None, workload: str) -> dict | None:
         out["valu_issue_ceiling_per_wave"] = ceil_w
         out["valu_issue_ceiling_per_simd"] = ceil_s
         out["valu_issue_frac_of_ceiling"] = v["active_inst_valu_per_wave_cycle"] / ceil_w
-        out["valu_issue_simd_frac_of_ceiling"] = v["frac"] / ceil_s
+        out["valu_issue_simd_frac_of_ceiling"] = v["valu_issue_per_simd"] / ceil_s
         out["calibration"] = "profiles/r05_valu_issue_calibration.json (measured at 1-4 waves per SIMD, interpolated)"
     except (OSError, ValueError, KeyError, IndexError, TypeError, ZeroDivisionError):
         pass
@@ -481,12 +481,13 @@ def main():
         render = {"kernel": "mmx_render_kernel", "kernel_ms": med["render_ms"], "launches_per_step": rl,
                   "concurrent_with_step": overlap,
                   "envs_per_launch": r_envs, "image_size": S, "bytes_per_launch": rbytes,
-                  "bound": "valu", "hbm_achieved_GBs": r_achieved, "hbm_frac": r_achieved / HBM_PEAK_GBS,
+                  "bound": None if rpmc is None else rpmc.get("valu", {}).get("bound"),
+                  "hbm_achieved_GBs": r_achieved, "hbm_frac": r_achieved / HBM_PEAK_GBS,
                   "share_of_kernel_time": None if overlap else med["render_ms"] / (med["render_ms"] + kern_ms),
                   "pixels_per_s": rl * r_envs * 2 * S * S / (med["render_ms"] * 1e-3),
                   "valu": None if rpmc is None else rpmc.get("valu"), "isolated": isolated,
-                  "note": "HBM is not the render kernel's roof (it writes 4 B per pixel); VALU issue is "
-                          "(valu: SQ counters of tools/render_pmc.sh for this configuration)" +
+                  "note": "HBM is not the render kernel's roof (it writes 4 B per pixel); bound / valu: SQ counters "
+                          "of tools/gpu.sh render_pmc for this configuration against the VALU issue calibration" +
                           ("; concurrent with the next step's launch: kernel_ms / pixels_per_s / hbm are "
                            "per span on the render stream, isolated.forward_ms is the render alone" if overlap else "")}
     if rank == 0:

@@ -74,6 +74,30 @@ def extended_sq(prof: str, n_timed: int, config: dict, rnd: str) -> dict | None:
                         "per quad-cycle (profiles/r05_valu_issue_calibration.json)")}
 
 
+
+def valu_ceiling(waves_per_simd: float):
+    """What a SIMD (and one of its waves) can issue at this many resident waves per SIMD, in the units
+    of SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES: the calibration kernel's measured issue (8 independent FMA
+    chains per wave, profiles/r05_valu_issue_calibration.json) interpolated over 1-4 waves per SIMD."""
+    import numpy as np
+
+    cal = json.load(open(os.path.join(REPO, "profiles", "r05_valu_issue_calibration.json")))
+    rows = sorted((r["waves_per_simd"], r["sq_active_inst_valu_per_wave_quad_cycle"], r["sq_valu_per_simd_quad_cycle"])
+                  for r in cal["scalar_v_fma_f32"] if r["chains"] == 8)
+    w = [r[0] for r in rows]
+    return float(np.interp(waves_per_simd, w, [r[1] for r in rows])), float(np.interp(waves_per_simd, w, [r[2] for r in rows]))
+
+
+def valu_reading(per_wave: float, waves_per_simd: float) -> dict:
+    """VALU issue of the kernel against the calibrated ceiling: 'latency' below 0.6 of it."""
+    cw, cs = valu_ceiling(waves_per_simd)
+    frac = per_wave / cw
+    return {"valu_issue_per_wave": per_wave, "waves_per_simd": waves_per_simd, "valu_issue_per_simd": per_wave * waves_per_simd,
+            "issue_ceiling_per_wave": cw, "issue_ceiling_per_simd": cs, "frac_of_ceiling": frac,
+            "bound": "latency" if frac < 0.6 else "valu-issue",
+            "units": "SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (instructions per quad-cycle); ceiling: "
+                     "profiles/r05_valu_issue_calibration.json at the kernel's waves per SIMD"}
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--round", default="r03")
@@ -124,16 +148,13 @@ def main():
         "hbm_bytes_per_dispatch": hbm, "hbm_bytes_per_env_step": hbm / unit,
         "fetch_bytes_per_env_step": 2.0 * fetch * 1024.0 / unit, "write_bytes_per_env_step": write * 1024.0 / unit,
         "sq_per_dispatch": sq,
-        "valu": {"bound": "valu-issue", "active_inst_valu_per_wave_cycle": per_wave, "waves_per_simd": waves_per_simd,
-                 "frac": per_wave * waves_per_simd,
+        "valu": {**valu_reading(per_wave, waves_per_simd), "active_inst_valu_per_wave_cycle": per_wave,
                  "valu_insts_per_env_step": sq["SQ_INSTS_VALU"] / unit,
                  "lds_bank_conflict_per_lds_active": sq["SQ_LDS_BANK_CONFLICT"] / max(sq["SQ_ACTIVE_INST_LDS"], 1.0),
                  "wait_any_per_wave_cycle": sq["SQ_WAIT_ANY"] / sq["SQ_WAVE_CYCLES"],
                  # mean fraction of the 64 lanes active per VALU instruction (rocprofiler's
                  # AvgNumActiveThreads / 64 for gfx950); None when the pass is missing
-                 "active_lane_fraction": lane_util,
-                 "note": "SIMD VALU issue utilisation = SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (per wave, same "
-                         "quad-cycle units) x resident waves per SIMD; 1.0 = the VALU issues every cycle"},
+                 "active_lane_fraction": lane_util},
         "note": "FETCH_SIZE x2 (gfx950 wide-read tally, MI355X_MICROARCH.md §HBM); dword-per-lane reads uncalibrated; "
                 "Infinity-Cache hits are counted by these memory-side counters",
     }

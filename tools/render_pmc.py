@@ -9,6 +9,30 @@ import os
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+
+def valu_ceiling(waves_per_simd: float):
+    """What a SIMD (and one of its waves) can issue at this many resident waves per SIMD, in the units
+    of SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES: the calibration kernel's measured issue (8 independent FMA
+    chains per wave, profiles/r05_valu_issue_calibration.json) interpolated over 1-4 waves per SIMD."""
+    import numpy as np
+
+    cal = json.load(open(os.path.join(REPO, "profiles", "r05_valu_issue_calibration.json")))
+    rows = sorted((r["waves_per_simd"], r["sq_active_inst_valu_per_wave_quad_cycle"], r["sq_valu_per_simd_quad_cycle"])
+                  for r in cal["scalar_v_fma_f32"] if r["chains"] == 8)
+    w = [r[0] for r in rows]
+    return float(np.interp(waves_per_simd, w, [r[1] for r in rows])), float(np.interp(waves_per_simd, w, [r[2] for r in rows]))
+
+
+def valu_reading(per_wave: float, waves_per_simd: float) -> dict:
+    """VALU issue of the kernel against the calibrated ceiling: 'latency' below 0.6 of it."""
+    cw, cs = valu_ceiling(waves_per_simd)
+    frac = per_wave / cw
+    return {"valu_issue_per_wave": per_wave, "waves_per_simd": waves_per_simd, "valu_issue_per_simd": per_wave * waves_per_simd,
+            "issue_ceiling_per_wave": cw, "issue_ceiling_per_simd": cs, "frac_of_ceiling": frac,
+            "bound": "latency" if frac < 0.6 else "valu-issue",
+            "units": "SQ_ACTIVE_INST_VALU / SQ_WAVE_CYCLES (instructions per quad-cycle); ceiling: "
+                     "profiles/r05_valu_issue_calibration.json at the kernel's waves per SIMD"}
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--round", default="r03")
@@ -44,9 +68,8 @@ def main():
     # what bench.py's C5 line cites (its `render.valu`), tagged with the configuration measured
     waves_per_simd = 4  # 512-lane workgroups (8 waves), two per CU (LDS), 4 SIMDs
     res["config"] = {"workload": "render", "envs_per_gpu": 8192, "env_steps_per_launch": 1, "lanes": a.lanes}
-    res["valu"] = {"bound": "valu-issue", "valu_insts_per_px": res["valu_insts_per_px"],
+    res["valu"] = {**valu_reading(res["valu_issue_per_wave_cycle"], waves_per_simd), "valu_insts_per_px": res["valu_insts_per_px"],
                    "active_inst_valu_per_wave_cycle": res["valu_issue_per_wave_cycle"],
-                   "waves_per_simd": waves_per_simd, "frac": res["valu_issue_per_wave_cycle"] * waves_per_simd,
                    "wait_any_per_wave_cycle": out.get("SQ_WAIT_ANY", 0) / max(out.get("SQ_WAVE_CYCLES", 1), 1),
                    "source": f"profiles/{a.round}_render_pmc.json"}
     dst = os.path.join(REPO, "profiles", f"{a.round}_render_pmc.json")
