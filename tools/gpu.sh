@@ -17,7 +17,8 @@
 #   dataset:S        f2 dataset collection + LeRobot writer, 8192 envs x 8192 episodes, S px
 #   ab               interleaved A/B of $LIBS against the product (tools/ab.sh; ROUNDS, STEPS, PMC, TESTS)
 #   occupancy        C3 env steps/s with the envs per CU lowered by dynamic LDS per workgroup (MMX_LDS_PAD;
-#                    residency per LDS size: profiles/r05_lds_residency.json, 14,080 B = 11 per CU)
+#                    1,280-byte blocks, profiles/r05_lds_residency.json: 12,640 B = 12 per CU; pads 2560 /
+#                    6400 / 8960 / 20480 B -> 10 / 8 / 7 / 4 per CU)
 # Env: R (round tag, default r06), MMX_LIB_PATH (a library other than the product for every recipe).
 set -o pipefail
 cd ${GRAFT_REPO_ROOT:-$(pwd)}; ROOT=$(pwd); mkdir -p gpurun_out
