@@ -199,7 +199,23 @@ static_assert(COL_CON % 4 == 0 && COL_WORK % 4 == 0, "16-byte aligned collision 
 static_assert(COL_WORK + COL_PLANES * COL_POLY <= SCR_FLOATS, "box-box polygons exceed the scratch region");
 static_assert(MMX_CAND_CAP <= COL_LIST && MMX_NPAIR < 4096, "collision scratch layout");
 
-#define SCR_DYN COL_WORK           // RNE frc + inertia [12][16], subtree force [12][6] (264), then:
+// The 192-row build (one env per CU quarter, C2's batches) gives each env a second wave, the
+// "helper": it runs each substep's dynamics (RNE, CRBA, smooth forces) while the env's wave runs the
+// collision, both after the kinematics (mj_step_wave).  Its scratch then sits past everything the
+// collision uses (the 192-row scratch region has the room); the 128-row build runs the phases in turn
+// on one wave and keeps the dynamics scratch in the narrowphase work space.
+#ifndef MMX_STEP_HELPER
+#define MMX_STEP_HELPER (MMX_LDSEFC == 192)
+#endif
+#if MMX_STEP_HELPER
+#define COL_END (COL_WORK + EPA_SCRATCH_FLOATS)  // the collision's scratch ends here (asserted below)
+static_assert(COL_WORK + COL_PLANES * COL_POLY <= COL_END && COL_WORK + MMX_MAXCON * CL_F <= COL_END,
+              "the narrowphase work space exceeds COL_END");
+#define SCR_DYN ((COL_END + 3) & ~3)
+#else
+#define SCR_DYN COL_WORK
+#endif
+// SCR_DYN: RNE frc + inertia [12][16], subtree force [12][6] (264), then:
 #define SCR_IC (SCR_DYN + 272)     // composite inertias [12][10]
 #define SCR_AF (SCR_IC + 120)      // actuator forces [8]
 #define SCR_BIAS (SCR_AF + 8)      // RNE bias force of the arm dofs [9]
@@ -2531,10 +2547,17 @@ DEV void mj_step_wave(int max_iter, float tol, EnvSh& E, float* con_dst) {
   CLK_DECL;
   kinematics_wave(E);
   CLK(stats, STAT_T_KIN);
+#if MMX_STEP_HELPER
+  __syncthreads();  // the kinematics are in LDS: the helper wave runs the dynamics beside the collision
+#else
   dynamics_wave(E);
   CLK(stats, STAT_T_DYN);
+#endif
   collide_wave(E, false);
   CLK(stats, STAT_T_COL);
+#if MMX_STEP_HELPER
+  __syncthreads();  // the helper's dynamics are in LDS
+#endif
   if (con_dst) store_contacts(con_dst, E);  // before the row build reuses contact fields
   float mu[RPL];  // the lane's rows' mu (LANE + 64 q), from the row build to the solver
   make_constraints_wave(E, mu);
@@ -3190,20 +3213,38 @@ extern "C" int mmx_fsm_profile_fields() { return FSMP_N; }
 // (C2's 1024 envs are four per CU: one wave per SIMD, whose spare registers hold what 2 waves per SIMD
 // saved to scratch; C2 +1.1 %, profiles/r06_ab_c2_l192_waves.json)
 #ifndef MMX_STEP_WAVES
-#define MMX_STEP_WAVES (MMX_LDSEFC == 128 ? 3 : 1)
+#define MMX_STEP_WAVES (MMX_LDSEFC == 128 ? 3 : (MMX_STEP_HELPER ? 2 : 1))
 #endif
+#define MMX_STEP_THREADS (MMX_STEP_HELPER ? 128 : 64)  // the env's wave (+ the helper wave)
 #ifndef MMX_STEP_SUFFIX
 #define MMX_STEP_SUFFIX
 #endif
 #define MMX_CAT2_(a, b) a##b
 #define MMX_CAT_(a, b) MMX_CAT2_(a, b)
 #define MMX_STEP_SYM(name) MMX_CAT_(name, MMX_STEP_SUFFIX)
-extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MMX_STEP_WAVES, MMX_STEP_WAVES)))
+extern "C" __global__ void __launch_bounds__(MMX_STEP_THREADS) __attribute__((amdgpu_waves_per_eu(MMX_STEP_WAVES, MMX_STEP_WAVES)))
 MMX_STEP_SYM(mmx_env_step_kernel)(MMXState S, const float* action, int adim, int expert, int base, int nsteps,
                                   const int* order) {
   // order (optional): the launch's envs in dispatch order, the grasp-carrying ones first (mmx_order_kernel)
   const int i = order ? order[blockIdx.x] : base + blockIdx.x;
   if (i >= S.N) return;
+#if MMX_STEP_HELPER
+  if (threadIdx.x >= 64) {  // the helper wave: the same workgroup barriers as the env's wave below
+    for (int k = 0; k < nsteps; k++) {
+      if (k) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        XSYNC();
+      }
+      XSYNC();  // step_begin's record load
+      for (int sub = 0; sub < MMX_NSUBSTEP; sub++) {
+        __syncthreads();  // the substep's kinematics (mj_step_wave)
+        dynamics_wave(g_E);
+        __syncthreads();  // -> the collision's end
+      }
+    }
+    return;
+  }
+#endif
   for (int k = 0; k < nsteps; k++) {
     if (k) {  // the previous step's record stores complete before this step reloads it
       __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
@@ -3489,7 +3530,7 @@ extern "C" hipError_t MMX_STEP_SYM(mmx_launch_step)(const MMXState* S, const flo
                                                     int count, int nsteps, hipStream_t st, const int* order) {
   if (count <= 0 || nsteps <= 0) return hipSuccess;
   if (nsteps > 1 && !expert) return hipErrorInvalidValue;  // host actions: one env step per launch
-  hipLaunchKernelGGL(MMX_STEP_SYM(mmx_env_step_kernel), dim3(count), dim3(64), step_lds_pad(), st, *S, action, adim, expert, base,
+  hipLaunchKernelGGL(MMX_STEP_SYM(mmx_env_step_kernel), dim3(count), dim3(MMX_STEP_THREADS), step_lds_pad(), st, *S, action, adim, expert, base,
                      nsteps, order);
   return hipGetLastError();
 }
