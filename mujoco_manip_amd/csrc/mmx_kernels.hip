@@ -200,10 +200,11 @@ static_assert(COL_WORK + COL_PLANES * COL_POLY <= SCR_FLOATS, "box-box polygons 
 static_assert(MMX_CAND_CAP <= COL_LIST && MMX_NPAIR < 4096, "collision scratch layout");
 
 // The 192-row build (one env per CU quarter, C2's batches) gives each env a second wave, the
-// "helper": it runs each substep's dynamics (RNE, CRBA, smooth forces) while the env's wave runs the
-// collision, both after the kinematics (mj_step_wave).  Its scratch then sits past everything the
-// collision uses (the 192-row scratch region has the room); the 128-row build runs the phases in turn
-// on one wave and keeps the dynamics scratch in the narrowphase work space.
+// "helper": per substep it runs the IK beside the env wave's kinematics, then the dynamics (RNE, CRBA,
+// smooth forces) beside the broadphase, then the GJK / EPA pairs beside the plane and box-box pairs
+// (mj_step_wave).  Its scratch (IK system, dynamics, EPA polytope, one after the other) sits past
+// everything the env wave's collision uses (the 192-row scratch region has the room); the 128-row build
+// runs the phases in turn on one wave and keeps them in the narrowphase work space.
 #ifndef MMX_STEP_HELPER
 #define MMX_STEP_HELPER (MMX_LDSEFC == 192)
 #endif
@@ -212,8 +213,12 @@ static_assert(MMX_CAND_CAP <= COL_LIST && MMX_NPAIR < 4096, "collision scratch l
 static_assert(COL_WORK + COL_PLANES * COL_POLY <= COL_END && COL_WORK + MMX_MAXCON * CL_F <= COL_END,
               "the narrowphase work space exceeds COL_END");
 #define SCR_DYN ((COL_END + 3) & ~3)
+#define SCR_IKW SCR_DYN  // the IK system [72] (before the dynamics, on the helper)
+#define SCR_EPA SCR_DYN  // the helper's EPA polytope (after the dynamics)
 #else
 #define SCR_DYN COL_WORK
+#define SCR_IKW 0
+#define SCR_EPA COL_EPA
 #endif
 // SCR_DYN: RNE frc + inertia [12][16], subtree force [12][6] (264), then:
 #define SCR_IC (SCR_DYN + 272)     // composite inertias [12][10]
@@ -221,7 +226,8 @@ static_assert(COL_WORK + COL_PLANES * COL_POLY <= COL_END && COL_WORK + MMX_MAXC
 #define SCR_BIAS (SCR_AF + 8)      // RNE bias force of the arm dofs [9]
 #define SCR_OBS COL_WORK           // observation (step end after its contact scan, reset, forward)
 #define SCR_ACT (COL_WORK + 96)    // raw action of the step (lane 0, before the substeps)
-static_assert(SCR_BIAS + 9 <= SCR_FLOATS && SCR_OBS + MMX_NOBS <= SCR_ACT && SCR_ACT + 12 <= SCR_FLOATS,
+static_assert(SCR_BIAS + 9 <= SCR_FLOATS && SCR_OBS + MMX_NOBS <= SCR_ACT && SCR_ACT + 12 <= SCR_FLOATS &&
+                  SCR_EPA + EPA_SCRATCH_FLOATS <= SCR_FLOATS && SCR_IKW + 72 <= SCR_FLOATS,
               "scratch layout");
 DEV float* scr_of(EnvSh& E) { return reinterpret_cast<float*>(&E.J); }
 DEV const float* scr_of(const EnvSh& E) { return reinterpret_cast<const float*>(&E.J); }
@@ -1114,7 +1120,7 @@ DEV void collide_pairs(EnvSh& E, bool only_ro, int which) {
       cand_unpack(cand[n0 + n1 + k], p, g1, g2);
       const Geom A = geom_lds(gx, g1), B = geom_lds(gx, g2);
       WaveSink cs(&E, p, !only_ro, g1, g2);
-      convex_convex(cs, A, B, scr + COL_EPA);
+      convex_convex(cs, A, B, scr + SCR_EPA);
     }
     SYNC();
     PROBE(5, stats, STAT_T_AUX2);
@@ -2490,7 +2496,7 @@ DEV void ik_lane0(EnvSh& E) {
 // (register Cholesky), dq = b + J' A^{-1} (e - J b) with b the null-space pull toward home
 // (= J' A^{-1} e + (I - J' A^{-1} J) b of controller.py:111-124).  Scratch: E.J (free here).
 DEV void ik_wave(EnvSh& E) {
-  float* W = scr_of(E);  // J [6][8] at 0, b [8] at 48, e [8] at 56, u [8] at 64
+  float* W = scr_of(E) + SCR_IKW;  // J [6][8] at 0, b [8] at 48, e [8] at 56, u [8] at 64
   const V3 ee = V3{kin_get(E, KIN_HAND_POS), kin_get(E, KIN_HAND_POS + 1), kin_get(E, KIN_HAND_POS + 2)};
   if (LANE < 7) {
     const int d = LANE;
@@ -2545,19 +2551,25 @@ DEV void ik_wave(EnvSh& E) {
 DEV void mj_step_wave(int max_iter, float tol, EnvSh& E, float* con_dst) {
   float* stats = E.stats;
   CLK_DECL;
+#if MMX_STEP_HELPER
+  // the env wave and the helper wave (the kernel's helper loop mirrors these workgroup barriers)
+  __syncthreads();  // C: the previous substep's state is in LDS; the helper runs the IK
   kinematics_wave(E);
   CLK(stats, STAT_T_KIN);
-#if MMX_STEP_HELPER
-  __syncthreads();  // the kinematics are in LDS: the helper wave runs the dynamics beside the collision
+  __syncthreads();  // A: the kinematics; the helper runs the dynamics beside the broadphase
+  collide_prune(E, false);
+  __syncthreads();  // P: the class lists (and the dynamics); the helper takes the GJK / EPA pairs
+  collide_pairs(E, false, 1);
+  __syncthreads();  // Q: the helper's contacts (the rank sort orders them by key)
+  collide_sort(E);
 #else
+  kinematics_wave(E);
+  CLK(stats, STAT_T_KIN);
   dynamics_wave(E);
   CLK(stats, STAT_T_DYN);
-#endif
   collide_wave(E, false);
-  CLK(stats, STAT_T_COL);
-#if MMX_STEP_HELPER
-  __syncthreads();  // the helper's dynamics are in LDS
 #endif
+  CLK(stats, STAT_T_COL);
   if (con_dst) store_contacts(con_dst, E);  // before the row build reuses contact fields
   float mu[RPL];  // the lane's rows' mu (LANE + 64 q), from the row build to the solver
   make_constraints_wave(E, mu);
@@ -3152,7 +3164,9 @@ __device__ __attribute__((noinline)) void substep(int max_iter, float tol, float
   EnvSh& E = g_E;
   float* stats = E.stats;
   CLK_DECL;
+#if !MMX_STEP_HELPER  // (the helper wave's, beside the kinematics: mj_step_wave)
   ik_wave(E);  // IK on the kinematics left by the previous position stage
+#endif
   CLK(stats, STAT_T_IK);
   mj_step_wave(max_iter, tol, E, con_dst);
 }
@@ -3236,10 +3250,14 @@ MMX_STEP_SYM(mmx_env_step_kernel)(MMXState S, const float* action, int adim, int
         XSYNC();
       }
       XSYNC();  // step_begin's record load
-      for (int sub = 0; sub < MMX_NSUBSTEP; sub++) {
-        __syncthreads();  // the substep's kinematics (mj_step_wave)
+      for (int sub = 0; sub < MMX_NSUBSTEP; sub++) {  // mj_step_wave's barriers C, A, P, Q
+        __syncthreads();
+        ik_wave(g_E);
+        __syncthreads();
         dynamics_wave(g_E);
-        __syncthreads();  // -> the collision's end
+        __syncthreads();
+        collide_pairs(g_E, false, 2);
+        __syncthreads();
       }
     }
     return;
