@@ -318,9 +318,9 @@ def main():
     # (obj_red, bin_red), keyframe start, no randomisation), c5 (c3 settings + 2 x 128^2 RGB
     # cameras per env step, 8192 envs per GPU as in the 65536-env / 8-GPU config)
     ap.add_argument("--workload", default="c3", choices=("c2", "c3", "c5"))
-    # env-step kernel layout (mmx_set_step_rows, bit-identical results): 0 = the library's default (128
-    # LDS rows, twelve envs per CU); C2's 1024 envs are four per CU, where the 192-row layout at one wave
-    # per SIMD is faster per env, so the c2 workload uses it
+    # env-step kernel layout (mmx_set_step_rows, bit-identical results): 0 = the library's choice from
+    # the batch size (192 LDS rows with a helper wave per env up to four envs per CU, e.g. C2's 1024;
+    # 128 rows, twelve per CU, above: DESIGN §2); 128 / 192 force one for A/B runs
     ap.add_argument("--step-rows", type=int, default=0, choices=(0, 128, 192))
     args = ap.parse_args()
     if args.workload == "c5":
@@ -329,8 +329,6 @@ def main():
             args.envs_per_gpu = 8192
     if args.workload == "c2" and args.envs_per_gpu == 4096:
         args.envs_per_gpu = 1024
-    if args.workload == "c2" and args.step_rows == 0:
-        args.step_rows = 192
 
     from mujoco_manip_amd.shard import dist_env, env_stats_record, gather_env_stats, shard_seeds, summarize_env_stats
 

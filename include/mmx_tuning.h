@@ -16,10 +16,11 @@ extern "C" {
 #endif
 
 /* Constraint rows the env-step kernel (mmx_step, mmx_rollout_expert) keeps in LDS: 128 (twelve envs
- * per CU, the default: the fastest layout once the batch fills the GPU's workgroup slots, C3 / C5 /
- * dataset generation) or 192 (four per CU, one wave per SIMD with its whole register file: faster per
- * env, for batches of at most four envs per CU, e.g. C2's 1024).  Env MMX_STEP_ROWS overrides at
- * create.  The rows past the LDS ones live in the env's HBM overflow block; the two layouts are
+ * per CU: the fastest layout once the batch fills the GPU's workgroup slots, C3 / C5 / dataset
+ * generation) or 192 (four envs per CU, each with a second "helper" wave that runs its IK, dynamics and
+ * GJK / EPA pairs beside the env wave's kinematics, broadphase and box pairs: faster per env, for
+ * batches of at most four envs per CU, e.g. C2's 1024).  mmx_create picks by the batch size (192 up to
+ * four envs per CU); env MMX_STEP_ROWS overrides at create.  The rows past the LDS ones live in the env's HBM overflow block; the two layouts are
  * bit-identical (a performance choice only).  MMX_EINVAL for any other value. */
 int mmx_set_step_rows(mmx_sim* sim, int32_t rows);
 int mmx_step_rows(const mmx_sim* sim);

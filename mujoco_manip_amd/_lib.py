@@ -409,7 +409,8 @@ class Sim:
 
     @property
     def step_rows(self) -> int:
-        """Constraint rows the env-step kernel keeps in LDS (128: eleven envs per CU; 192: eight)."""
+        """Constraint rows the env-step kernel keeps in LDS (128: twelve envs per CU; 192: four, each
+        with a helper wave; chosen at create from the batch size)."""
         return int(self.L.mmx_step_rows(self.ptr))
 
     @step_rows.setter

@@ -64,9 +64,9 @@ struct mmx_sim {
   // overrides): with the staggered lanes 32 beat 16 by 0.5 % and 8 lost 2.7 % on 512-step C3 windows
   // (profiles/r06_sweep_launch_shape.json)
   int fuse = 32;
-  // constraint rows the env-step kernel keeps in LDS: 128 (eleven envs per CU, the default) or 192
-  // (eight per CU, mmx_step_l192.hip: faster when the batch leaves CU slots empty; mmx_set_step_rows,
-  // MMX_STEP_ROWS)
+  // constraint rows the env-step kernel keeps in LDS: 128 (twelve envs per CU) or 192 (four per CU, each
+  // with a helper wave, mmx_step_l192.hip: faster when the batch leaves CU slots empty); chosen at create
+  // from the batch size, mmx_set_step_rows / MMX_STEP_ROWS override
   int step_rows = 128;
   // env steps launched longest first (mmx_order_kernel; mmx_set_step_order, MMX_STEP_ORDER=0 at
   // create turns it off): the launch's order only, never its results
@@ -365,7 +365,12 @@ int mmx_create(const mmx_config* cfg, mmx_sim** out) {
   int lanes = std::min(N / 1024, 4);
   if (const char* v = std::getenv("MMX_STREAMS")) lanes = std::atoi(v);
   if (const char* v = std::getenv("MMX_FUSE")) sim->fuse = std::max(1, std::atoi(v));
-  sim->step_rows = 128;
+  // the layout: 192 rows (one env wave + its helper wave, four envs per CU) while the batch fits the
+  // chip at four per CU, where each env's own speed counts (C2's 1024 envs: 1.52 M vs 1.29 M env
+  // steps/s); 128 rows (twelve per CU) for larger batches, where slots count
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, cfg->device) != hipSuccess) cus = 0;
+  sim->step_rows = cus > 0 && N <= 4 * cus ? 192 : 128;
   if (const char* v = std::getenv("MMX_STEP_ROWS")) {
     const int r = std::atoi(v);
     if (r == 128 || r == 192) sim->step_rows = r;

@@ -154,7 +154,7 @@ struct EnvSh {
 static __shared__ EnvSh g_E;
 // twelve workgroups (envs) per CU share its 160 KiB of LDS, allocated in 1,280-byte blocks (measured:
 // tools/calib/lds_occ.hip, profiles/r05_lds_residency.json): the occupancy the kernel is tuned for (r06;
-// r05: eleven; with 192 LDS rows, MMX_LDSEFC=192, eight).  Twelve waves are three per SIMD, the
+// r05: eleven; with 192 LDS rows, MMX_LDSEFC=192, four, each with a helper wave).  Twelve waves are three per SIMD, the
 // 168-VGPR budget of amdgpu_waves_per_eu(3).
 static_assert(MMX_LDSEFC != 128 || (sizeof(EnvSh) + 1279) / 1280 * 1280 * 12 <= 160 * 1024,
               "EnvSh no longer fits 12 envs per CU");

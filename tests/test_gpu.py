@@ -87,22 +87,26 @@ def test_physics_parity_one_substep(margin):  # L1: fp32 GPU vs fp64 oracle, con
 
 
 def test_step_layout_api():
-    """mmx_set_step_rows / mmx_step_rows: 128 rows (eleven envs per CU) by default, with or without
-    cameras, 192 (eight) on request, anything else rejected."""
+    """mmx_set_step_rows / mmx_step_rows: by default 192 rows (four envs per CU, each with a helper
+    wave) while the batch fits four per CU, 128 (twelve per CU) above, with or without cameras; either
+    on request, anything else rejected."""
     from mujoco_manip_amd import _lib
 
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
     a = _lib.Sim(8, action_mode="abs_pos", image_size=0)
     b = _lib.Sim(8, action_mode="abs_pos", image_size=32)
+    c = _lib.Sim(4 * cus + 1, action_mode="abs_pos", image_size=0)
     try:
-        assert a.step_rows == 128 and b.step_rows == 128
-        a.step_rows = 192
-        assert a.step_rows == 192
+        assert a.step_rows == 192 and b.step_rows == 192 and c.step_rows == 128
+        a.step_rows = 128
+        assert a.step_rows == 128
         with pytest.raises(RuntimeError):
             a.step_rows = 100
-        assert a.step_rows == 192
+        assert a.step_rows == 128
     finally:
         a.close()
         b.close()
+        c.close()
 
 
 def test_step_order_bit_identical(margin, monkeypatch):
@@ -145,8 +149,10 @@ def test_step_order_bit_identical(margin, monkeypatch):
 
 
 def test_step_layouts_agree(margin):
-    """The two env-step kernel layouts (128 LDS rows + HBM overflow at eleven envs per CU; 192 LDS rows
-    at eight) are a performance choice only: 1024 C3 envs in lockstep through their approach and grasp
+    """The two env-step kernel layouts (128 LDS rows + HBM overflow at twelve envs per CU; 192 LDS rows
+    at four, each env with a helper wave running its IK, dynamics and GJK / EPA pairs beside the env
+    wave's kinematics, broadphase and box pairs) are a performance choice only: 1024 C3 envs in lockstep
+    through their approach and grasp
     phases, where the contact piles put rows past 128 into the overflow block of the first layout
     only, end every one of 60 env steps bit-identical (the Hessian pass assigns each row group to the
     same MFMA accumulator whichever address space holds it)."""

@@ -120,7 +120,8 @@ def _oracle_run_episode_uncached(seed, pool):
 def test_c3_episodes_match_oracle(margin, rows):
     """SURVEY §8d L2 over 48 C3 episodes (episode seeds SeedSequence(42), all 9 tasks): success
     flag and placement equal, episode length within +-2 env steps, final cube within 1 cm; with both
-    env-step kernel layouts (128 LDS rows / eleven envs per CU, 192 / eight: mmx_set_step_rows)."""
+    env-step kernel layouts (128 LDS rows / twelve envs per CU, 192 / four with helper waves:
+    mmx_set_step_rows)."""
     from mujoco_manip_amd import _lib
     from mujoco_manip_amd.constants import BINS, OBJECTS, TASK_SETS
 

@@ -1,5 +1,6 @@
 """Collision candidate tests with test-only builds (_build.TEST_VARIANTS), each run in a child process
-because the binding loads one library per process.
+because the binding loads one library per process.  The test builds recompile the 128-row kernel only
+(their 192-row kernel is the product's), so the children pin the 128-row layout (MMX_STEP_ROWS).
 
 * Contact-overflow KAT: more sphere-test survivors than the candidate list holds must reach
   env_error as ERR_CON_OVERFLOW, whichever substep of the env step overflowed (the flag is sticky from
@@ -42,7 +43,8 @@ def test_candidate_list_overflow_reaches_env_error():
         pytest.skip("needs an MI355X")
     lib = os.path.join(REPO, "mujoco_manip_amd", "libmmx_col4.so")
     assert os.path.exists(lib), "test build missing: run __graft_entry__.build()"
-    r = subprocess.run([sys.executable, "-c", CHILD, REPO], env=dict(os.environ, MMX_LIB_PATH=lib), capture_output=True,
+    r = subprocess.run([sys.executable, "-c", CHILD, REPO], env=dict(os.environ, MMX_LIB_PATH=lib, MMX_STEP_ROWS="128"),
+                       capture_output=True,
                        text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("OVERFLOW_ENVS")][0].split()
@@ -107,7 +109,7 @@ def test_broadphase_list_equals_full_prune():
     for lib in ("libmmx.so", "libmmx_nolist.so"):
         path = os.path.join(REPO, "mujoco_manip_amd", lib)
         assert os.path.exists(path), "test build missing: run __graft_entry__.build()"
-        r = subprocess.run([sys.executable, "-c", CHILD_DIGEST, REPO], env=dict(os.environ, MMX_LIB_PATH=path),
+        r = subprocess.run([sys.executable, "-c", CHILD_DIGEST, REPO], env=dict(os.environ, MMX_LIB_PATH=path, MMX_STEP_ROWS="128"),
                            capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
         lines = {ln.split()[0]: ln.split()[1:] for ln in r.stdout.splitlines() if ln.startswith(("DIGESTS", "PHASES"))}
