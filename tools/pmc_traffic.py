@@ -133,10 +133,12 @@ def main():
     if os.path.isdir(lanes_dir):
         ln = timed_mean(per_dispatch(lanes_dir, ["SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU"]), n_timed)
         lane_util = ln["SQ_THREAD_CYCLES_VALU"] / max(64.0 * ln["SQ_ACTIVE_INST_VALU"], 1.0)
-    # resident one-wave workgroups (envs) per SIMD: at most 12 per CU since r06 (12,640 B of LDS per
-    # env in 1,280-byte blocks; r05: 11)
-    per_cu = float(os.environ.get("MMX_ENVS_PER_CU", "12"))
-    waves_per_simd = min(per_cu * 256.0, float(line["config"]["envs_per_gpu"])) / 1024.0
+    # resident waves per SIMD: the 128-row layout runs one wave per env, at most 12 envs per CU (12,640 B
+    # of LDS per env in 1,280-byte blocks; r05: 11); the 192-row layout two (the env wave and its helper),
+    # at most 4 envs per CU
+    helper = int(line["config"].get("step_kernel_lds_rows", 128)) == 192
+    per_cu = float(os.environ.get("MMX_ENVS_PER_CU", "4" if helper else "12"))
+    waves_per_simd = min(per_cu * 256.0, float(line["config"]["envs_per_gpu"])) * (2.0 if helper else 1.0) / 1024.0
     per_wave = sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_WAVE_CYCLES"]
     hbm = 2.0 * fetch * 1024.0 + write * 1024.0
     rec = {
