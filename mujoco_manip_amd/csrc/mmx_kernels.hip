@@ -3223,9 +3223,9 @@ extern "C" int mmx_fsm_profile_fields() { return FSMP_N; }
 #endif
 
 // waves per SIMD the step kernel's register allocation is made for: 3 for the 128-row layout (168
-// VGPRs: twelve envs per CU); 1 for the 192-row layout, the one for batches that leave CU slots empty
-// (C2's 1024 envs are four per CU: one wave per SIMD, whose spare registers hold what 2 waves per SIMD
-// saved to scratch; C2 +1.1 %, profiles/r06_ab_c2_l192_waves.json)
+// VGPRs: twelve envs per CU); 2 for the 192-row layout, the one for batches that leave CU slots empty
+// (C2's 1024 envs are four per CU, each an env wave and its helper wave: eight waves per CU, 248 VGPRs;
+// C2 1.29 -> 1.52 M, profiles/r06_ab_c2_helper.json; without the helper it ran one wave per SIMD)
 #ifndef MMX_STEP_WAVES
 #define MMX_STEP_WAVES (MMX_LDSEFC == 128 ? 3 : (MMX_STEP_HELPER ? 2 : 1))
 #endif
@@ -3476,8 +3476,8 @@ extern "C" __global__ void __launch_bounds__(QWG) mmx_queue_kernel(MMXState S, M
 }
 
 // Dispatch order of an env range for the step kernel, longest first.  An env step's cycles follow its
-// FSM phase (profiles/archive/r05_fsm_profile.json, cycles per env step): lift / move to bin / lower to bin
-// ~2.35 M, close gripper / settle ~2.0 M, release / retreat ~1.63 M, the rest ~1.3-1.42 M.  A counting
+// FSM phase (profiles/r06_fsm_profile.json, cycles per env step at twelve per CU): lift / move to bin /
+// lower to bin ~2.5 M, close gripper / settle ~2.2 M, release / retreat ~1.7 M, the rest ~1.4-1.5 M.  A counting
 // sort over those four classes (refined by rows, below) puts the long ones at the front of order[],
 // so the launch's last workgroups are short ones (C3 +2.0 %, C5 +3.8 %).  One workgroup of any size (a single
 // wave beside running step launches: it then fits a CU the step kernel fills); the order within a
